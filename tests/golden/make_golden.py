@@ -1,0 +1,577 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under ``tests/golden/`` by running the REFERENCE itself.
+
+Run in the build container only (it needs ``/root/reference``; it refuses to run without it, so
+it is inert on the GPU box):
+
+    python tests/golden/make_golden.py
+
+How the reference is loaded:
+  * ``/root/reference`` goes on ``sys.path`` with bytecode writing disabled (read-only tree).
+  * ``torchvision`` is absent from this image.  The reference imports it at module top level
+    only; a stub module is installed in ``sys.modules`` that carries NO arithmetic:
+    ``torchvision.ops.nms`` is bound to the reference's own ``operators.iou_utils.nms`` called
+    with ``top_k = n`` (the NMS parity anchor named in SURVEY.md §8(c)).
+  * Networks are never constructed (their constructors fetch pretrained weights); prior
+    generators are called as unbound methods on a dummy ``self``.
+  * Per-image matching intermediates (locals of the criterion ``forward``) are captured with
+    ``sys.settrace`` on the criterion's own code object — the reference's own values, not a
+    restatement.
+
+Outputs are plain ``.npz`` (no pickles) and one ``priors.json``.
+"""
+import hashlib
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = '/root/reference'
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from shape_based_object_detection_amd import synth  # noqa: E402  (input recipe only)
+
+
+# ----------------------------------------------------------------------------- reference loading
+def load_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit('make_golden.py: /root/reference is absent — fixtures are generated in '
+                         'the build container only')
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    state = {}
+
+    def nms_standin(boxes, scores, iou_threshold):
+        keep, count = state['iou_utils'].nms(boxes, scores, iou_threshold, top_k=boxes.size(0))
+        return keep[:count]
+
+    tv = types.ModuleType('torchvision')
+    tv.__path__ = []
+    tr = types.ModuleType('torchvision.transforms')
+    tr.__path__ = []
+    trf = types.ModuleType('torchvision.transforms.functional')
+    ops = types.ModuleType('torchvision.ops')
+    ops.nms = nms_standin
+    tvm = types.ModuleType('torchvision.models')
+    tv.transforms, tv.ops, tv.models = tr, ops, tvm
+    tr.functional = trf
+    sys.modules.update({'torchvision': tv, 'torchvision.transforms': tr,
+                        'torchvision.transforms.functional': trf, 'torchvision.ops': ops,
+                        'torchvision.models': tvm})
+    import operators.iou_utils as iou_utils
+    import operators.Loss as Loss
+    import operators.Deformable_convolution as DCN
+    import metrics
+    import dataset.transforms as transforms
+    import models  # noqa: F401  (registers submodules)
+    import models.utils as mutils
+    import detect_scripts.detect_tools as dtools
+    state['iou_utils'] = iou_utils
+    return types.SimpleNamespace(
+        iou_utils=iou_utils, Loss=Loss, DCN=DCN, metrics=metrics, transforms=transforms,
+        mutils=mutils, dtools=dtools,
+        SSD300=sys.modules['models.SSD300'], SSD512=sys.modules['models.SSD512'],
+        RetinaNet=sys.modules['models.RetinaNet'], RefineDet=sys.modules['models.RefineDet512'])
+
+
+class Cfg(dict):
+    """EasyDict-like config: attribute and item access (``train_anchor.py:35-37``)."""
+    __getattr__ = dict.__getitem__
+
+
+def capture_locals(code, fn, *args, **kwargs):
+    """Run ``fn`` and return (result, list of f_locals snapshots at each return of ``code``)."""
+    snaps = []
+
+    def tracer(frame, event, arg):
+        if frame.f_code is not code:
+            return None
+
+        def local(frame, event, arg):
+            if event == 'return':
+                snaps.append(dict(frame.f_locals))
+            return local
+        return local
+
+    sys.settrace(tracer)
+    try:
+        out = fn(*args, **kwargs)
+    finally:
+        sys.settrace(None)
+    return out, snaps
+
+
+def f32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def i64(t):
+    return t.detach().cpu().numpy().astype(np.int64)
+
+
+def save(name, d):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **d)
+    print('wrote', path, '%.1f KB' % (os.path.getsize(path) / 1024))
+
+
+# ----------------------------------------------------------------------------- fixtures
+def gen_priors(R):
+    dummy = types.SimpleNamespace(device='cpu')
+    out = {}
+    arrs = {'SSD300': R.SSD300.SSD300.create_prior_boxes(dummy),
+            'SSD512': R.SSD512.SSD512.create_prior_boxes(dummy),
+            'RETINA': R.RetinaNet.RetinaNet.create_anchors(dummy),
+            'REFINEDET': R.RefineDet.RefineDet512.create_prior_boxes(dummy)}
+    for k, v in arrs.items():
+        b = v.numpy().astype(np.float32).tobytes()
+        out[k] = {'n_priors': int(v.shape[0]), 'sha256': hashlib.sha256(b).hexdigest(),
+                  'head': v[:3].tolist(), 'tail': v[-3:].tolist()}
+    with open(os.path.join(HERE, 'priors.json'), 'w') as f:
+        json.dump(out, f, indent=1)
+    print('wrote priors.json')
+    return {k: v for k, v in arrs.items()}
+
+
+def degenerate_boxes():
+    e = np.float32(1e-5)
+    return torch.tensor([
+        [0.2, 0.2, 0.2, 0.2],                  # zero-area point
+        [0.3, 0.3, 0.3 + float(e), 0.3 + float(e)],  # width == 1e-5f
+        [0.3, 0.3, 0.300001, 0.300001],        # tiny
+        [0.5, 0.5, 0.4, 0.4],                  # inverted
+        [-0.2, -0.1, 0.3, 0.4],                # partly outside [0,1]
+        [1.5, 1.5, 1.6, 1.6],                  # fully outside
+        [0.1, 0.1, 0.1, 0.6],                  # zero width only
+        [0.0, 0.0, 1.0, 1.0],                  # whole image
+    ], dtype=torch.float32)
+
+
+def gen_jaccard(R, priors):
+    d = {}
+    g = torch.Generator().manual_seed(7)
+    pxy = R.transforms.cxcy_to_xy(priors['SSD512'])
+    anchors = torch.cat([pxy[::37], degenerate_boxes(), torch.rand(20, 4, generator=g)], 0)
+    cases = []
+    boxes, _ = synth.make_gt(3, seed=11)
+    cases += boxes
+    cases.append(degenerate_boxes())
+    cases.append(torch.cat([boxes[0], degenerate_boxes()], 0))
+    for k, gt in enumerate(cases):
+        d['c%d_gt' % k] = f32(gt)
+        d['c%d_anchors' % k] = f32(anchors)
+        d['c%d_metrics' % k] = f32(R.metrics.find_jaccard_overlap(gt, anchors))
+        d['c%d_plain' % k] = f32(R.iou_utils.jaccard(gt, anchors))
+    d['n_cases'] = np.int64(len(cases))
+    save('jaccard.npz', d)
+
+
+def criterion_capture(R, module, cls, priors, boxes, labels, locs, scores, cfg):
+    crit = cls(priors_cxcy=priors, config=cfg)
+    return capture_locals(cls.forward.__code__, crit, locs, scores, boxes, labels)
+
+
+def gen_match(R, priors):
+    """Bit-exact assignment pins: object/overlap per prior, classes, neg classes, encoded locs."""
+    d = {}
+    P = priors['SSD512']
+    pxy = R.transforms.cxcy_to_xy(P)
+    cfg = Cfg(reg_weights=1.0, device='cpu', n_classes=21, reg_loss='smoothl1', cls_loss='ce')
+    cases = []
+    for seed, G in [(1, 1), (2, 5), (3, 16)]:
+        b, l = synth.make_gt(1, seed=seed, max_objects=G)
+        cases.append((b[0], l[0]))
+    # zero-overlap object first → shifted (filtered) j quirk
+    b, l = synth.make_gt(1, seed=4)
+    cases.append((torch.cat([torch.tensor([[1.5, 1.5, 1.6, 1.6]]), b[0]], 0),
+                  torch.cat([torch.tensor([7]), l[0]], 0)))
+    # two objects sharing one best prior → last writer wins
+    box = pxy[4321:4322].clone()
+    cases.append((torch.cat([box, box, torch.tensor([[0.1, 0.1, 0.5, 0.6]])], 0),
+                  torch.tensor([3, 9, 12])))
+    # exact prior duplicates and degenerate GT
+    cases.append((torch.cat([pxy[100:101], pxy[5000:5001], degenerate_boxes()[:3]], 0),
+                  torch.tensor([1, 2, 3, 4, 5])))
+    # duplicated prior geometry: which of the equal-IoU priors wins (first-index ties)
+    cases.append((torch.tensor([[0.25, 0.25, 0.75, 0.75], [0.0, 0.0, 1.0, 1.0]]), torch.tensor([5, 6])))
+    for k, (bx, lb) in enumerate(cases):
+        locs, scores = synth.make_preds(1, P.shape[0], 21, seed=100 + k)
+        _, snaps = criterion_capture(R, R.SSD512, R.SSD512.MultiBoxLoss512, P, [bx], [lb],
+                                     locs, scores, cfg)
+        s = snaps[-1]
+        d['c%d_boxes' % k] = f32(bx)
+        d['c%d_labels' % k] = i64(lb)
+        d['c%d_obj' % k] = s['object_for_each_prior'].numpy().astype(np.int16)
+        d['c%d_ovl' % k] = f32(s['overlap_for_each_prior'])
+        d['c%d_cls' % k] = s['true_classes'][0].numpy().astype(np.int8)
+        d['c%d_neg' % k] = s['true_neg_classes'][0].numpy().astype(np.int8)
+        pos = s['true_classes'][0] > 0
+        d['c%d_enc_pos' % k] = f32(s['true_locs_encoded'][0][pos])   # encoded targets at positives
+        d['c%d_locs_sha' % k] = np.array(hashlib.sha256(f32(locs[0]).tobytes()).hexdigest())
+    d['n_cases'] = np.int64(len(cases))
+    save('match_ssd512.npz', d)
+
+    # RefineDet ARM (binary labels vs fixed priors) and ODM (vs decoded ARM boxes) matching.
+    d = {}
+    PR = priors['REFINEDET']
+    cfg = Cfg(reg_weights=1.0, device='cpu', n_classes=21)
+    B = 3
+    boxes, labels = synth.make_gt(B, seed=21)
+    arm_locs, arm_scores = synth.make_preds(B, PR.shape[0], 2, seed=21)
+    odm_locs, odm_scores = synth.make_preds(B, PR.shape[0], 21, seed=22)
+    crit = R.RefineDet.RefineDetLoss(priors_cxcy=PR, config=cfg)
+    _, arm_snaps = capture_locals(R.RefineDet.RefineDetLoss.compute_arm_loss.__code__,
+                                  crit.compute_arm_loss, arm_locs, arm_scores, boxes, labels)
+    _, odm_snaps = capture_locals(R.RefineDet.RefineDetLoss.compute_odm_loss.__code__,
+                                  crit.compute_odm_loss, arm_locs, arm_scores, odm_locs, odm_scores,
+                                  boxes, labels)
+    for i in range(B):
+        d['b%d_boxes' % i] = f32(boxes[i])
+        d['b%d_labels' % i] = i64(labels[i])
+    d['arm_locs_sha'] = np.array(hashlib.sha256(f32(arm_locs).tobytes()).hexdigest())
+    d['arm_scores_sha'] = np.array(hashlib.sha256(f32(arm_scores).tobytes()).hexdigest())
+    arm_cls = arm_snaps[-1]['true_classes']
+    odm_cls = odm_snaps[-1]['true_classes']
+    d['arm_cls'] = arm_cls.numpy().astype(np.int8)
+    d['arm_enc_pos'] = f32(arm_snaps[-1]['true_locs_encoded'][arm_cls > 0])
+    d['odm_cls'] = odm_cls.numpy().astype(np.int8)
+    d['odm_enc_pos'] = f32(odm_snaps[-1]['true_locs_encoded'][odm_cls > 0])
+    d['odm_pos'] = odm_snaps[-1]['positive_priors'].numpy().astype(np.uint8)
+    save('match_refinedet.npz', d)
+
+
+def gen_iou_utils_match(R, priors):
+    d = {}
+    P = priors['SSD300']
+    var = [0.1, 0.2]
+    boxes, labels = synth.make_gt(2, seed=31)
+    loc_t = torch.zeros(2, P.shape[0], 4)
+    conf_t = torch.zeros(2, P.shape[0], dtype=torch.long)
+    loc_t2 = torch.zeros(2, P.shape[0], 4)
+    conf_t2 = torch.zeros(2, P.shape[0], dtype=torch.long)
+    for i in range(2):
+        R.iou_utils.match(0.5, boxes[i], P, var, labels[i], loc_t, conf_t, i)
+        R.iou_utils.match_ious(0.5, boxes[i], P, var, labels[i], loc_t2, conf_t2, i)
+        d['b%d_boxes' % i] = f32(boxes[i])
+        d['b%d_labels' % i] = i64(labels[i])
+    d['match_loc'] = f32(loc_t)
+    d['match_conf'] = i64(conf_t)
+    d['match_ious_loc'] = f32(loc_t2)
+    d['match_ious_conf'] = i64(conf_t2)
+    save('match_iou_utils.npz', d)
+
+
+def gen_codecs(R, priors):
+    d = {}
+    T, U = R.transforms, R.iou_utils
+    P = priors['SSD300'][::5].contiguous()
+    g = torch.Generator().manual_seed(41)
+    xy = torch.rand(P.shape[0], 2, generator=g) * 0.7
+    wh = torch.rand(P.shape[0], 2, generator=g) * 0.3 + 0.01
+    boxes = torch.cat([xy, xy + wh], 1)
+    locs = torch.randn(P.shape[0], 4, generator=g) * 0.3
+    d['priors'] = f32(P)
+    d['boxes'] = f32(boxes)
+    d['locs'] = f32(locs)
+    d['xy_to_cxcy'] = f32(T.xy_to_cxcy(boxes))
+    d['cxcy_to_xy'] = f32(T.cxcy_to_xy(P))
+    d['cxcy_to_gcxgcy'] = f32(T.cxcy_to_gcxgcy(T.xy_to_cxcy(boxes), P))
+    d['gcxgcy_to_cxcy'] = f32(T.gcxgcy_to_cxcy(locs, P))
+    d['point_form'] = f32(U.point_form(P))
+    d['encode'] = f32(U.encode(boxes, P, [0.1, 0.2]))
+    d['decode'] = f32(U.decode(locs, P, [0.1, 0.2]))
+    save('codecs.npz', d)
+
+
+def gen_losses(R):
+    d = {}
+    L, U = R.Loss, R.iou_utils
+    g = torch.Generator().manual_seed(51)
+    N, C = 97, 6
+    # aligned pairs with overlap
+    xy = torch.rand(N, 2, generator=g) * 0.6
+    wh = torch.rand(N, 2, generator=g) * 0.3 + 0.02
+    t = torch.cat([xy, xy + wh], 1)
+    p = (t + torch.randn(N, 4, generator=g) * 0.03).contiguous()
+    d['box_p'] = f32(p)
+    d['box_t'] = f32(t)
+    for name in ['iou', 'giou', 'diou', 'ciou']:
+        fn = getattr(U, 'bbox_overlaps_' + name)
+        pp = p.clone().requires_grad_(True)
+        o = fn(pp, t)
+        o.sum().backward()
+        d['ov_' + name] = f32(o)
+        d['ov_%s_grad' % name] = f32(pp.grad)
+    w = torch.rand(N, generator=g)
+    for lt in ['Iou', 'Giou', 'Diou', 'Ciou']:
+        for red in ['mean', 'sum']:
+            pp = p.clone().requires_grad_(True)
+            loss = L.IouLoss(pred_mode='Corner', reduce=red, losstype=lt)(pp, t)
+            loss.backward()
+            d['iouloss_%s_%s' % (lt, red)] = f32(loss)
+            d['iouloss_%s_%s_grad' % (lt, red)] = f32(pp.grad)
+        pp = p.clone().requires_grad_(True)
+        loss = L.IouLoss(pred_mode='Corner', losstype=lt)(pp, t, weights=w)
+        loss.backward()
+        d['iouloss_%s_w' % lt] = f32(loss)
+        d['iouloss_%s_w_grad' % lt] = f32(pp.grad)
+    # Center mode: decode(loc, priors, variances) then Diou
+    pri = torch.cat([(t[:, :2] + t[:, 2:]) / 2 + 0.01, (t[:, 2:] - t[:, :2]) * 1.1], 1)
+    loc = (torch.randn(N, 4, generator=g) * 0.2).requires_grad_(True)
+    loss = L.IouLoss(pred_mode='Center', variances=[0.1, 0.2], losstype='Diou')(loc, t, prior_data=pri)
+    loss.backward()
+    d['center_priors'] = f32(pri)
+    d['center_loc'] = f32(loc)
+    d['iouloss_center'] = f32(loss)
+    d['iouloss_center_grad'] = f32(loc.grad)
+    # smooth L1
+    a = torch.randn(N, 4, generator=g) * 0.3
+    b = torch.randn(N, 4, generator=g) * 0.3
+    d['sl1_a'] = f32(a)
+    d['sl1_b'] = f32(b)
+    d['sl1_w'] = f32(w)
+    for red in ['mean', 'sum']:
+        aa = a.clone().requires_grad_(True)
+        loss = L.SmoothL1Loss(reduction=red)(aa, b)
+        loss.backward()
+        d['sl1_' + red] = f32(loss)
+        d['sl1_%s_grad' % red] = f32(aa.grad)
+    aa = a.clone().requires_grad_(True)
+    loss = L.SmoothL1Loss()(aa, b, weights=w[:, None])
+    loss.backward()
+    d['sl1_w_loss'] = f32(loss)
+    d['sl1_w_grad'] = f32(aa.grad)
+    # focal losses
+    logits = torch.randn(N, C, generator=g) * 2
+    y = torch.randint(0, C, (N,), generator=g)
+    y[:10] = 0
+    d['logits'] = f32(logits)
+    d['y'] = i64(y)
+    x = logits.clone().requires_grad_(True)
+    loss = L.focal_loss(x, y, device='cpu')
+    loss.backward()
+    d['focal'] = f32(loss)
+    d['focal_grad'] = f32(x.grad)
+    x = logits.clone().requires_grad_(True)
+    loss = L.focal_loss(x, y, alpha=[0.3, 0.6], gamma=1.5, device='cpu')
+    loss.backward()
+    d['focal_b'] = f32(loss)
+    d['focal_b_grad'] = f32(x.grad)
+    cfg = Cfg(device='cpu')
+    x = logits.clone().requires_grad_(True)
+    loss = L.SigmoidFocalLoss(gamma=2.0, alpha=0.25, config=cfg)(x, y)
+    loss.backward()
+    d['sfocal'] = f32(loss)
+    d['sfocal_grad'] = f32(x.grad)
+    x = logits.clone().requires_grad_(True)
+    loss = L.FocalLoss()(x, y)
+    loss.backward()
+    d['bfocal'] = f32(loss)
+    d['bfocal_grad'] = f32(x.grad)
+    save('losses.npz', d)
+
+
+CRITERIA = [
+    # name, module attr, class, prior arch, prior stride, C, B, reg_loss, cls_loss
+    ('ssd512_sl1_ce', 'SSD512', 'MultiBoxLoss512', 'SSD512', 8, 6, 3, 'smoothl1', 'ce'),
+    ('ssd512_diou_focal', 'SSD512', 'MultiBoxLoss512', 'SSD512', 8, 6, 3, 'diou', 'focal'),
+    ('ssd300_l1_ce', 'SSD300', 'MultiBoxLoss300', 'SSD300', 7, 6, 3, 'l1', 'ce'),
+    ('ssd300_diou_focal', 'SSD300', 'MultiBoxLoss300', 'SSD300', 7, 6, 3, 'diou', 'focal'),
+    ('retina_diou_focal', 'RetinaNet', 'RetinaFocalLoss', 'RETINA', 16, 6, 3, 'diou', 'focal'),
+    ('retina_sl1_ce', 'RetinaNet', 'RetinaFocalLoss', 'RETINA', 16, 6, 3, 'smoothl1', 'ce'),
+    ('ssd512full_diou_focal', 'SSD512', 'MultiBoxLoss512', 'SSD512', 1, 21, 2, 'diou', 'focal'),
+    ('ssd512full_sl1_ce', 'SSD512', 'MultiBoxLoss512', 'SSD512', 1, 21, 2, 'smoothl1', 'ce'),
+]
+
+
+def gen_criteria(R, priors):
+    for name, mod, cls, arch, stride, C, B, reg, clsl in CRITERIA:
+        d = {}
+        P = priors[arch][::stride].contiguous()
+        boxes, labels = synth.make_gt(B, seed=61, n_classes=C)
+        locs, scores = synth.make_preds(B, P.shape[0], C, seed=61)
+        cfg = Cfg(reg_weights=1.0, device='cpu', n_classes=C, reg_loss=reg, cls_loss=clsl)
+        crit = getattr(getattr(R, mod), cls)(priors_cxcy=P, config=cfg)
+        lo = locs.clone().requires_grad_(True)
+        sc = scores.clone().requires_grad_(True)
+        loss = crit(lo, sc, boxes, labels)
+        loss.backward()
+        full = stride == 1
+        d['prior_stride'] = np.int64(stride)
+        d['arch'] = np.array(arch)
+        d['n_classes'] = np.int64(C)
+        d['batch'] = np.int64(B)
+        for i in range(B):
+            d['b%d_boxes' % i] = f32(boxes[i])
+            d['b%d_labels' % i] = i64(labels[i])
+        d['loss'] = f32(loss)
+        if full:   # inputs regenerate from the recipe; pin with checksums + samples
+            d['locs_sha'] = np.array(hashlib.sha256(f32(locs).tobytes()).hexdigest())
+            d['scores_sha'] = np.array(hashlib.sha256(f32(scores).tobytes()).hexdigest())
+            gl, gs = f32(lo.grad), f32(sc.grad)
+            d['grad_locs_abssum'] = np.float64(np.abs(gl).astype(np.float64).sum())
+            d['grad_scores_abssum'] = np.float64(np.abs(gs).astype(np.float64).sum())
+            rows = np.flatnonzero(np.abs(gl).sum(-1).reshape(-1) > 0)[:200]
+            d['grad_locs_rows'] = rows.astype(np.int64)
+            d['grad_locs_at_rows'] = gl.reshape(-1, 4)[rows]
+            srows = np.random.RandomState(0).choice(B * P.shape[0], 300, replace=False)
+            d['grad_scores_rows'] = srows.astype(np.int64)
+            d['grad_scores_at_rows'] = gs.reshape(-1, C)[srows]
+        else:
+            d['locs'] = f32(locs)
+            d['scores'] = f32(scores)
+            d['grad_locs'] = f32(lo.grad)
+            d['grad_scores'] = f32(sc.grad)
+        save('crit_%s.npz' % name, d)
+
+    # RefineDet: arm + odm
+    d = {}
+    P = priors['REFINEDET'][::8].contiguous()
+    C, B = 6, 3
+    boxes, labels = synth.make_gt(B, seed=71, n_classes=C)
+    arm_locs, arm_scores = synth.make_preds(B, P.shape[0], 2, seed=71)
+    odm_locs, odm_scores = synth.make_preds(B, P.shape[0], C, seed=72)
+    cfg = Cfg(reg_weights=1.0, device='cpu', n_classes=C)
+    crit = R.RefineDet.RefineDetLoss(priors_cxcy=P, config=cfg)
+    ts = [t.clone().requires_grad_(True) for t in (arm_locs, arm_scores, odm_locs, odm_scores)]
+    loss = crit(*ts, boxes, labels)
+    loss.backward()
+    for i in range(B):
+        d['b%d_boxes' % i] = f32(boxes[i])
+        d['b%d_labels' % i] = i64(labels[i])
+    for n, t0, t in zip(['arm_locs', 'arm_scores', 'odm_locs', 'odm_scores'],
+                        (arm_locs, arm_scores, odm_locs, odm_scores), ts):
+        d[n] = f32(t0)
+        d[n + '_grad'] = f32(t.grad)
+    d['loss'] = f32(loss)
+    d['arm_loss'] = f32(crit.compute_arm_loss(arm_locs, arm_scores, boxes, labels))
+    d['prior_stride'] = np.int64(8)
+    save('crit_refinedet.npz', d)
+
+
+def gen_nms(R):
+    d = {}
+    U = R.iou_utils
+    g = torch.Generator().manual_seed(81)
+    k = 0
+    for n, thr, top_k in [(50, 0.5, 200), (300, 0.45, 200), (300, 0.3, 50), (1, 0.5, 200),
+                          (120, 0.7, 120)]:
+        xy = torch.rand(n, 2, generator=g) * 0.8
+        wh = torch.rand(n, 2, generator=g) * 0.2 + 0.01
+        boxes = torch.cat([xy, xy + wh], 1)
+        scores = torch.randperm(n, generator=g).float() / n + 0.001   # tie-free
+        keep, count = U.nms(boxes, scores, thr, top_k)
+        dkeep, dcount = U.diounms(boxes, scores, thr, top_k)
+        d['c%d_boxes' % k] = f32(boxes)
+        d['c%d_scores' % k] = f32(scores)
+        d['c%d_thr' % k] = np.float64(thr)
+        d['c%d_topk' % k] = np.int64(top_k)
+        d['c%d_keep' % k] = i64(keep)
+        d['c%d_count' % k] = np.int64(count)
+        d['c%d_dkeep' % k] = i64(dkeep)
+        d['c%d_dcount' % k] = np.int64(dcount)
+        k += 1
+    d['n_cases'] = np.int64(k)
+    empty = U.nms(torch.zeros(0, 4), torch.zeros(0))
+    d['empty_is_tensor'] = np.int64(isinstance(empty, torch.Tensor))
+    save('nms.npz', d)
+
+
+def gen_detect(R, priors):
+    d = {}
+    P = priors['SSD512'][::16].contiguous()
+    C, B = 6, 2
+    k = 0
+    variants = [('utils', 'offset', 'softmax', False), ('utils', 'center', 'softmax', False),
+                ('utils', 'corner', 'softmax', False), ('utils', 'offset', 'sigmoid', False),
+                ('utils', 'offset', 'softmax', True), ('tools', 'offset', 'softmax', False),
+                ('tools_refine', 'corner', 'softmax', True)]
+    for fn, box_type, focal_type, use_pos in variants:
+        locs, scores = synth.make_preds(B, P.shape[0], C, seed=91 + k, bg_shift=2.0)
+        if box_type == 'center':
+            locs = torch.cat([P[None, :, :2] + locs[..., :2] * 0.1, P[None, :, 2:] * torch.exp(locs[..., 2:])], -1)
+        elif box_type == 'corner':
+            locs = R.transforms.cxcy_to_xy(P)[None] + locs * 0.2
+        pos = None
+        if use_pos:
+            pos = torch.rand(B, P.shape[0], generator=torch.Generator().manual_seed(k)) > 0.3
+        cfg = Cfg(device='cpu', focal_type=focal_type, model={'box_type': box_type})
+        locs_in = locs.clone()
+        min_score, max_overlap, top_k = 0.05, 0.45, 60
+        if fn == 'utils':
+            ob, ol, os_ = R.mutils.detect(locs_in, scores, min_score, max_overlap, top_k, P, cfg,
+                                          prior_positives_idx=pos)
+        elif fn == 'tools':
+            ob, ol, os_ = R.dtools.detect(locs_in, scores, min_score, max_overlap, top_k, P)
+        else:
+            ob, ol, os_ = R.dtools.detect_refine(locs_in, scores, min_score, max_overlap, top_k, P,
+                                                 prior_positives_idx=pos)
+        d['c%d_fn' % k] = np.array(fn)
+        d['c%d_box_type' % k] = np.array(box_type)
+        d['c%d_focal_type' % k] = np.array(focal_type)
+        d['c%d_locs' % k] = f32(locs)
+        d['c%d_locs_after' % k] = f32(locs_in)      # the in-place clamp_ quirk
+        d['c%d_scores' % k] = f32(scores)
+        if pos is not None:
+            d['c%d_pos' % k] = pos.numpy().astype(np.uint8)
+        d['c%d_counts' % k] = np.array([x.shape[0] for x in ob], dtype=np.int64)
+        d['c%d_boxes' % k] = f32(torch.cat(ob, 0))
+        d['c%d_labels' % k] = i64(torch.cat(ol, 0))
+        d['c%d_scores_out' % k] = f32(torch.cat(os_, 0))
+        d['c%d_params' % k] = np.array([min_score, max_overlap, top_k], dtype=np.float64)
+        k += 1
+    d['n_cases'] = np.int64(k)
+    d['prior_stride'] = np.int64(16)
+    save('detect.npz', d)
+
+
+def gen_dcn(R):
+    d = {}
+    k = 0
+    for (B, C, O, H, W, stride) in [(2, 8, 6, 9, 9, 1), (1, 5, 4, 7, 10, 2), (2, 16, 8, 6, 6, 1)]:
+        torch.manual_seed(k)
+        m = R.DCN.DeformConv2d(C, O, kernel_size=3, padding=1, stride=stride)
+        with torch.no_grad():     # non-zero offset/modulation branches so sampling is exercised
+            m.p_conv.weight.normal_(0, 0.3)
+            m.m_conv.weight.normal_(0, 0.3)
+        g = torch.Generator().manual_seed(100 + k)
+        x = torch.randn(B, C, H, W, generator=g).requires_grad_(True)
+        out = m(x)
+        gout = torch.randn(out.shape, generator=g)
+        out.backward(gout)
+        pre = 'c%d_' % k
+        d[pre + 'shape'] = np.array([B, C, O, H, W, stride], dtype=np.int64)
+        d[pre + 'x'] = f32(x)
+        d[pre + 'out'] = f32(out)
+        d[pre + 'gout'] = f32(gout)
+        d[pre + 'gx'] = f32(x.grad)
+        for n, p in m.named_parameters():
+            d[pre + 'w_' + n.replace('.', '_')] = f32(p)
+            d[pre + 'g_' + n.replace('.', '_')] = f32(p.grad)
+        k += 1
+    d['n_cases'] = np.int64(k)
+    save('dcn.npz', d)
+
+
+def main():
+    torch.set_num_threads(8)
+    R = load_reference()
+    priors = gen_priors(R)
+    gen_jaccard(R, priors)
+    gen_match(R, priors)
+    gen_iou_utils_match(R, priors)
+    gen_codecs(R, priors)
+    gen_losses(R)
+    gen_criteria(R, priors)
+    gen_nms(R)
+    gen_detect(R, priors)
+    gen_dcn(R)
+
+
+if __name__ == '__main__':
+    main()
