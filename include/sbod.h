@@ -1,0 +1,224 @@
+/*
+ * sbod.h — C ABI of libsbod_hip.so, the gfx950 (MI355X) implementation of the
+ * shape_based_object_detection hot path: anchor matching, detection losses, box decode + NMS
+ * and DeformConv2d.
+ *
+ * Conventions:
+ *   - every pointer is a DEVICE pointer unless documented otherwise; the caller owns all memory
+ *     (outputs and workspaces are allocated by the caller, e.g. from torch's caching allocator);
+ *   - every call is asynchronous on `stream` (a hipStream_t passed as void*); nothing here
+ *     allocates, frees or synchronises, so every call is hipGraph-capturable;
+ *   - return SBOD_OK (0) or a negative sbod_status; sbod_last_error() then holds a message
+ *     (thread-local).  Nothing throws across the ABI;
+ *   - ragged per-image ground truth is packed as gt_boxes [sum(G_i), 4] float32 xyxy,
+ *     gt_labels [sum(G_i)] int64 and gt_offsets [B + 1] int32 (image b owns rows
+ *     gt_offsets[b] .. gt_offsets[b+1]-1) — the collate_fn list-of-tensors batch of
+ *     dataset/Datasets.py:58-86, concatenated once per step;
+ *   - load after `import torch` so SONAME libamdhip64.so.7 binds to torch's HIP runtime.
+ *
+ * Each entry point cites the reference Python interface it replaces (file:line in the
+ * upstream repository).
+ */
+#ifndef SBOD_H
+#define SBOD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBOD_ABI_VERSION 1
+
+typedef enum sbod_status {
+  SBOD_OK = 0,
+  SBOD_E_INVALID = -1,      /* bad argument / shape */
+  SBOD_E_HIP = -2,          /* HIP runtime error (launch failure) */
+  SBOD_E_WORKSPACE = -3,    /* workspace too small */
+  SBOD_E_UNSUPPORTED = -4   /* size beyond what this build supports (message says which) */
+} sbod_status;
+
+/* ---------------------------------------------------------------- library */
+const char *sbod_version(void);
+int sbod_abi_version(void);
+const char *sbod_last_error(void);
+
+/* ---------------------------------------------------------------- a1 / a4: pairwise IoU
+ * Replaces metrics.find_jaccard_overlap (metrics.py:208-252; mode SBOD_IOU_METRICS: +1e-5
+ * denominator, zero-GT -> 0, zero-anchor -> -1) and iou_utils.jaccard (iou_utils.py:215-233;
+ * mode SBOD_IOU_PLAIN).  out[b, g, p] for g < G_b; rows g >= G_b are left untouched.
+ * anchors: [P,4] xyxy shared when anchor_batch_stride == 0, else image b reads
+ * anchors + b * anchor_batch_stride (elements). */
+enum { SBOD_IOU_METRICS = 0, SBOD_IOU_PLAIN = 1 };
+int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int B, int Gmax,
+                          const float *anchors, int64_t anchor_batch_stride, int P, int mode,
+                          float *out, void *stream);
+
+/* ---------------------------------------------------------------- a2 / a3: anchor matching
+ * Replaces the per-image matching block of every criterion
+ * (models/SSD512.py:532-572, SSD300.py:501-542, RetinaNet.py:409-449,
+ *  RefineDet512.py:745-785 (ARM, SBOD_MATCH_BINARY) and :846-886 (ODM, SBOD_MATCH_ODM)):
+ * find_jaccard_overlap -> max(dim 0) / max(dim 1) (first index on ties) -> forced match with the
+ * FILTERED j, last writer wins -> label / negative thresholds.
+ *   anchors: xyxy [P,4] (shared priors_xy); for SBOD_MATCH_ODM `anchors` are the ARM locs
+ *            [B,P,4] (gcxgcy) decoded on the fly against priors_cxcy, exactly
+ *            cxcy_to_xy(gcxgcy_to_cxcy(arm_locs[i], priors_cxcy)) (RefineDet512.py:850).
+ *   arm_scores: [B,P,2] logits, only for SBOD_MATCH_ODM (easy negatives softmax[...,1] < theta).
+ *   Outputs [B,P]: obj (object per prior, int32), ovl (overlap per prior after the forced match).
+ *   n_pos [B+1] int32: positives per image (+ the batch total at n_pos[B]).  Labels and the
+ *   negative mask are derived from (obj, ovl, gt_labels) by the loss kernels.
+ * Workspace: sbod_match_workspace_bytes(B, Gmax). */
+enum { SBOD_MATCH_BINARY = 1, SBOD_MATCH_ODM = 2 };
+size_t sbod_match_workspace_bytes(int B, int Gmax);
+int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt_offsets,
+                   int B, int Gmax, const float *anchors, const float *priors_cxcy,
+                   const float *arm_scores, int P, float threshold, float theta, int flags,
+                   int32_t *obj, float *ovl, int32_t *n_pos, void *workspace,
+                   size_t workspace_bytes, void *stream);
+
+/* Expand matcher outputs to the reference's tensors (for parity tests and the iou_utils API):
+ * cls [B,P] int64 (labels[obj], 0 where ovl < threshold; binary -> 0/1),
+ * neg [B,P] int64 (labels[obj], -1 where ovl < neg_threshold),
+ * true_xy [B,P,4] (gt_boxes[obj]) and enc [B,P,4] (cxcy_to_gcxgcy(xy_to_cxcy(gt[obj]), prior)).
+ * Any output pointer may be NULL. */
+int sbod_match_expand_f32(const float *gt_boxes, const int64_t *gt_labels,
+                          const int32_t *gt_offsets, int B, const int32_t *obj, const float *ovl,
+                          const float *priors_cxcy, const float *odm_arm_locs, int P,
+                          float threshold, float neg_threshold, int flags, int64_t *cls,
+                          int64_t *neg, float *true_xy, float *enc, void *stream);
+
+/* iou_utils.match / match_ious (iou_utils.py:236-321): plain jaccard vs point_form(priors),
+ * best-prior fill 2.0, UNFILTERED j, conf = labels + 1.  Writes loc_t[idx] / conf_t[idx]
+ * rows (caller passes the row pointers).  encode != 0 -> encode(variances) else raw matches. */
+int sbod_match_ssd_f32(const float *truths, const int64_t *labels, int G,
+                       const float *priors_cxcy, int P, float threshold, float var0, float var1,
+                       int encode, float *loc_t_row, int64_t *conf_t_row, void *workspace,
+                       size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------- a3: box codecs
+ * dataset/transforms.py:26-83 and iou_utils.py:167-177, 324-368.  n rows of 4 floats.
+ * priors may be [n,4] or broadcast [P,4] with rows = n (prior_rows > 0 -> row i uses
+ * prior i % prior_rows). */
+enum { SBOD_CODEC_XY_TO_CXCY = 0, SBOD_CODEC_CXCY_TO_XY = 1, SBOD_CODEC_ENCODE_TENFIVE = 2,
+       SBOD_CODEC_DECODE_TENFIVE = 3, SBOD_CODEC_ENCODE_VAR = 4, SBOD_CODEC_DECODE_VAR = 5,
+       SBOD_CODEC_DECODE_TENFIVE_XY = 6 };
+int sbod_codec_f32(int op, const float *in, const float *priors, int64_t n, int64_t prior_rows,
+                   float var0, float var1, float *out, void *stream);
+
+/* ---------------------------------------------------------------- a5-a10: fused criterion
+ * One pass over the predictions of every criterion in models/*.py: per prior the label is
+ * derived from the matcher, the box loss (a5/a6) and class loss (a7/a10) and their gradients
+ * are produced together (one read of locs/scores, one write of their gradients).
+ *   reg:  SBOD_REG_SMOOTHL1 (Loss.py:203-226, beta 1/9, mean over positive rows),
+ *         SBOD_REG_L1 (nn.L1Loss, SSD300.py:465, mean over elements),
+ *         SBOD_REG_DIOU (IouLoss 'Corner' Diou on decoded boxes, Loss.py:164-200).
+ *   cls:  SBOD_CLS_FOCAL (softmax focal_loss, Loss.py:9-38, rows = positives + negatives),
+ *         SBOD_CLS_CE (CrossEntropy + hard-negative mining, a10).
+ *   flags: SBOD_LOSS_FOCAL_NORM (divide focal by total positives, RetinaNet.py:471-472),
+ *          pool for CE mining: SBOD_POOL_NONPOS (SSD512.py:601-623), SBOD_POOL_NEG
+ *          (RetinaNet.py:478-503), SBOD_POOL_GLOBAL_NEG (SSD300.py:567-591),
+ *          SBOD_POOL_NONPOS_NOT_EASY (RefineDet512.py:910-936); SBOD_MATCH_BINARY / _ODM as
+ *          for the matcher.
+ *   locs/scores: [B,P,4] / [B,P,C], dtype float32 (SBOD_DT_F32) or bfloat16 (SBOD_DT_BF16);
+ *   grad_locs/grad_scores: same shape and dtype; may be NULL (forward only).
+ *   loss_out: device float[4] = {total, conf, loc, n_pos_total}.
+ *   npos_total: device int32 pointer to the normaliser (the matcher's n_pos[B], or a
+ *   cross-rank all-reduced copy for data parallelism).
+ * Workspace: sbod_loss_workspace_bytes(B, P). */
+enum { SBOD_REG_SMOOTHL1 = 0, SBOD_REG_L1 = 1, SBOD_REG_DIOU = 2 };
+enum { SBOD_CLS_FOCAL = 0, SBOD_CLS_CE = 1 };
+enum { SBOD_DT_F32 = 0, SBOD_DT_BF16 = 1 };
+enum { SBOD_LOSS_FOCAL_NORM = 4, SBOD_POOL_NONPOS = 0, SBOD_POOL_NEG = 8,
+       SBOD_POOL_GLOBAL_NEG = 16, SBOD_POOL_NONPOS_NOT_EASY = 32 };
+size_t sbod_loss_workspace_bytes(int B, int P);
+int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, int P, int C,
+                       const float *priors_cxcy, const float *odm_arm_locs,
+                       const float *arm_scores, const float *gt_boxes, const int64_t *gt_labels,
+                       const int32_t *gt_offsets, const int32_t *obj, const float *ovl,
+                       const int32_t *n_pos, const int32_t *npos_total, float threshold,
+                       float neg_threshold, float theta, int reg, int cls, int flags,
+                       int neg_pos_ratio, float reg_weight, float focal_alpha, float focal_gamma,
+                       void *grad_locs, void *grad_scores, float *loss_out, void *workspace,
+                       size_t workspace_bytes, void *stream);
+
+/* grad *= (*scale) in place unless *scale == 1 (decided on the device: no host sync).
+ * Used by backward to apply the upstream gradient to gradients produced by the fused
+ * forward. */
+int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, void *stream);
+
+/* ---------------------------------------------------------------- a5/a6/a7/a8/a9 standalone
+ * The operators.Loss / iou_utils API on already-selected rows.  Each call writes the per-row
+ * (or per-element) values and their local derivatives; the Python layer applies the
+ * reference's own reductions (Loss.py:192-200, 219-226, 38, 80, 103) through autograd.
+ *   aligned overlap (iou_utils.py:6-164): overlap [n] and d overlap / d b1 [n,4] (grad may be
+ *     NULL); the reference's clamp masks and its min/max tie rule (gradient split in half).
+ *   smooth L1 (Loss.py:213-217): loss [n] and d loss / d pred [n] per element.
+ *   focal (Loss.py:9-38 softmax, :41-80 sigmoid, :83-103 bce): loss [rows] and
+ *     d loss / d logits [rows, C]. */
+enum { SBOD_OV_IOU = 0, SBOD_OV_GIOU = 1, SBOD_OV_DIOU = 2, SBOD_OV_CIOU = 3 };
+int sbod_aligned_overlap_f32(int kind, const float *b1, const float *b2, int64_t n,
+                             float *overlap, float *grad_b1, void *stream);
+int sbod_smooth_l1_f32(const float *pred, const float *target, int64_t n, float beta,
+                       float *loss, float *grad, void *stream);
+enum { SBOD_FOCAL_SOFTMAX = 0, SBOD_FOCAL_SIGMOID = 1, SBOD_FOCAL_BCE = 2 };
+int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t rows, int C,
+                   float alpha_fg, float alpha_bg, float gamma, float *row_loss, float *grad,
+                   void *stream);
+
+/* ---------------------------------------------------------------- a11-a13: decode + NMS
+ * Replaces models/utils.py:181-297 (detect), detect_scripts/detect_tools.py:100-341
+ * (detect / detect_refine, final class-agnostic NMS) and the torchvision.ops.nms it calls
+ * (torchvision semantics: descending stable order, suppress IoU > thr).
+ *   box_type: SBOD_BOX_OFFSET (gcxgcy vs priors), SBOD_BOX_CENTER (cxcy), SBOD_BOX_CORNER
+ *             (xyxy; clamped IN PLACE into `locs`, the reference's clamp_ quirk).
+ *   act: SBOD_ACT_SOFTMAX | SBOD_ACT_SIGMOID.
+ *   pos_mask: [B,P] uint8 (prior_positives_idx) or NULL.
+ *   Outputs: det_boxes [B,top_k,4], det_labels [B,top_k] int64, det_scores [B,top_k],
+ *            det_count [B] int32 (rows beyond count are unspecified);
+ *            debug_probs [B,P,C] / debug_boxes [B,P,4] may be NULL.
+ *   final_nms < 0 disables the detect_tools final class-agnostic NMS.
+ * Workspace: sbod_detect_workspace_bytes(B, P, C). */
+enum { SBOD_BOX_OFFSET = 0, SBOD_BOX_CENTER = 1, SBOD_BOX_CORNER = 2 };
+enum { SBOD_ACT_SOFTMAX = 0, SBOD_ACT_SIGMOID = 1 };
+size_t sbod_detect_workspace_bytes(int B, int P, int C);
+int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
+                    const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
+                    float min_score, float max_overlap, int top_k, float final_nms,
+                    float *det_boxes, int64_t *det_labels, float *det_scores, int32_t *det_count,
+                    float *debug_probs, float *debug_boxes, void *workspace,
+                    size_t workspace_bytes, void *stream);
+
+/* Single-segment greedy NMS (iou_utils.nms / diounms, iou_utils.py:385-530; torchvision.ops.nms).
+ *   variant: SBOD_NMS_TV (union (a_i + a_j) - inter, suppress iff IoU > thr),
+ *            SBOD_NMS_REF (iou_utils.nms: union (a_j - inter) + a_i, keep iff IoU <= thr,
+ *                          the top_k highest kept BEFORE suppression),
+ *            SBOD_NMS_DIOU (iou_utils.diounms incl. its center_y2 quirk, beta1 exponent).
+ *   keep [n] int64 (indices, descending score), count [1] int32. top_k <= 0: no truncation. */
+enum { SBOD_NMS_TV = 0, SBOD_NMS_REF = 1, SBOD_NMS_DIOU = 2 };
+size_t sbod_nms_workspace_bytes(int64_t n);
+int sbod_nms_f32(const float *boxes, const float *scores, int64_t n, float overlap, int top_k,
+                 int variant, float beta1, int64_t *keep, int32_t *count, void *workspace,
+                 size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------- a14: DeformConv2d
+ * operators/Deformable_convolution.py:33-146 (modulated DCNv2, rows|cols offset layout,
+ * p_0 starting at 1, floor-before-clamp, border clamp, k x k stride-k bias-free conv).
+ *   x [B,C,H,W], offset [B,2k²,Ho,Wo] (p_conv output), mask_logits [B,k²,Ho,Wo] (m_conv
+ *   output BEFORE sigmoid, or NULL for modulation=False), weight [O,C,k,k] -> out [B,O,Ho,Wo].
+ *   Backward: grad_out -> grad_x, grad_offset, grad_mask_logits, grad_weight (any may be NULL).
+ * Workspace: sbod_dcn_workspace_bytes(...). */
+size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
+int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logits,
+                     const float *weight, int B, int C, int H, int W, int O, int k, int stride,
+                     int pad, float *out, void *workspace, size_t workspace_bytes, void *stream);
+int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logits,
+                     const float *weight, const float *grad_out, int B, int C, int H, int W,
+                     int O, int k, int stride, int pad, float *grad_x, float *grad_offset,
+                     float *grad_mask_logits, float *grad_weight, void *workspace,
+                     size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SBOD_H */

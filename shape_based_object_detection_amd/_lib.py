@@ -1,0 +1,118 @@
+"""ctypes binding of libsbod_hip.so (the C ABI in include/sbod.h).
+
+The library is loaded AFTER ``import torch`` so its SONAME ``libamdhip64.so.7`` binds to the HIP
+runtime torch already mapped.  There is no fallback: if the library is missing or a call
+fails, this raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen; see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('SBOD_LIB', os.path.join(_HERE, 'lib', 'libsbod_hip.so'))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/sbod.h one to one.
+SIGNATURES = {
+    'sbod_version': (ctypes.c_char_p, []),
+    'sbod_abi_version': (I32, []),
+    'sbod_last_error': (ctypes.c_char_p, []),
+    'sbod_iou_pairwise_f32': (I32, [P, P, I32, I32, P, I64, I32, I32, P, P]),
+    'sbod_match_workspace_bytes': (SZ, [I32, I32]),
+    'sbod_match_f32': (I32, [P, P, P, I32, I32, P, P, P, I32, F32, F32, I32, P, P, P, P, SZ, P]),
+    'sbod_match_expand_f32': (I32, [P, P, P, I32, P, P, P, P, I32, F32, F32, I32, P, P, P, P, P]),
+    'sbod_match_ssd_f32': (I32, [P, P, I32, P, I32, F32, F32, F32, I32, P, P, P, SZ, P]),
+    'sbod_codec_f32': (I32, [I32, P, P, I64, I64, F32, F32, P, P]),
+    'sbod_loss_workspace_bytes': (SZ, [I32, I32]),
+    'sbod_multibox_loss': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, P, F32, F32,
+                                 F32, I32, I32, I32, I32, F32, F32, F32, P, P, P, P, SZ, P]),
+    'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),
+    'sbod_aligned_overlap_f32': (I32, [I32, P, P, I64, P, P, P]),
+    'sbod_smooth_l1_f32': (I32, [P, P, I64, F32, P, P, P]),
+    'sbod_focal_f32': (I32, [I32, P, P, I64, I32, F32, F32, F32, P, P, P]),
+    'sbod_detect_workspace_bytes': (SZ, [I32, I32, I32]),
+    'sbod_detect_f32': (I32, [P, P, I32, I32, I32, P, P, I32, I32, F32, F32, I32, F32, P, P, P, P,
+                              P, P, P, SZ, P]),
+    'sbod_nms_workspace_bytes': (SZ, [I64]),
+    'sbod_nms_f32': (I32, [P, P, I64, F32, I32, I32, F32, P, P, P, SZ, P]),
+    'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
+    'sbod_dcn_fwd_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),
+    'sbod_dcn_bwd_f32': (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, P,
+                               P, SZ, P]),
+}
+
+# Constants of include/sbod.h.
+IOU_METRICS, IOU_PLAIN = 0, 1
+MATCH_BINARY, MATCH_ODM = 1, 2
+CODEC = dict(xy_to_cxcy=0, cxcy_to_xy=1, encode_tenfive=2, decode_tenfive=3, encode_var=4,
+             decode_var=5, decode_tenfive_xy=6)
+REG = dict(smoothl1=0, l1=1, diou=2)
+CLS = dict(focal=0, ce=1)
+DT_F32, DT_BF16 = 0, 1
+LOSS_FOCAL_NORM = 4
+POOL = dict(nonpos=0, neg=8, global_neg=16, nonpos_not_easy=32)
+OV = dict(iou=0, giou=1, diou=2, ciou=3)
+FOCAL = dict(softmax=0, sigmoid=1, bce=2)
+BOX = dict(offset=0, center=1, corner=2)
+ACT = dict(softmax=0, sigmoid=1)
+NMS = dict(tv=0, ref=1, diou=2)
+
+
+class SbodError(RuntimeError):
+    pass
+
+
+_lib = None
+MISSING = []   # declared in include/sbod.h but not exported (tests assert this is empty)
+
+
+def lib():
+    """The loaded library (raises SbodError when it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SbodError('libsbod_hip.so not found at %s — build it with '
+                            '`python -m shape_based_object_detection_amd.build`' % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                MISSING.append(name)
+                continue
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    """Invoke an sbod_* entry point; raise SbodError with sbod_last_error() on failure."""
+    st = getattr(lib(), name)(*args)
+    if st != 0:
+        msg = lib().sbod_last_error().decode(errors='replace')
+        raise SbodError('%s failed (%d): %s' % (name, st, msg))
+    return st
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_device(*tensors, what='sbod'):
+    """The HIP path only: CPU tensors are rejected (no silent CPU fallback)."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise SbodError('%s: expected ROCm device tensors, got a %s tensor. The sbod hot path '
+                            'has no CPU implementation; move inputs to the GPU.' % (what, t.device))

@@ -1,0 +1,68 @@
+// Library plumbing: version, thread-local error string, launch checks, device-side grad scale.
+#include <cstdarg>
+#include <cstring>
+
+#include "sbod_common.h"
+
+namespace sbod {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int launch_status(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return SBOD_E_HIP;
+  }
+  return SBOD_OK;
+}
+
+// grad *= *scale unless *scale == 1 (every block reads the scalar and exits early).
+template <typename T>
+__global__ __launch_bounds__(256) void k_scale(T *__restrict__ g, int64_t n, const float *scale) {
+  const float s = *scale;
+  if (s == 1.0f) return;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if constexpr (sizeof(T) == 4) {
+      g[i] = g[i] * s;
+    } else {
+      float v = __uint_as_float(static_cast<uint32_t>(g[i]) << 16) * s;
+      uint32_t u = __float_as_uint(v);
+      u += 0x7fffu + ((u >> 16) & 1u);
+      g[i] = static_cast<T>(u >> 16);
+    }
+  }
+}
+
+}  // namespace sbod
+
+extern "C" {
+
+const char *sbod_version(void) { return "sbod-hip 0.1.0 (gfx950)"; }
+int sbod_abi_version(void) { return SBOD_ABI_VERSION; }
+const char *sbod_last_error(void) { return sbod::g_err; }
+
+int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, void *stream) {
+  SBOD_REQUIRE(n >= 0 && scale != nullptr, "sbod_scale_inplace: bad arguments");
+  if (n == 0) return SBOD_OK;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (dtype == SBOD_DT_F32)
+    hipLaunchKernelGGL(sbod::k_scale<float>, dim3(blocks), dim3(256), 0, sbod::as_stream(stream),
+                       static_cast<float *>(grad), n, scale);
+  else
+    hipLaunchKernelGGL(sbod::k_scale<uint16_t>, dim3(blocks), dim3(256), 0,
+                       sbod::as_stream(stream), static_cast<uint16_t *>(grad), n, scale);
+  SBOD_LAUNCHED("sbod_scale_inplace");
+  return SBOD_OK;
+}
+
+}  // extern "C"

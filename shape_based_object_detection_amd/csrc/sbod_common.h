@@ -1,0 +1,127 @@
+// Shared device/host helpers for libsbod_hip.so (gfx950 only).
+//
+// Numerics contract: the library is compiled with -ffp-contract=off and IEEE division, and
+// every expression that feeds an integer decision (IoU -> argmax, NMS suppression, label
+// thresholds) is written in the reference's evaluation order, so those decisions are the
+// reference CPU path's bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "sbod.h"
+
+namespace sbod {
+
+void set_error(const char *fmt, ...);
+int launch_status(const char *what);  // hipGetLastError -> SBOD_OK / SBOD_E_HIP
+
+constexpr int kWave = 64;
+constexpr float kIouEps = 1e-5f;  // metrics.py:233 EPS (compared as float32, like torch)
+
+#define SBOD_REQUIRE(cond, ...)            \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::sbod::set_error(__VA_ARGS__);       \
+      return SBOD_E_INVALID;                \
+    }                                       \
+  } while (0)
+
+#define SBOD_LAUNCHED(what)                       \
+  do {                                            \
+    int _st = ::sbod::launch_status(what);        \
+    if (_st != SBOD_OK) return _st;               \
+  } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// Monotone float <-> uint32 mapping: a < b  <=>  ord(a) < ord(b) (for non-NaN floats).
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+  uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), m, kWave);
+  uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), m, kWave);
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    unsigned long long o = shfl_xor_u64(v, m);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+  return v;
+}
+
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+  return v;
+}
+
+// Block-wide sum (blockDim.x multiple of 64, <= 1024); result valid in every thread.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T *scratch /* >= 16 */) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  T s = 0;
+  for (int i = 0; i < nw; ++i) s += scratch[i];
+  return s;
+}
+
+// ----------------------------------------------------------------------------- box codecs
+// dataset/transforms.py:37-45 / 69-83 in the reference's evaluation order.
+struct Box4 {
+  float a, b, c, d;
+};
+
+// cxcy_to_xy(gcxgcy_to_cxcy(g, prior)).  c = g_xy * p_wh / 10 + p_xy; wh = exp(g_wh / 5) * p_wh.
+__device__ __forceinline__ Box4 decode_tenfive_xy(Box4 g, Box4 p) {
+  float cx = g.a * p.c / 10.f + p.a;
+  float cy = g.b * p.d / 10.f + p.b;
+  float w = expf(g.c / 5.f) * p.c;
+  float h = expf(g.d / 5.f) * p.d;
+  return Box4{cx - w / 2.f, cy - h / 2.f, cx + w / 2.f, cy + h / 2.f};
+}
+
+// xy_to_cxcy (transforms.py:26-34).
+__device__ __forceinline__ Box4 xy_to_cxcy(Box4 x) {
+  return Box4{(x.c + x.a) / 2.f, (x.d + x.b) / 2.f, x.c - x.a, x.d - x.b};
+}
+
+// cxcy_to_gcxgcy (transforms.py:48-66): (c - pc) / (pwh / 10), log(wh / pwh) * 5.
+__device__ __forceinline__ Box4 encode_tenfive(Box4 c, Box4 p) {
+  return Box4{(c.a - p.a) / (p.c / 10.f), (c.b - p.b) / (p.d / 10.f), logf(c.c / p.c) * 5.f,
+              logf(c.d / p.d) * 5.f};
+}
+
+__device__ __forceinline__ Box4 ld4(const float *p) {
+  float4 v = *reinterpret_cast<const float4 *>(p);
+  return Box4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void st4(float *p, Box4 b) {
+  *reinterpret_cast<float4 *>(p) = make_float4(b.a, b.b, b.c, b.d);
+}
+
+}  // namespace sbod
