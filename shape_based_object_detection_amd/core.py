@@ -117,3 +117,93 @@ def codec(op, x, priors=None, var=(0.1, 0.2), out=None):
     L.call('sbod_codec_f32', L.CODEC[op], L.ptr(x), L.ptr(priors), n, prow, float(var[0]),
            float(var[1]), L.ptr(out), L.stream_of(x))
     return out
+
+
+# ----------------------------------------------------------------------------- fused criterion
+class CriterionSpec:
+    """Static description of one criterion (which losses, pools and normalisers)."""
+
+    __slots__ = ('reg', 'cls', 'flags', 'neg_pos_ratio', 'reg_weight', 'alpha', 'gamma')
+
+    def __init__(self, reg, cls, flags=0, neg_pos_ratio=3, reg_weight=1.0, alpha=0.25, gamma=2.0):
+        self.reg, self.cls, self.flags = reg, cls, flags
+        self.neg_pos_ratio, self.reg_weight = neg_pos_ratio, reg_weight
+        self.alpha, self.gamma = alpha, gamma
+
+
+class _FusedLoss(torch.autograd.Function):
+    """Forward computes the loss AND the gradients w.r.t. locs/scores in one pass (read once,
+    write once); backward applies the upstream scalar on the device (no host sync, no pass at
+    all when it is 1)."""
+
+    @staticmethod
+    def forward(ctx, locs, scores, run, want):
+        out, gl, gs = run(want)
+        ctx.save_for_backward(gl, gs)
+        ctx.consumed = False
+        ctx.set_materialize_grads(False)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.consumed:
+            raise RuntimeError('sbod fused criterion: backward through the same graph twice is not '
+                               'supported (its gradients are produced in forward)')
+        ctx.consumed = True
+        gl, gs = ctx.saved_tensors
+        if g is None or gl is None:
+            return None, None, None, None
+        g = g.detach().to(torch.float32).reshape(1).contiguous()
+        for t in (gl, gs):
+            L.call('sbod_scale_inplace', L.ptr(t), L.DT_F32 if t.dtype == torch.float32 else L.DT_BF16,
+                   t.numel(), L.ptr(g), L.stream_of(t))
+        return gl, gs, None, None
+
+
+def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, spec, threshold,
+                    neg_threshold, theta=0.01, arm_locs=None, arm_scores=None):
+    """Scalar loss (autograd-enabled) of one criterion pass; also returns the device vector
+    {total, conf, loc, n_pos_total} (no sync)."""
+    locs = locs.contiguous()
+    scores = scores.contiguous()
+    if locs.dtype not in (torch.float32, torch.bfloat16) or scores.dtype != locs.dtype:
+        raise TypeError('sbod criterion: locs/scores must both be float32 or bfloat16')
+    dt = L.DT_F32 if locs.dtype == torch.float32 else L.DT_BF16
+    B, P, C = scores.shape
+    if locs.shape != (B, P, 4) or priors_cxcy.shape[0] != P:
+        raise AssertionError('n_priors mismatch: priors %d, locs %s, scores %s'
+                             % (priors_cxcy.shape[0], tuple(locs.shape), tuple(scores.shape)))
+    dev = locs.device
+    stream = L.stream_of(locs)
+
+    holder = []
+
+    def run(want_grad):
+        out = torch.empty(4, dtype=torch.float32, device=dev)
+        holder.append(out)
+        gl = torch.empty_like(locs) if want_grad else None
+        gs = torch.empty_like(scores) if want_grad else None
+        nb = L.lib().sbod_loss_workspace_bytes(B, P)
+        ws = workspace(nb, dev)
+        L.call('sbod_multibox_loss', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy),
+               L.ptr(arm_locs), L.ptr(arm_scores), L.ptr(gt.boxes), L.ptr(gt.labels),
+               L.ptr(gt.offsets), L.ptr(obj), L.ptr(ovl), L.ptr(n_pos), L.ptr(npos_total),
+               float(threshold), float(neg_threshold), float(theta), spec.reg, spec.cls, spec.flags,
+               int(spec.neg_pos_ratio), float(spec.reg_weight), float(spec.alpha), float(spec.gamma),
+               L.ptr(gl), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
+        return out, gl, gs
+
+    want = torch.is_grad_enabled() and (locs.requires_grad or scores.requires_grad)
+    loss = _FusedLoss.apply(locs, scores, run, want)
+    return loss, holder[0]
+
+
+def allreduce_npos(n_pos, group=None):
+    """Data parallel: the global positive count (one 4-byte SUM all-reduce over RCCL, enqueued on
+    the current stream — no host sync).  Every rank then normalises by the global count, so the
+    per-rank gradients are exactly the global-batch gradient's slices."""
+    import torch.distributed as dist
+    tot = n_pos[-1:].clone()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
+    return tot

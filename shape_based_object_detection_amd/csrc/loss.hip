@@ -1,0 +1,718 @@
+// Detection losses: the fused per-prior criterion pass (every criterion of models/*.py), the
+// hard-negative mining top-k (radix select), the finaliser, and the standalone operators.Loss
+// kernels.
+//
+// Fused pass, one workgroup = 256 priors of one image:
+//   * the [256 x C] score tile is staged through LDS with coalesced loads (rows of C floats,
+//     C odd -> conflict-free per-lane row reads), softmax / focal / CE and their gradients are
+//     computed per lane in registers + LDS, and the gradient tile is stored back coalesced;
+//   * locs are one 16-byte load per lane; the label / positive / negative state is derived
+//     from the matcher's (obj, ovl) planes and the image's GT labels;
+//   * gradients are produced in the same pass (forward-with-grad), scaled by the global
+//     normaliser read from device memory (matcher total or an all-reduced copy for DP), so a
+//     training step reads the predictions once and writes their gradients once.
+// Roofline: HBM-bound; algorithmic bytes per launch = B*P*(4+C)*s read + B*P*(4+C)*s written.
+#include <hip/hip_bf16.h>
+
+#include "sbod_common.h"
+
+namespace sbod {
+
+constexpr int kLTile = 256;
+constexpr float kHalfBetaDefault = 0.5f / 9.f;
+
+__device__ __forceinline__ float ldf(const float *p) { return *p; }
+__device__ __forceinline__ float ldf(const uint16_t *p) {
+  return __uint_as_float(static_cast<uint32_t>(*p) << 16);
+}
+__device__ __forceinline__ void stf(float *p, float v) { *p = v; }
+__device__ __forceinline__ void stf(uint16_t *p, float v) {
+  __hip_bfloat16 h = __float2bfloat16(v);
+  *p = *reinterpret_cast<uint16_t *>(&h);
+}
+
+// torch.maximum / torch.minimum backward: on ties the gradient is split in half.
+__device__ __forceinline__ float dmax_a(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
+__device__ __forceinline__ float dmin_a(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
+
+struct OvOut {
+  float v;
+  float g[4];  // d v / d b1 (x1, y1, x2, y2)
+};
+
+// Row-wise IoU / GIoU / DIoU / CIoU of iou_utils.py:6-164 (forward in the reference's
+// evaluation order) and the hand-derived reverse mode of the same graph (clamp masks inclusive,
+// CIoU's alpha / arctan / w_temp treated as constants as under its torch.no_grad()).
+__device__ OvOut aligned_overlap(int kind, Box4 p, Box4 t, bool want_grad) {
+  const float x1 = p.a, y1 = p.b, x2 = p.c, y2 = p.d;
+  const float X1 = t.a, Y1 = t.b, X2 = t.c, Y2 = t.d;
+  const float w1 = x2 - x1, h1 = y2 - y1, w2 = X2 - X1, h2 = Y2 - Y1;
+  const float a1 = w1 * h1, a2 = w2 * h2;
+  const float ix2 = fminf(x2, X2), iy2 = fminf(y2, Y2), ix1 = fmaxf(x1, X1), iy1 = fmaxf(y1, Y1);
+  const float iwr = ix2 - ix1, ihr = iy2 - iy1;
+  const float iw = iwr < 0.f ? 0.f : iwr, ih = ihr < 0.f ? 0.f : ihr;
+  const float ia = iw * ih;
+  const float U = a1 + a2 - ia;
+  const float iou = ia / U;
+  float ow = 0.f, oh = 0.f, owr = 0.f, ohr = 0.f, ox2 = 0.f, oy2 = 0.f, ox1 = 0.f, oy1 = 0.f;
+  if (kind != SBOD_OV_IOU) {
+    ox2 = fmaxf(x2, X2);
+    oy2 = fmaxf(y2, Y2);
+    ox1 = fminf(x1, X1);
+    oy1 = fminf(y1, Y1);
+    owr = ox2 - ox1;
+    ohr = oy2 - oy1;
+    ow = owr < 0.f ? 0.f : owr;
+    oh = ohr < 0.f ? 0.f : ohr;
+  }
+  float raw, lo = -1.f;
+  // gradient seeds (for d raw)
+  float g_ia = 0.f, g_U = 0.f, g_ow = 0.f, g_oh = 0.f, g_cx1 = 0.f, g_cy1 = 0.f, g_w1 = 0.f, g_h1 = 0.f;
+  const float cx1 = (x2 + x1) / 2.f, cy1 = (y2 + y1) / 2.f;
+  const float cx2 = (X2 + X1) / 2.f, cy2 = (Y2 + Y1) / 2.f;
+  if (kind == SBOD_OV_IOU) {
+    raw = iou;
+    lo = 0.f;
+    g_ia = 1.f / U;
+    g_U = -iou / U;
+  } else if (kind == SBOD_OV_GIOU) {
+    const float C = ow * oh;
+    raw = iou - (C - U) / C;
+    g_ia = 1.f / U;
+    g_U = -iou / U + 1.f / C;
+    const float g_C = -U / (C * C);
+    g_ow = g_C * oh;
+    g_oh = g_C * ow;
+  } else {
+    const float dx = cx2 - cx1, dy = cy2 - cy1;
+    const float idiag = dx * dx + dy * dy;
+    const float odiag = ow * ow + oh * oh;
+    const float u = idiag / odiag;
+    float g_u = -1.f;
+    if (kind == SBOD_OV_DIOU) {
+      raw = iou - u;
+    } else {  // CIoU (iou_utils.py:84-93)
+      const float K4 = static_cast<float>(4.0 / (M_PI * M_PI));
+      const float K8 = static_cast<float>(8.0 / (M_PI * M_PI));
+      const float arct = atanf(w2 / h2) - atanf(w1 / h1);
+      const float v = K4 * (arct * arct);
+      const float S = 1.f - iou;
+      const float alpha = v / (S + v);
+      const float wt = 2.f * w1;
+      const float m = w1 - wt;
+      const float ar = (K8 * arct) * (m * h1);
+      raw = iou - (u + alpha * ar);
+      const float g_ar = -alpha;
+      g_w1 += g_ar * (K8 * arct) * h1;  // through m = w1 - w_temp (w_temp constant)
+      g_h1 += g_ar * (K8 * arct) * m;
+    }
+    g_ia = 1.f / U;
+    g_U = -iou / U;
+    const float g_idiag = g_u / odiag;
+    const float g_odiag = -g_u * idiag / (odiag * odiag);
+    g_cx1 = g_idiag * (-2.f * dx);
+    g_cy1 = g_idiag * (-2.f * dy);
+    g_ow = g_odiag * 2.f * ow;
+    g_oh = g_odiag * 2.f * oh;
+  }
+  OvOut r;
+  r.v = fminf(fmaxf(raw, lo), 1.f);
+  r.g[0] = r.g[1] = r.g[2] = r.g[3] = 0.f;
+  if (!want_grad || !(raw >= lo && raw <= 1.f)) return r;
+  // U = a1 + a2 - ia
+  const float g_a1 = g_U;
+  g_ia -= g_U;
+  g_w1 += g_a1 * h1;
+  g_h1 += g_a1 * w1;
+  const float g_iwr = iwr >= 0.f ? g_ia * ih : 0.f;
+  const float g_ihr = ihr >= 0.f ? g_ia * iw : 0.f;
+  float gx1 = -g_iwr * dmax_a(x1, X1), gx2 = g_iwr * dmin_a(x2, X2);
+  float gy1 = -g_ihr * dmax_a(y1, Y1), gy2 = g_ihr * dmin_a(y2, Y2);
+  if (kind != SBOD_OV_IOU) {
+    const float g_owr = owr >= 0.f ? g_ow : 0.f;
+    const float g_ohr = ohr >= 0.f ? g_oh : 0.f;
+    gx2 += g_owr * dmax_a(x2, X2);
+    gx1 -= g_owr * dmin_a(x1, X1);
+    gy2 += g_ohr * dmax_a(y2, Y2);
+    gy1 -= g_ohr * dmin_a(y1, Y1);
+  }
+  gx1 += 0.5f * g_cx1 - g_w1;
+  gx2 += 0.5f * g_cx1 + g_w1;
+  gy1 += 0.5f * g_cy1 - g_h1;
+  gy2 += 0.5f * g_cy1 + g_h1;
+  r.g[0] = gx1;
+  r.g[1] = gy1;
+  r.g[2] = gx2;
+  r.g[3] = gy2;
+  return r;
+}
+
+// d/d(gcxgcy) of cxcy_to_xy(gcxgcy_to_cxcy(g, prior)) given d/d(x1,y1,x2,y2).
+__device__ __forceinline__ void decode_backward(const float gb[4], Box4 g, Box4 pr, float out[4]) {
+  const float w = expf(g.c / 5.f) * pr.c, h = expf(g.d / 5.f) * pr.d;
+  const float gcx = gb[0] + gb[2], gcy = gb[1] + gb[3];
+  const float gw = 0.5f * (gb[2] - gb[0]), gh = 0.5f * (gb[3] - gb[1]);
+  out[0] = gcx * pr.c / 10.f;
+  out[1] = gcy * pr.d / 10.f;
+  out[2] = gw * w / 5.f;
+  out[3] = gh * h / 5.f;
+}
+
+__device__ __forceinline__ float powg(float x, float gamma) {
+  return gamma == 2.f ? x * x : powf(x, gamma);
+}
+__device__ __forceinline__ float powg1(float x, float gamma) {  // x^(gamma-1)
+  return gamma == 2.f ? x : powf(x, gamma - 1.f);
+}
+
+// Softmax-focal of one row (Loss.py:9-38): q = p_t; background rows weighted by p_bg (sic).
+// e[] holds exp(z - max) on entry; writes d loss / d z (times scale) into e[] when grad.
+// Returns the row loss (NaN when any class probability is exactly 0, as 0 * log 0 in the
+// reference).
+__device__ __forceinline__ float focal_row(float *e, int C, int t, float s, float afg, float abg,
+                                           float gamma, float scale, bool grad) {
+  const float inv = 1.f / s;
+  float pmin = 1.f;
+  for (int c = 0; c < C; ++c) pmin = fminf(pmin, e[c] * inv);
+  const float q = e[t] * inv;
+  const float lq = logf(q);
+  float loss, dq;
+  if (t == 0) {  // alpha_bg * p0^gamma * (-log p0)
+    loss = abg * powg(q, gamma) * -lq;
+    dq = abg * (gamma * powg1(q, gamma) * -lq - powg1(q, gamma));
+  } else {       // alpha_fg * (1 - p_t)^gamma * (-log p_t)
+    const float om = 1.f - q;
+    loss = afg * powg(om, gamma) * -lq;
+    dq = afg * (-gamma * powg1(om, gamma) * -lq - powg(om, gamma) / q);
+  }
+  if (!(pmin > 0.f)) loss = __builtin_nanf("");
+  if (grad) {
+    const float k = dq * q * scale;
+    for (int c = 0; c < C; ++c) {
+      const float pc = e[c] * inv;
+      e[c] = loss != loss ? loss : k * ((c == t ? 1.f : 0.f) - pc);
+    }
+  }
+  return loss;
+}
+
+struct LossArgs {
+  int B, P, C;
+  const float *priors, *arm_locs, *arm_scores, *gt;
+  const int64_t *labels;
+  const int32_t *off, *obj, *npos_total;
+  const float *ovl;
+  float thr, nthr, theta;
+  int reg, cls, flags;
+  float reg_weight, afg, abg, gamma;
+  float *partials, *pool;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__restrict__ locs,
+                                                     const T *__restrict__ scores,
+                                                     T *__restrict__ glocs, T *__restrict__ gsc) {
+  extern __shared__ float s_sc[];
+  __shared__ float s_red[16];
+  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x;
+  const int P = a.P, C = a.C;
+  const int np = min(kLTile, P - p0);
+  const int64_t rbase = static_cast<int64_t>(b) * P + p0;
+  const T *sbase = scores + rbase * C;
+  for (int i = tid; i < np * C; i += kLTile) s_sc[i] = ldf(sbase + i);
+  const float n = static_cast<float>(*a.npos_total);
+  const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
+  const bool grad = gsc != nullptr;
+  __syncthreads();
+  float conf_l = 0.f, loc_l = 0.f;
+  if (tid < np) {
+    const int p = p0 + tid;
+    const int64_t i = rbase + tid;
+    const int g = a.off[b] + a.obj[i];
+    const float v = a.ovl[i];
+    int c = v < a.thr ? 0 : static_cast<int>(a.labels[g]);
+    if (a.flags & SBOD_MATCH_BINARY) c = c > 0 ? 1 : 0;
+    const bool negrow = v < a.nthr;
+    bool easy = false;
+    if (odm) {  // RefineDet512.py:894-899
+      const float z0 = a.arm_scores[2 * i], z1 = a.arm_scores[2 * i + 1];
+      const float m = fmaxf(z0, z1);
+      const float e0 = expf(z0 - m), e1 = expf(z1 - m);
+      easy = e1 / (e0 + e1) < a.theta;
+    }
+    const bool pos = c > 0 && !easy;
+    // ---------------- box regression
+    float gl[4] = {0.f, 0.f, 0.f, 0.f};
+    if (pos) {
+      const Box4 lc{ldf(locs + 4 * i), ldf(locs + 4 * i + 1), ldf(locs + 4 * i + 2), ldf(locs + 4 * i + 3)};
+      const Box4 pri_cxcy = ld4(a.priors + 4 * static_cast<int64_t>(p));
+      const Box4 tb = ld4(a.gt + 4 * static_cast<int64_t>(g));
+      if (a.reg == SBOD_REG_DIOU) {  // SSD512.py:579-581: IouLoss(Diou) on decoded boxes
+        const Box4 d = decode_tenfive_xy(lc, pri_cxcy);
+        const OvOut r = aligned_overlap(SBOD_OV_DIOU, d, tb, grad);
+        loc_l += 1.f - r.v;
+        if (grad) {
+          const float s = -a.reg_weight / n;
+          const float gb[4] = {r.g[0] * s, r.g[1] * s, r.g[2] * s, r.g[3] * s};
+          decode_backward(gb, lc, pri_cxcy, gl);
+        }
+      } else {  // smooth-L1 (Loss.py:213-217) or L1 on encoded targets
+        const Box4 pr = odm ? xy_to_cxcy(decode_tenfive_xy(ld4(a.arm_locs + 4 * i), pri_cxcy)) : pri_cxcy;
+        const Box4 e = encode_tenfive(xy_to_cxcy(tb), pr);
+        const float lv[4] = {lc.a, lc.b, lc.c, lc.d}, ev[4] = {e.a, e.b, e.c, e.d};
+        const bool l1 = a.reg == SBOD_REG_L1;
+        const float beta = 1.f / 9.f;
+        const float s = l1 ? a.reg_weight / (4.f * n) : a.reg_weight / n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d = lv[k] - ev[k];
+          const float x = fabsf(d);
+          const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+          if (l1) {
+            loc_l += x;
+            gl[k] = sg * s;
+          } else if (x >= beta) {
+            loc_l += x - kHalfBetaDefault;
+            gl[k] = sg * s;
+          } else {
+            loc_l += 0.5f * (x * x) / beta;
+            gl[k] = (x / beta) * sg * s;
+          }
+        }
+      }
+    }
+    if (glocs) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
+    }
+    // ---------------- classification
+    float *row = s_sc + tid * C;
+    float m = row[0];
+    for (int k = 1; k < C; ++k) m = fmaxf(m, row[k]);
+    const float zt = row[c];
+    float s = 0.f;
+    for (int k = 0; k < C; ++k) {
+      const float e = expf(row[k] - m);
+      row[k] = e;
+      s += e;
+    }
+    if (a.cls == SBOD_CLS_FOCAL) {
+      if (pos || negrow) {  // SSD512.py:588-593: rows = positives ++ negatives(IoU < thr - 0.1)
+        const float scale = (a.flags & SBOD_LOSS_FOCAL_NORM) ? 1.f / n : 1.f;
+        conf_l += focal_row(row, C, c, s, a.afg, a.abg, a.gamma, scale, grad);
+      } else if (grad) {
+        for (int k = 0; k < C; ++k) row[k] = 0.f;
+      }
+    } else {
+      const float ce = -((zt - m) - logf(s));  // cross_entropy = -log_softmax[t]
+      if (pos) {
+        conf_l += ce;
+        a.pool[i] = -1.f;
+        if (grad) {
+          const float inv = 1.f / s, sc = 1.f / n;
+          for (int k = 0; k < C; ++k) row[k] = (row[k] * inv - (k == c ? 1.f : 0.f)) * sc;
+        }
+      } else {
+        bool member;
+        const int pool = a.flags & (SBOD_POOL_NEG | SBOD_POOL_GLOBAL_NEG | SBOD_POOL_NONPOS_NOT_EASY);
+        if (pool == SBOD_POOL_NEG || pool == SBOD_POOL_GLOBAL_NEG) member = negrow;
+        else if (pool == SBOD_POOL_NONPOS_NOT_EASY) member = !easy;
+        else member = true;
+        a.pool[i] = member ? ce : -1.f;
+        if (grad)
+          for (int k = 0; k < C; ++k) row[k] = 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  if (grad) {
+    T *gbase = gsc + rbase * C;
+    for (int i = tid; i < np * C; i += kLTile) stf(gbase + i, s_sc[i]);
+  }
+  conf_l = block_sum(conf_l, s_red);
+  loc_l = block_sum(loc_l, s_red + 8);
+  if (tid == 0) {
+    const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
+    a.partials[2 * blk] = conf_l;
+    a.partials[2 * blk + 1] = loc_l;
+  }
+}
+
+// ----------------------------------------------------------------------------- hard negatives
+// Per segment (one image, or the whole batch for SSD300's global pool) the sum of the k
+// largest pool values (k = ratio * positives), found by a 4-pass 8-bit radix select on the
+// float bits (pool values are >= 0; excluded rows hold -1).  Ties at the threshold take the
+// lowest indices.  Selected rows get the CE gradient (softmax - onehot(0)) / n_pos.
+constexpr int kHBlock = 1024;
+constexpr int kHWaves = kHBlock / 64;
+constexpr int kHStage = 32768;  // values staged in LDS when the segment fits
+
+__device__ __forceinline__ bool pool_key(float v, uint32_t &u) {
+  if (!(v >= 0.f)) return false;
+  u = __float_as_uint(v + 0.f);  // -0 -> +0
+  return true;
+}
+
+template <typename T, bool kStaged>
+__global__ __launch_bounds__(kHBlock) void k_hnm(const float *__restrict__ pool, int P, int B,
+                                                 int global, const int32_t *__restrict__ npos,
+                                                 int ratio, const T *__restrict__ scores,
+                                                 T *__restrict__ gsc, int C,
+                                                 const int32_t *__restrict__ npos_total,
+                                                 float *__restrict__ hnm_sum) {
+  extern __shared__ float s_val[];
+  __shared__ uint32_t s_hist[kHWaves][256];
+  __shared__ uint32_t s_tot[256];
+  __shared__ uint32_t s_state[4];  // prefix, kk, all, eq
+  __shared__ float s_red[16];
+  __shared__ int s_wcnt[kHWaves];
+  const int seg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t n = global ? static_cast<int64_t>(B) * P : P;
+  const int64_t base = global ? 0 : static_cast<int64_t>(seg) * P;
+  const int64_t k = static_cast<int64_t>(ratio) * (global ? npos[B] : npos[seg]);
+  const float *src = pool + base;
+  if (kStaged) {
+    for (int64_t i = tid; i < n; i += kHBlock) s_val[i] = src[i];
+    __syncthreads();
+  }
+  auto val = [&](int64_t i) -> float { return kStaged ? s_val[i] : src[i]; };
+  if (k <= 0) {
+    if (tid == 0) hnm_sum[seg] = 0.f;
+    return;
+  }
+  uint32_t prefix = 0, mask = 0;
+  int64_t kk = k;
+  bool all = false;
+  uint32_t eqcount = 0;
+  for (int level = 0; level < 4; ++level) {
+    const int shift = 24 - 8 * level;
+    for (int i = tid; i < kHWaves * 256; i += kHBlock) (&s_hist[0][0])[i] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += kHBlock) {
+      uint32_t u;
+      if (pool_key(val(i), u) && (u & mask) == prefix) atomicAdd(&s_hist[wv][(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t t = 0;
+      for (int w = 0; w < kHWaves; ++w) t += s_hist[w][tid];
+      s_tot[tid] = t;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t all_flag = 0;
+      if (level == 0) {
+        uint64_t total = 0;
+        for (int d = 0; d < 256; ++d) total += s_tot[d];
+        if (total <= static_cast<uint64_t>(kk)) all_flag = 1;
+      }
+      uint64_t acc = 0;
+      int d = 255;
+      if (!all_flag) {
+        for (; d > 0; --d) {
+          if (acc + s_tot[d] >= static_cast<uint64_t>(kk)) break;
+          acc += s_tot[d];
+        }
+      }
+      s_state[0] = prefix | (static_cast<uint32_t>(d) << shift);
+      s_state[1] = static_cast<uint32_t>(kk - static_cast<int64_t>(acc));
+      s_state[2] = all_flag;
+      s_state[3] = s_tot[d];
+    }
+    __syncthreads();
+    all = s_state[2] != 0;
+    if (all) break;
+    prefix = s_state[0];
+    kk = s_state[1];
+    eqcount = s_state[3];
+    mask |= 0xffu << shift;
+    __syncthreads();
+  }
+  const float nrm = 1.f / static_cast<float>(*npos_total);
+  const bool ordered = !all && eqcount > static_cast<uint32_t>(kk);
+  float sum = 0.f;
+  int64_t running = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kHBlock) {
+    const int64_t i = c0 + tid;
+    uint32_t u = 0;
+    const bool mem = i < n && pool_key(val(i), u);
+    bool sel = mem && (all || u > prefix || (u == prefix && !ordered));
+    if (ordered) {  // ties at the threshold: lowest indices first
+      const bool eq = mem && u == prefix;
+      const unsigned long long bal = __ballot(eq);
+      const int before = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) s_wcnt[wv] = __popcll(bal);
+      __syncthreads();
+      int64_t off = running;
+      for (int w = 0; w < wv; ++w) off += s_wcnt[w];
+      if (eq && off + before < kk) sel = true;
+      int64_t tot = 0;
+      for (int w = 0; w < kHWaves; ++w) tot += s_wcnt[w];
+      running += tot;
+      __syncthreads();
+    }
+    if (sel) {
+      sum += val(i);
+      if (gsc) {
+        const int64_t r = base + i;
+        const T *z = scores + r * C;
+        float m = ldf(z);
+        for (int q = 1; q < C; ++q) m = fmaxf(m, ldf(z + q));
+        float s = 0.f;
+        for (int q = 0; q < C; ++q) s += expf(ldf(z + q) - m);
+        const float inv = 1.f / s;
+        T *gz = gsc + r * C;
+        for (int q = 0; q < C; ++q) stf(gz + q, (expf(ldf(z + q) - m) * inv - (q == 0 ? 1.f : 0.f)) * nrm);
+      }
+    }
+  }
+  sum = block_sum(sum, s_red);
+  if (tid == 0) hnm_sum[seg] = sum;
+}
+
+__global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ partials, int nparts,
+                                                    const float *__restrict__ hnm, int nseg,
+                                                    const int32_t *__restrict__ npos_total, int reg,
+                                                    int cls, int flags, float reg_weight,
+                                                    float *__restrict__ out) {
+  __shared__ double s_red[16];
+  double c = 0.0, l = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    c += partials[2 * i];
+    l += partials[2 * i + 1];
+  }
+  for (int i = threadIdx.x; i < nseg; i += blockDim.x) c += hnm[i];
+  c = block_sum(c, s_red);
+  __syncthreads();
+  l = block_sum(l, s_red);
+  if (threadIdx.x == 0) {
+    const float n = static_cast<float>(*npos_total);
+    const float conf = (cls == SBOD_CLS_CE || (flags & SBOD_LOSS_FOCAL_NORM))
+                           ? static_cast<float>(c) / n : static_cast<float>(c);
+    const float loc = reg == SBOD_REG_L1 ? static_cast<float>(l) / (4.f * n) : static_cast<float>(l) / n;
+    out[0] = conf + reg_weight * loc;
+    out[1] = conf;
+    out[2] = loc;
+    out[3] = n;
+  }
+}
+
+// ----------------------------------------------------------------------------- standalone
+__global__ __launch_bounds__(256) void k_aligned(int kind, const float *__restrict__ b1,
+                                                 const float *__restrict__ b2, int64_t n,
+                                                 float *__restrict__ ov, float *__restrict__ g) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  OvOut r = aligned_overlap(kind, ld4(b1 + 4 * i), ld4(b2 + 4 * i), g != nullptr);
+  ov[i] = r.v;
+  if (g) st4(g + 4 * i, Box4{r.g[0], r.g[1], r.g[2], r.g[3]});
+}
+
+__global__ __launch_bounds__(256) void k_smooth_l1(const float *__restrict__ a,
+                                                   const float *__restrict__ b, int64_t n,
+                                                   float beta, float *__restrict__ loss,
+                                                   float *__restrict__ g) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float d = a[i] - b[i], x = fabsf(d);
+  const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+  const bool big = x >= beta;
+  loss[i] = big ? x - 0.5f * beta : 0.5f * (x * x) / beta;
+  if (g) g[i] = big ? sg : (x / beta) * sg;
+}
+
+__global__ __launch_bounds__(256) void k_focal_rows(int kind, const float *__restrict__ z,
+                                                    const int64_t *__restrict__ tgt, int64_t rows,
+                                                    int C, float afg, float abg, float gamma,
+                                                    float *__restrict__ loss, float *__restrict__ g) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const float *x = z + r * C;
+  float *gr = g ? g + r * C : nullptr;
+  const int t = static_cast<int>(tgt[r]);
+  float L = 0.f;
+  if (kind == SBOD_FOCAL_SOFTMAX) {
+    float m = x[0];
+    for (int c = 1; c < C; ++c) m = fmaxf(m, x[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += expf(x[c] - m);
+    const float inv = 1.f / s;
+    float pmin = 1.f;
+    for (int c = 0; c < C; ++c) pmin = fminf(pmin, expf(x[c] - m) * inv);
+    const float q = expf(x[t] - m) * inv, lq = logf(q);
+    float dq;
+    if (t == 0) {
+      L = abg * powg(q, gamma) * -lq;
+      dq = abg * (gamma * powg1(q, gamma) * -lq - powg1(q, gamma));
+    } else {
+      const float om = 1.f - q;
+      L = afg * powg(om, gamma) * -lq;
+      dq = afg * (-gamma * powg1(om, gamma) * -lq - powg(om, gamma) / q);
+    }
+    if (!(pmin > 0.f)) L = __builtin_nanf("");
+    if (gr)
+      for (int c = 0; c < C; ++c)
+        gr[c] = L != L ? L : dq * q * ((c == t ? 1.f : 0.f) - expf(x[c] - m) * inv);
+  } else if (kind == SBOD_FOCAL_SIGMOID) {  // Loss.py:48-80, column 0 excluded
+    if (gr) gr[0] = 0.f;
+    for (int c = 1; c < C; ++c) {
+      const float p = 1.f / (1.f + expf(-x[c]));
+      const float lp = logf(p), l1p = logf(1.f - p);
+      const float t1 = powg(1.f - p, gamma) * lp, t2 = powg(p, gamma) * l1p;
+      const float m1 = t == c ? 1.f : 0.f, m2 = (t != c && t > 0) ? 1.f : 0.f;
+      L += -(m1 * afg * t1) - (m2 * (1.f - afg) * t2);
+      if (gr) {
+        const float dp = p * (1.f - p);
+        const float d1 = -gamma * powg1(1.f - p, gamma) * lp + powg(1.f - p, gamma) / p;
+        const float d2 = gamma * powg1(p, gamma) * l1p - powg(p, gamma) / (1.f - p);
+        gr[c] = -(m1 * afg * d1 * dp) - (m2 * (1.f - afg) * d2 * dp);
+      }
+    }
+  } else {  // FocalLoss (Loss.py:91-103): BCE-with-logits, prediction clamped to [1e-4, 1-1e-4]
+    for (int c = 0; c < C; ++c) {
+      const float zc = x[c];
+      const float y = t == c ? 1.f : 0.f;
+      const float sg = 1.f / (1.f + expf(-zc));
+      const float pred = fminf(fmaxf(sg, 1e-4f), 1.f - 1e-4f);
+      const float mx = fmaxf(-zc, 0.f);
+      const float ce = (1.f - y) * zc + mx + logf(expf(-mx) + expf(-zc - mx));
+      const float al = y * afg + (1.f - y) * (1.f - afg);
+      const float pt = y == 1.f ? pred : 1.f - pred;
+      const float w = powg(1.f - pt, gamma);
+      L += al * w * ce;
+      if (gr) {
+        const float dpred = (sg >= 1e-4f && sg <= 1.f - 1e-4f) ? sg * (1.f - sg) : 0.f;
+        const float dpt = y == 1.f ? dpred : -dpred;
+        gr[c] = al * (-gamma * powg1(1.f - pt, gamma) * dpt * ce + w * (sg - y));
+      }
+    }
+  }
+  loss[r] = L;
+}
+
+}  // namespace sbod
+
+using namespace sbod;
+
+namespace {
+struct LossWs {
+  float *partials, *pool, *hnm;
+  size_t bytes;
+};
+LossWs carve(void *w, int B, int P) {
+  const size_t nblk = static_cast<size_t>(B) * ((P + kLTile - 1) / kLTile);
+  char *c = static_cast<char *>(w);
+  LossWs r;
+  r.partials = reinterpret_cast<float *>(c);
+  size_t o = align_up(nblk * 2 * sizeof(float));
+  r.pool = reinterpret_cast<float *>(c + o);
+  o += align_up(static_cast<size_t>(B) * P * sizeof(float));
+  r.hnm = reinterpret_cast<float *>(c + o);
+  o += align_up((B + 1) * sizeof(float));
+  r.bytes = o;
+  return r;
+}
+}  // namespace
+
+extern "C" {
+
+size_t sbod_loss_workspace_bytes(int B, int P) { return carve(nullptr, B, P).bytes; }
+
+int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, int P, int C,
+                       const float *priors_cxcy, const float *odm_arm_locs,
+                       const float *arm_scores, const float *gt_boxes, const int64_t *gt_labels,
+                       const int32_t *gt_offsets, const int32_t *obj, const float *ovl,
+                       const int32_t *n_pos, const int32_t *npos_total, float threshold,
+                       float neg_threshold, float theta, int reg, int cls, int flags,
+                       int neg_pos_ratio, float reg_weight, float focal_alpha, float focal_gamma,
+                       void *grad_locs, void *grad_scores, float *loss_out, void *workspace,
+                       size_t workspace_bytes, void *stream) {
+  SBOD_REQUIRE(B > 0 && P > 0 && C >= 2 && locs && scores && priors_cxcy && gt_boxes &&
+                   gt_labels && gt_offsets && obj && ovl && n_pos && npos_total && loss_out,
+               "sbod_multibox_loss: bad arguments (B=%d P=%d C=%d)", B, P, C);
+  SBOD_REQUIRE(dtype == SBOD_DT_F32 || dtype == SBOD_DT_BF16, "sbod_multibox_loss: dtype %d", dtype);
+  SBOD_REQUIRE(reg >= 0 && reg <= 2 && (cls == 0 || cls == 1), "sbod_multibox_loss: reg/cls");
+  SBOD_REQUIRE(C * kLTile * 4 <= 160 * 1024, "sbod_multibox_loss: C=%d too large for one LDS tile", C);
+  const bool odm = (flags & SBOD_MATCH_ODM) != 0;
+  SBOD_REQUIRE(!odm || (odm_arm_locs && arm_scores), "sbod_multibox_loss: ODM needs ARM locs/scores");
+  LossWs ws = carve(workspace, B, P);
+  if (workspace_bytes < ws.bytes) {
+    set_error("sbod_multibox_loss: workspace %zu < %zu", workspace_bytes, ws.bytes);
+    return SBOD_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  LossArgs a{B, P, C, priors_cxcy, odm_arm_locs, arm_scores, gt_boxes, gt_labels, gt_offsets, obj,
+             npos_total, ovl, threshold, neg_threshold, theta, reg, cls, flags, reg_weight,
+             focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool};
+  dim3 grid((P + kLTile - 1) / kLTile, B);
+  const size_t lds = static_cast<size_t>(kLTile) * C * sizeof(float);
+  if (dtype == SBOD_DT_F32)
+    hipLaunchKernelGGL(k_multibox<float>, grid, dim3(kLTile), lds, s, a,
+                       static_cast<const float *>(locs), static_cast<const float *>(scores),
+                       static_cast<float *>(grad_locs), static_cast<float *>(grad_scores));
+  else
+    hipLaunchKernelGGL(k_multibox<uint16_t>, grid, dim3(kLTile), lds, s, a,
+                       static_cast<const uint16_t *>(locs), static_cast<const uint16_t *>(scores),
+                       static_cast<uint16_t *>(grad_locs), static_cast<uint16_t *>(grad_scores));
+  SBOD_LAUNCHED("k_multibox");
+  int nseg = 0;
+  if (cls == SBOD_CLS_CE) {
+    const int global = (flags & SBOD_POOL_GLOBAL_NEG) ? 1 : 0;
+    nseg = global ? 1 : B;
+    const int64_t segn = global ? static_cast<int64_t>(B) * P : P;
+    const bool staged = segn <= kHStage;
+    const size_t hl = staged ? segn * sizeof(float) : 0;
+#define SBOD_HNM(T, ST)                                                                         \
+  hipLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, ws.pool, P, B, global,    \
+                     n_pos, neg_pos_ratio, static_cast<const T *>(scores), static_cast<T *>(grad_scores), C, \
+                     npos_total, ws.hnm)
+    if (dtype == SBOD_DT_F32) {
+      if (staged) SBOD_HNM(float, true); else SBOD_HNM(float, false);
+    } else {
+      if (staged) SBOD_HNM(uint16_t, true); else SBOD_HNM(uint16_t, false);
+    }
+#undef SBOD_HNM
+    SBOD_LAUNCHED("k_hnm");
+  }
+  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(256), 0, s, ws.partials,
+                     static_cast<int>(grid.x * grid.y), ws.hnm, nseg, npos_total, reg, cls, flags,
+                     reg_weight, loss_out);
+  SBOD_LAUNCHED("k_loss_final");
+  return SBOD_OK;
+}
+
+int sbod_aligned_overlap_f32(int kind, const float *b1, const float *b2, int64_t n,
+                             float *overlap, float *grad_b1, void *stream) {
+  SBOD_REQUIRE(kind >= 0 && kind <= 3 && n >= 0 && (n == 0 || (b1 && b2 && overlap)),
+               "sbod_aligned_overlap_f32: bad arguments");
+  if (n == 0) return SBOD_OK;
+  hipLaunchKernelGGL(k_aligned, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), kind, b1,
+                     b2, n, overlap, grad_b1);
+  SBOD_LAUNCHED("k_aligned");
+  return SBOD_OK;
+}
+
+int sbod_smooth_l1_f32(const float *pred, const float *target, int64_t n, float beta,
+                       float *loss, float *grad, void *stream) {
+  SBOD_REQUIRE(n >= 0 && (n == 0 || (pred && target && loss)), "sbod_smooth_l1_f32: bad arguments");
+  if (n == 0) return SBOD_OK;
+  hipLaunchKernelGGL(k_smooth_l1, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), pred,
+                     target, n, beta, loss, grad);
+  SBOD_LAUNCHED("k_smooth_l1");
+  return SBOD_OK;
+}
+
+int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t rows, int C,
+                   float alpha_fg, float alpha_bg, float gamma, float *row_loss, float *grad,
+                   void *stream) {
+  SBOD_REQUIRE(kind >= 0 && kind <= 2 && rows >= 0 && C >= 1 &&
+                   (rows == 0 || (logits && target && row_loss)),
+               "sbod_focal_f32: bad arguments");
+  if (rows == 0) return SBOD_OK;
+  hipLaunchKernelGGL(k_focal_rows, dim3((rows + 255) / 256), dim3(256), 0, as_stream(stream), kind,
+                     logits, target, rows, C, alpha_fg, alpha_bg, gamma, row_loss, grad);
+  SBOD_LAUNCHED("k_focal_rows");
+  return SBOD_OK;
+}
+
+}  // extern "C"

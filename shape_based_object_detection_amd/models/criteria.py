@@ -1,0 +1,183 @@
+"""Drop-in criteria: the reference's loss classes, same constructor/forward signatures, running
+the fused HIP path (matcher kernels + one fused loss pass + mining + finaliser).
+
+  * ``MultiBoxLoss512``  — ``models/SSD512.py:477-626``
+  * ``MultiBoxLoss300``  — ``models/SSD300.py:446-594`` (nn.L1Loss box loss, global mining pool)
+  * ``RetinaFocalLoss``  — ``models/RetinaNet.py:353-506`` (focal / n_pos, negatives-only pool)
+  * ``RefineDetLoss``    — ``models/RefineDet512.py:698-956`` (binary ARM + ODM on decoded ARM)
+
+Constructed as ``criterion(priors_cxcy=model.priors_cxcy, config=config)`` (train_anchor.py:172)
+with ``config`` exposing ``reg_weights, device, n_classes, reg_loss, cls_loss``; called as
+``criterion(locs [B,P,4], scores [B,P,C], boxes: list of [G_i,4], labels: list of [G_i])``.
+Returns a 0-d loss tensor with autograd.  ``last_components`` holds the device vector
+{total, conf, loc, n_pos} of the last call (no sync).
+
+Data parallelism: set ``distributed = True`` (optionally ``process_group``) and every rank
+normalises by the all-reduced positive count, so summing model gradients over ranks gives the
+single-device batch gradient.
+"""
+import torch
+from torch import nn
+
+from .. import _lib as L
+from .. import core
+from ..dataset.transforms import cxcy_to_xy
+
+
+def _cfg(config, key, default=None):
+    if isinstance(config, dict):
+        return config.get(key, default)
+    return getattr(config, key, default)
+
+
+class _AnchorCriterion(nn.Module):
+    KIND = 'ssd512'
+
+    def __init__(self, priors_cxcy, config, threshold=0.5, neg_pos_ratio=3):
+        super().__init__()
+        self.priors_cxcy = priors_cxcy
+        self.priors_xy = cxcy_to_xy(priors_cxcy)
+        self.threshold = threshold
+        self.neg_pos_ratio = neg_pos_ratio
+        self.alpha = _cfg(config, 'reg_weights', 1.0)
+        self.device = _cfg(config, 'device')
+        self.n_classes = _cfg(config, 'n_classes')
+        self.config = config
+        self.distributed = False
+        self.process_group = None
+        self.last_components = None
+
+    def increase_threshold(self, increment=0.1):
+        if self.threshold >= 0.7:
+            return
+        self.threshold += increment
+
+    def _spec(self):
+        reg_loss = str(_cfg(self.config, 'reg_loss', 'smoothl1')).upper()
+        cls_loss = str(_cfg(self.config, 'cls_loss', 'ce')).upper()
+        if reg_loss == 'DIOU':
+            reg = L.REG['diou']
+        else:
+            reg = L.REG['l1'] if self.KIND == 'ssd300' else L.REG['smoothl1']
+        if cls_loss == 'FOCAL':
+            cls = L.CLS['focal']
+            flags = L.LOSS_FOCAL_NORM if self.KIND == 'retina' else 0
+        else:
+            cls = L.CLS['ce']
+            flags = {'ssd512': L.POOL['nonpos'], 'ssd300': L.POOL['global_neg'],
+                     'retina': L.POOL['neg']}[self.KIND]
+            if self.KIND == 'ssd300' and self.distributed:
+                raise NotImplementedError('MultiBoxLoss300 CE mining pools negatives across the whole '
+                                          'batch (SSD300.py:580-588); a cross-rank top-k is not '
+                                          'implemented — use focal loss or one rank')
+        return core.CriterionSpec(reg, cls, flags, self.neg_pos_ratio, float(self.alpha))
+
+    def forward(self, predicted_locs, predicted_scores, boxes, labels):
+        L.require_device(predicted_locs, predicted_scores, what=type(self).__name__)
+        B, P, _ = predicted_scores.shape
+        n_priors = self.priors_cxcy.size(0)
+        assert n_priors == predicted_locs.size(1) == predicted_scores.size(1)
+        gt = core.pack_gt(boxes, labels)
+        obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold)
+        tot = core.allreduce_npos(npos, self.process_group) if self.distributed else npos[B:]
+        loss, comps = core.fused_criterion(predicted_locs, predicted_scores, gt, obj, ovl, npos, tot,
+                                           self.priors_cxcy, self._spec(), self.threshold,
+                                           self.threshold - 0.1)
+        self.last_components = comps
+        return loss
+
+
+class MultiBoxLoss512(_AnchorCriterion):
+    """``models/SSD512.py:477-626``: SmoothL1 (beta 1/9) or DIoU box loss; unnormalised softmax
+    focal over positives + negatives, or CE with per-image mining over all non-positives."""
+    KIND = 'ssd512'
+
+
+class MultiBoxLoss300(_AnchorCriterion):
+    """``models/SSD300.py:446-594``: nn.L1Loss (mean over elements) or DIoU; CE mining over the
+    negatives of the whole batch (global top sum(3 n_pos))."""
+    KIND = 'ssd300'
+
+
+class RetinaFocalLoss(_AnchorCriterion):
+    """``models/RetinaNet.py:353-506``: focal divided by the batch positives; CE mining over the
+    negatives (IoU < threshold - 0.1) of each image."""
+    KIND = 'retina'
+
+
+class RefineDetLoss(nn.Module):
+    """``models/RefineDet512.py:698-956``."""
+
+    def __init__(self, priors_cxcy, config, threshold=0.5, neg_pos_ratio=3, theta=0.01):
+        super().__init__()
+        self.priors_cxcy = priors_cxcy
+        self.priors_xy = cxcy_to_xy(priors_cxcy)
+        self.threshold = threshold
+        self.neg_pos_ratio = neg_pos_ratio
+        self.alpha = _cfg(config, 'reg_weights', 1.0)
+        self.device = _cfg(config, 'device')
+        self.n_classes = _cfg(config, 'n_classes')
+        self.config = config
+        self.theta = theta
+        self.distributed = False
+        self.process_group = None
+        self.last_components = None
+
+    def increase_threshold(self, increment=0.05):
+        if self.threshold + increment >= 0.7:
+            self.threshold = 0.7
+        else:
+            self.threshold += increment
+
+    def _tot(self, npos, B):
+        return core.allreduce_npos(npos, self.process_group) if self.distributed else npos[B:]
+
+    def compute_arm_loss(self, arm_locs, arm_scores, boxes, labels):
+        """Binary anchor-refinement loss vs the fixed priors (RefineDet512.py:730-820)."""
+        L.require_device(arm_locs, arm_scores, what='RefineDetLoss')
+        B, P, _ = arm_scores.shape
+        gt = core.pack_gt(boxes, labels)
+        obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold, flags=L.MATCH_BINARY)
+        spec = core.CriterionSpec(L.REG['smoothl1'], L.CLS['ce'], L.MATCH_BINARY | L.POOL['nonpos'],
+                                  self.neg_pos_ratio, float(self.alpha))
+        loss, comps = core.fused_criterion(arm_locs, arm_scores, gt, obj, ovl, npos,
+                                           self._tot(npos, B), self.priors_cxcy, spec, self.threshold,
+                                           self.threshold - 0.1)
+        self.last_components = comps
+        return loss
+
+    def compute_odm_loss(self, arm_locs, arm_scores, odm_locs, odm_scores, boxes, labels):
+        """Refined-detection loss vs the per-image decoded ARM boxes with easy negatives
+        (softmax(ARM)[...,1] < theta) removed (RefineDet512.py:822-939)."""
+        L.require_device(arm_locs, arm_scores, odm_locs, odm_scores, what='RefineDetLoss')
+        B, P, _ = odm_scores.shape
+        assert P == self.priors_cxcy.size(0) == odm_locs.size(1)
+        al = arm_locs.detach().contiguous().float()
+        asc = arm_scores.detach().contiguous().float()
+        gt = core.pack_gt(boxes, labels)
+        obj, ovl, npos = core.match(gt, al, P, self.threshold, flags=L.MATCH_ODM,
+                                    priors_cxcy=self.priors_cxcy, arm_scores=asc, theta=self.theta)
+        spec = core.CriterionSpec(L.REG['smoothl1'], L.CLS['ce'],
+                                  L.MATCH_ODM | L.POOL['nonpos_not_easy'], self.neg_pos_ratio,
+                                  float(self.alpha))
+        loss, comps = core.fused_criterion(odm_locs, odm_scores, gt, obj, ovl, npos, self._tot(npos, B),
+                                           self.priors_cxcy, spec, self.threshold, self.threshold - 0.1,
+                                           theta=self.theta, arm_locs=al, arm_scores=asc)
+        self.last_components = comps
+        return loss
+
+    def forward(self, arm_locs, arm_scores, odm_locs, odm_scores, boxes, labels):
+        arm = self.compute_arm_loss(arm_locs, arm_scores, boxes, labels)
+        odm = self.compute_odm_loss(arm_locs.detach(), arm_scores.detach(), odm_locs, odm_scores,
+                                    boxes, labels)
+        return arm + odm
+
+
+def criterion_entry(arch):
+    """The criterion half of ``models/__init__.py:model_entry`` (networks are out of scope)."""
+    a = arch.upper()
+    table = {'SSD300': MultiBoxLoss300, 'SSD512': MultiBoxLoss512, 'RETINA50': RetinaFocalLoss,
+             'RETINA101': RetinaFocalLoss, 'REFINEDET': RefineDetLoss}
+    if a not in table:
+        raise NotImplementedError('criterion for %s is not part of the sbod hot path' % arch)
+    return table[a]
