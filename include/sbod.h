@@ -50,7 +50,7 @@ const char *sbod_last_error(void);
  * mode SBOD_IOU_PLAIN).  out[b, g, p] for g < G_b; rows g >= G_b are left untouched.
  * anchors: [P,4] xyxy shared when anchor_batch_stride == 0, else image b reads
  * anchors + b * anchor_batch_stride (elements). */
-enum { SBOD_IOU_METRICS = 0, SBOD_IOU_PLAIN = 1 };
+enum { SBOD_IOU_METRICS = 0, SBOD_IOU_PLAIN = 1, SBOD_IOU_INTER = 2 /* intersection areas */ };
 int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int B, int Gmax,
                           const float *anchors, int64_t anchor_batch_stride, int P, int mode,
                           float *out, void *stream);
@@ -178,13 +178,17 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
  *            det_count [B] int32 (rows beyond count are unspecified);
  *            debug_probs [B,P,C] / debug_boxes [B,P,4] may be NULL.
  *   final_nms < 0 disables the detect_tools final class-agnostic NMS.
+ *   window: per-class candidate window (0 = auto: next_pow2(top_k + 1)).  Only the first top_k
+ *   outputs are observable, so NMS runs on each class's best `window` candidates; when a
+ *   candidate outside a truncated window could still reach the output, det_count[b] = -1 and the
+ *   caller re-runs with a larger window (results never depend on the window size).
  * Workspace: sbod_detect_workspace_bytes(B, P, C). */
 enum { SBOD_BOX_OFFSET = 0, SBOD_BOX_CENTER = 1, SBOD_BOX_CORNER = 2 };
 enum { SBOD_ACT_SOFTMAX = 0, SBOD_ACT_SIGMOID = 1 };
 size_t sbod_detect_workspace_bytes(int B, int P, int C);
 int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                     const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
-                    float min_score, float max_overlap, int top_k, float final_nms,
+                    float min_score, float max_overlap, int top_k, float final_nms, int window,
                     float *det_boxes, int64_t *det_labels, float *det_scores, int32_t *det_count,
                     float *debug_probs, float *debug_boxes, void *workspace,
                     size_t workspace_bytes, void *stream);

@@ -37,8 +37,8 @@ SIGNATURES = {
     'sbod_smooth_l1_f32': (I32, [P, P, I64, F32, P, P, P]),
     'sbod_focal_f32': (I32, [I32, P, P, I64, I32, F32, F32, F32, P, P, P]),
     'sbod_detect_workspace_bytes': (SZ, [I32, I32, I32]),
-    'sbod_detect_f32': (I32, [P, P, I32, I32, I32, P, P, I32, I32, F32, F32, I32, F32, P, P, P, P,
-                              P, P, P, SZ, P]),
+    'sbod_detect_f32': (I32, [P, P, I32, I32, I32, P, P, I32, I32, F32, F32, I32, F32, I32, P, P, P,
+                              P, P, P, P, SZ, P]),
     'sbod_nms_workspace_bytes': (SZ, [I64]),
     'sbod_nms_f32': (I32, [P, P, I64, F32, I32, I32, F32, P, P, P, SZ, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
@@ -48,7 +48,7 @@ SIGNATURES = {
 }
 
 # Constants of include/sbod.h.
-IOU_METRICS, IOU_PLAIN = 0, 1
+IOU_METRICS, IOU_PLAIN, IOU_INTER = 0, 1, 2
 MATCH_BINARY, MATCH_ODM = 1, 2
 CODEC = dict(xy_to_cxcy=0, cxcy_to_xy=1, encode_tenfive=2, decode_tenfive=3, encode_var=4,
              decode_var=5, decode_tenfive_xy=6)

@@ -207,3 +207,144 @@ def allreduce_npos(n_pos, group=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
     return tot
+
+
+# ----------------------------------------------------------------------------- detection
+def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='offset',
+           act='softmax', pos_mask=None, final_nms=None, debug=False, window=0):
+    """Batched decode + per-class NMS + top-k.  Returns (boxes, labels, scores) lists of per-image
+    tensors (views of batched device outputs).  ONE host sync: the per-image counts."""
+    L.require_device(locs, scores, what='detect')
+    B, P, C = scores.shape
+    if top_k <= 0:
+        raise ValueError('top_k must be positive')
+    dev = scores.device
+    sc = scores.contiguous().float()
+    in_place = box_type not in ('offset', 'center')
+    lc = locs if (locs.is_contiguous() and locs.dtype == torch.float32) else locs.contiguous().float()
+    if not in_place and lc is locs:
+        pass  # offset/center decode never writes the caller's tensor
+    pri = priors_cxcy.contiguous().float() if priors_cxcy is not None else None
+    pm = pos_mask.contiguous().to(torch.uint8) if pos_mask is not None else None
+    out_b = torch.empty(B, top_k, 4, dtype=torch.float32, device=dev)
+    out_l = torch.empty(B, top_k, dtype=torch.int64, device=dev)
+    out_s = torch.empty(B, top_k, dtype=torch.float32, device=dev)
+    cnt = torch.empty(B, dtype=torch.int32, device=dev)
+    dbg_p = torch.empty(B, P, C, dtype=torch.float32, device=dev) if debug else None
+    dbg_b = torch.empty(B, P, 4, dtype=torch.float32, device=dev) if debug else None
+    nb = L.lib().sbod_detect_workspace_bytes(B, P, C)
+    ws = workspace(nb, dev)
+    fn = -1.0 if final_nms is None else float(final_nms)
+    for w in (window, 4096):
+        L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
+               L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(w), L.ptr(out_b),
+               L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg_p), L.ptr(dbg_b), L.ptr(ws), nb,
+               L.stream_of(sc))
+        counts = cnt.cpu().tolist()
+        if min(counts) >= 0:
+            break
+    else:
+        raise L.SbodError('detect: a per-class candidate window of 4096 is not enough to decide the '
+                          'top-%d outputs exactly (pathological suppression); unsupported' % top_k)
+    if in_place and lc is not locs:
+        locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
+    res = ([out_b[b, :n] for b, n in enumerate(counts)], [out_l[b, :n] for b, n in enumerate(counts)],
+           [out_s[b, :n] for b, n in enumerate(counts)])
+    if debug:
+        return res, dbg_p, dbg_b
+    return res
+
+
+def nms(boxes, scores, overlap, top_k=0, variant='tv', beta1=1.0):
+    """Single-segment greedy NMS on the device. Returns (keep [n] int64 zero-padded, count tensor)."""
+    L.require_device(boxes, scores, what='nms')
+    n = boxes.shape[0]
+    b = boxes.contiguous().float()
+    s = scores.contiguous().float()
+    keep = torch.empty(n, dtype=torch.int64, device=boxes.device)
+    count = torch.empty(1, dtype=torch.int32, device=boxes.device)
+    nb = L.lib().sbod_nms_workspace_bytes(n)
+    ws = workspace(nb, boxes.device)
+    L.call('sbod_nms_f32', L.ptr(b), L.ptr(s), n, float(overlap), int(top_k), L.NMS[variant],
+           float(beta1), L.ptr(keep), L.ptr(count), L.ptr(ws), nb, L.stream_of(b))
+    return keep, count
+
+
+# ----------------------------------------------------------------------------- standalone losses
+class _RowOp(torch.autograd.Function):
+    """Per-row values + per-row local derivative from one kernel; backward = grad_out * local."""
+
+    @staticmethod
+    def forward(ctx, x, run, want):
+        val, local = run(want)
+        ctx.save_for_backward(local)
+        return val
+
+    @staticmethod
+    def backward(ctx, g):
+        (local,) = ctx.saved_tensors
+        if local is None:
+            return None, None, None
+        while g.dim() < local.dim():
+            g = g.unsqueeze(-1)
+        return g * local, None, None
+
+
+def aligned_overlap(kind, b1, b2):
+    """Row-wise IoU / GIoU / DIoU / CIoU [n] with autograd w.r.t. ``b1``."""
+    L.require_device(b1, b2, what='bbox_overlaps')
+    if b2.requires_grad and torch.is_grad_enabled():
+        raise NotImplementedError('sbod bbox_overlaps_*: gradients w.r.t. the second (target) box '
+                                  'set are not implemented')
+    n = b1.shape[0]
+    x1, x2 = b1.contiguous().float(), b2.detach().contiguous().float()
+
+    def run(want):
+        ov = torch.empty(n, dtype=torch.float32, device=b1.device)
+        g = torch.empty(n, 4, dtype=torch.float32, device=b1.device) if want else None
+        L.call('sbod_aligned_overlap_f32', L.OV[kind], L.ptr(x1), L.ptr(x2), n, L.ptr(ov), L.ptr(g),
+               L.stream_of(x1))
+        return ov, g
+
+    want = torch.is_grad_enabled() and b1.requires_grad
+    return _RowOp.apply(x1, run, want)
+
+
+def smooth_l1_elementwise(pred, target, beta):
+    L.require_device(pred, target, what='SmoothL1Loss')
+    p, t = pred.contiguous().float(), target.contiguous().float()
+    if p.shape != t.shape:
+        p, t = torch.broadcast_tensors(p, t)
+        p, t = p.contiguous(), t.contiguous()
+    n = p.numel()
+
+    def run(want):
+        loss = torch.empty_like(p)
+        g = torch.empty_like(p) if want else None
+        L.call('sbod_smooth_l1_f32', L.ptr(p), L.ptr(t), n, float(beta), L.ptr(loss), L.ptr(g),
+               L.stream_of(p))
+        return loss, g
+
+    want = torch.is_grad_enabled() and pred.requires_grad
+    out = _RowOp.apply(p, run, want)
+    if target.requires_grad and torch.is_grad_enabled():
+        raise NotImplementedError('sbod SmoothL1Loss: gradients w.r.t. target are not implemented')
+    return out
+
+
+def focal_rows(kind, logits, target, alpha_fg, alpha_bg, gamma):
+    """Per-row focal loss [rows] (softmax / sigmoid / bce forms) with autograd w.r.t. logits."""
+    L.require_device(logits, target, what='focal')
+    z = logits.contiguous().float()
+    y = target.contiguous().to(torch.int64)
+    rows, C = z.shape
+
+    def run(want):
+        loss = torch.empty(rows, dtype=torch.float32, device=z.device)
+        g = torch.empty_like(z) if want else None
+        L.call('sbod_focal_f32', L.FOCAL[kind], L.ptr(z), L.ptr(y), rows, C, float(alpha_fg),
+               float(alpha_bg), float(gamma), L.ptr(loss), L.ptr(g), L.stream_of(z))
+        return loss, g
+
+    want = torch.is_grad_enabled() and logits.requires_grad
+    return _RowOp.apply(z, run, want)

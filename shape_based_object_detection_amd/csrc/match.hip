@@ -186,10 +186,18 @@ __global__ __launch_bounds__(kTile) void k_iou_pairwise(const float *__restrict_
   float aarea = ax * ay;
   bool azero = (ax < kIouEps) && (ay < kIouEps);
   float *o = out + (static_cast<int64_t>(b) * Gmax) * P + p;
-  for (int g = 0; g < G; ++g)
-    o[static_cast<int64_t>(g) * P] = mode == SBOD_IOU_METRICS
-                                         ? iou_metrics(s_gt[g], q.a, q.b, q.c, q.d, aarea, azero)
-                                         : iou_plain(s_gt[g], q.a, q.b, q.c, q.d, aarea);
+  for (int g = 0; g < G; ++g) {
+    float v;
+    if (mode == SBOD_IOU_METRICS) {
+      v = iou_metrics(s_gt[g], q.a, q.b, q.c, q.d, aarea, azero);
+    } else if (mode == SBOD_IOU_PLAIN) {
+      v = iou_plain(s_gt[g], q.a, q.b, q.c, q.d, aarea);
+    } else {  // metrics.py:192-205 / iou_utils.py:192-212 intersect
+      const GtTile &t = s_gt[g];
+      v = fmaxf(fminf(t.x2, q.c) - fmaxf(t.x1, q.a), 0.f) * fmaxf(fminf(t.y2, q.d) - fmaxf(t.y1, q.b), 0.f);
+    }
+    o[static_cast<int64_t>(g) * P] = v;
+  }
 }
 
 // Matcher outputs -> the reference's per-prior tensors (parity tests / iou_utils API).

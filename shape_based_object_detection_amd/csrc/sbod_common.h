@@ -39,6 +39,12 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
+inline int next_pow2_host(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
 // Monotone float <-> uint32 mapping: a < b  <=>  ord(a) < ord(b) (for non-NaN floats).
 __device__ __forceinline__ uint32_t f2ord(float f) {
   uint32_t u = __float_as_uint(f);
