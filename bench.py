@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Throughput of the sbod hot path on MI355X (contract: one JSON line on rank 0).
+
+One step = one pass of the hot path over one batch of SSD512 synthetic input resident in HBM
+(SURVEY §8(d) recipe; BASELINE.json metric "images/sec train step SSD512 batch=32"):
+  1. MultiBoxLoss512 (DIoU box loss + softmax focal, the configs[1] losses) forward AND
+     backward through the drop-in criterion: ground-truth packing, the HIP matcher, the fused
+     loss+gradient pass, and the upstream-gradient application;
+  2. models.utils.detect on the same batch (softmax, offset decode + clamp, per-class NMS at
+     IoU 0.45, min_score 0.01, top_k 200), whose per-image lists need one device->host sync.
+Per-GPU batch is fixed (weak scaling); with N > 1 every rank owns its images and the loss
+normaliser (batch positives) is SUM-all-reduced over RCCL each step, as data-parallel training
+needs for exact single-device parity.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+from shape_based_object_detection_amd import _lib as L  # noqa: E402
+from shape_based_object_detection_amd import synth  # noqa: E402
+from shape_based_object_detection_amd.models import criteria as CR  # noqa: E402
+from shape_based_object_detection_amd.models import utils as MU  # noqa: E402
+from shape_based_object_detection_amd.models.priors import prior_table  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+N_CLASSES = 21
+ARCH = 'SSD512'
+
+
+class Cfg(dict):
+    __getattr__ = dict.__getitem__
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-sample-images', type=int, default=2)
+    return ap.parse_args()
+
+
+def make_batch(B, seed, dev):
+    P = prior_table(ARCH).shape[0]
+    boxes, labels = synth.make_gt(B, seed=seed, n_classes=N_CLASSES)
+    locs, scores = synth.make_preds(B, P, N_CLASSES, seed=seed)
+    det_scores = scores.clone()
+    det_scores[:, :, 0] += 6.0            # detection workload: +6 background logit (§8(d))
+    return ([b.to(dev) for b in boxes], [l.to(dev) for l in labels], locs.to(dev), scores.to(dev),
+            det_scores.to(dev))
+
+
+def bytes_per_step(B, P, C):
+    """Algorithmic HBM bytes of the fused loss pass: read locs+scores once,
+    write their gradients once, priors once per batch."""
+    return B * P * 2 * (4 + C) * 4 + 16 * P
+
+
+def cpu_baseline(B_sample, threads):
+    """The oracle (CPU restatement of the reference, pinned by tests/golden) on host cores:
+    criterion fwd+bwd on B_sample images + detect on B_sample images.  kind = 'port'."""
+    import numpy as np
+    from oracle import loss_ref as LR
+    from oracle import match_ref as M
+    torch.set_num_threads(threads)
+    Pn = prior_table(ARCH)
+    P = torch.from_numpy(Pn)
+    boxes, labels = synth.make_gt(B_sample, seed=0, n_classes=N_CLASSES)
+    locs, scores = synth.make_preds(B_sample, Pn.shape[0], N_CLASSES, seed=0)
+    det = scores.clone()
+    det[:, :, 0] += 6.0
+    t0 = time.perf_counter()
+    lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
+    loss = LR.criterion('ssd512', P, lo, sc, boxes, labels, 'diou', 'focal')
+    loss.backward()
+    t1 = time.perf_counter()
+    probs = torch.softmax(det, 2).numpy()
+    bx = M.decode_boxes(locs.numpy(), Pn, 'offset')
+    M.detect(probs, bx, 0.01, 0.45, 200)
+    t2 = time.perf_counter()
+    per_img = (t2 - t0) / B_sample
+    return {'value': round(1.0 / per_img, 4), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
+            'sample': '%d SSD512 images: oracle MultiBoxLoss512 (DIoU+focal) fwd+bwd %.2f s + oracle '
+                      'detect (numpy greedy NMS, torchvision semantics) %.2f s, torch/numpy on %d host '
+                      'threads' % (B_sample, t1 - t0, t2 - t1, threads)}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    L.lib()
+    B = a.batch
+    Pn = prior_table(ARCH)
+    P = Pn.shape[0]
+    priors = torch.from_numpy(Pn).to(dev)
+    cfg = Cfg(reg_weights=1.0, device=dev, n_classes=N_CLASSES, reg_loss='diou', cls_loss='focal',
+              focal_type='softmax', model={'box_type': 'offset'})
+    crit = CR.MultiBoxLoss512(priors_cxcy=priors, config=cfg)
+    crit.distributed = world > 1
+    boxes, labels, locs0, scores0, det_scores = make_batch(B, 1000 * rank, dev)
+    locs = locs0.clone().requires_grad_(True)
+    scores = scores0.clone().requires_grad_(True)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    loss_ms = []
+
+    def step(record=False):
+        locs.grad = None
+        scores.grad = None
+        if record:
+            ev[0].record()
+        loss = crit(locs, scores, boxes, labels)
+        loss.backward()
+        if record:
+            ev[1].record()
+        det = MU.detect(locs.detach(), det_scores, 0.01, 0.45, 200, priors, cfg)
+        return loss, det
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(record=True)
+        loss_ms.append((ev[0], ev[1]))
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    crit_ms = sorted(s.elapsed_time(e) for s, e in loss_ms)
+    crit_ms_med = crit_ms[len(crit_ms) // 2]
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    imgs = world * B * a.steps
+    value = imgs / elapsed
+    ms_step = elapsed / a.steps * 1e3
+    nbytes = bytes_per_step(B, P, N_CLASSES)
+    line = {
+        'metric': 'images/sec train step SSD512 batch=32 @1/2/4/8 GPU; IoU+NMS Manchors/sec',
+        'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': a.steps,
+        'warmup': a.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+        'config': {'workload': 'SSD512 per-GPU batch %d: MultiBoxLoss512(DIoU+focal) fwd+bwd + '
+                               'detect(min_score 0.01, iou 0.45, top_k 200)' % B,
+                   'global_batch': world * B, 'n_priors': P, 'n_classes': N_CLASSES,
+                   'parallelism': 'dp%d' % world},
+        'manchors_per_sec': round(world * B * P * a.steps / elapsed / 1e6, 3),
+        'criterion_fwd_bwd_ms_median': round(crit_ms_med, 4),
+        'criterion_GBps_algorithmic': round(nbytes / (crit_ms_med * 1e-3) / 1e9, 1),
+    }
+    if not a.no_cpu_baseline:
+        threads = min(os.cpu_count() or 1, 16)
+        line['cpu_baseline'] = cpu_baseline(a.cpu_sample_images, threads)
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -70,7 +70,8 @@ int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int 
  *   negative mask are derived from (obj, ovl, gt_labels) by the loss kernels.
  * Workspace: sbod_match_workspace_bytes(B, Gmax). */
 enum { SBOD_MATCH_BINARY = 1, SBOD_MATCH_ODM = 2 };
-size_t sbod_match_workspace_bytes(int B, int Gmax);
+size_t sbod_match_workspace_bytes(int B, int Gmax);          /* enough for P <= 2^20 */
+size_t sbod_match_workspace_bytes_p(int B, int Gmax, int P);  /* exact for this P */
 int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt_offsets,
                    int B, int Gmax, const float *anchors, const float *priors_cxcy,
                    const float *arm_scores, int P, float threshold, float theta, int flags,

@@ -50,13 +50,29 @@ def pack_gt(boxes, labels, device=None, allow_empty=False):
                            'ground-truth objects, as in the reference criterion)')
     device = device or boxes[0].device
     L.require_device(*boxes, *labels, what='pack_gt')
-    gb = torch.cat([b.reshape(-1, 4) for b in boxes]).to(torch.float32).contiguous()
-    gl = torch.cat([l.reshape(-1) for l in labels]).to(torch.int64).contiguous()
+    gb = torch.cat(boxes if boxes[0].dim() == 2 else [b.reshape(-1, 4) for b in boxes])
+    gl = torch.cat(labels if labels[0].dim() == 1 else [l.reshape(-1) for l in labels])
+    if gb.dtype != torch.float32:
+        gb = gb.float()
+    if gl.dtype != torch.int64:
+        gl = gl.long()
     return GtPack(gb, gl, _offsets_tensor(counts, device), counts)
 
 
-def workspace(nbytes, device):
-    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+_WS = {}
+
+
+def workspace(nbytes, device, slot='default'):
+    """Device scratch, cached per (device, current stream, slot) and grown on demand.  Reuse is
+    safe because every user of a slot runs in stream order on that stream."""
+    dev = torch.device(device)
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream if dev.type == 'cuda' else 0, slot)
+    buf = _WS.get(key)
+    n = max(int(nbytes), 1)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=dev)
+        _WS[key] = buf
+    return buf
 
 
 def iou_pairwise(gt, anchors, mode=L.IOU_METRICS, anchor_batch_stride=0):
@@ -78,8 +94,8 @@ def match(gt, anchors, P, threshold=0.5, flags=0, priors_cxcy=None, arm_scores=N
     obj = torch.empty(B, P, dtype=torch.int32, device=dev)
     ovl = torch.empty(B, P, dtype=torch.float32, device=dev)
     npos = torch.empty(B + 1, dtype=torch.int32, device=dev)
-    nb = L.lib().sbod_match_workspace_bytes(B, gt.gmax)
-    ws = workspace(nb, dev)
+    nb = L.lib().sbod_match_workspace_bytes_p(B, gt.gmax, P)
+    ws = workspace(nb, dev, 'match')
     L.call('sbod_match_f32', L.ptr(gt.boxes), L.ptr(gt.labels), L.ptr(gt.offsets), B, gt.gmax,
            L.ptr(anchors.contiguous()), L.ptr(priors_cxcy), L.ptr(arm_scores), P, float(threshold),
            float(theta), int(flags), L.ptr(obj), L.ptr(ovl), L.ptr(npos), L.ptr(ws), nb,
@@ -184,7 +200,7 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
         gl = torch.empty_like(locs) if want_grad else None
         gs = torch.empty_like(scores) if want_grad else None
         nb = L.lib().sbod_loss_workspace_bytes(B, P)
-        ws = workspace(nb, dev)
+        ws = workspace(nb, dev, 'loss')
         L.call('sbod_multibox_loss', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy),
                L.ptr(arm_locs), L.ptr(arm_scores), L.ptr(gt.boxes), L.ptr(gt.labels),
                L.ptr(gt.offsets), L.ptr(obj), L.ptr(ovl), L.ptr(n_pos), L.ptr(npos_total),
@@ -233,7 +249,7 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     dbg_p = torch.empty(B, P, C, dtype=torch.float32, device=dev) if debug else None
     dbg_b = torch.empty(B, P, 4, dtype=torch.float32, device=dev) if debug else None
     nb = L.lib().sbod_detect_workspace_bytes(B, P, C)
-    ws = workspace(nb, dev)
+    ws = workspace(nb, dev, 'detect')
     fn = -1.0 if final_nms is None else float(final_nms)
     for w in (window, 4096):
         L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
@@ -248,8 +264,11 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
                           'top-%d outputs exactly (pathological suppression); unsupported' % top_k)
     if in_place and lc is not locs:
         locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
-    res = ([out_b[b, :n] for b, n in enumerate(counts)], [out_l[b, :n] for b, n in enumerate(counts)],
-           [out_s[b, :n] for b, n in enumerate(counts)])
+    sizes = []
+    for n in counts:
+        sizes += [n, top_k - n]
+    res = (list(out_b.view(B * top_k, 4).split(sizes)[0::2]), list(out_l.view(-1).split(sizes)[0::2]),
+           list(out_s.view(-1).split(sizes)[0::2]))
     if debug:
         return res, dbg_p, dbg_b
     return res
@@ -264,7 +283,7 @@ def nms(boxes, scores, overlap, top_k=0, variant='tv', beta1=1.0):
     keep = torch.empty(n, dtype=torch.int64, device=boxes.device)
     count = torch.empty(1, dtype=torch.int32, device=boxes.device)
     nb = L.lib().sbod_nms_workspace_bytes(n)
-    ws = workspace(nb, boxes.device)
+    ws = workspace(nb, boxes.device, 'nms')
     L.call('sbod_nms_f32', L.ptr(b), L.ptr(s), n, float(overlap), int(top_k), L.NMS[variant],
            float(beta1), L.ptr(keep), L.ptr(count), L.ptr(ws), nb, L.stream_of(b))
     return keep, count

@@ -35,6 +35,49 @@ __device__ __forceinline__ void stf(uint16_t *p, float v) {
 __device__ __forceinline__ float dmax_a(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }
 __device__ __forceinline__ float dmin_a(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 
+// [n] floats global <-> LDS, 16 bytes per lane when the global side is 16-byte aligned.
+__device__ __forceinline__ void tile_load(float *dst, const float *src, int n) {
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    const int n4 = n >> 2;
+    const float4 *s4 = reinterpret_cast<const float4 *>(src);
+    float4 *d4 = reinterpret_cast<float4 *>(dst);
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
+    for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  }
+}
+__device__ __forceinline__ void tile_load(float *dst, const uint16_t *src, int n) {
+  if ((reinterpret_cast<uintptr_t>(src) & 7) == 0) {
+    const int n4 = n >> 2;
+    const uint2 *s4 = reinterpret_cast<const uint2 *>(src);
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+      const uint2 v = s4[i];
+      dst[4 * i] = __uint_as_float(v.x << 16);
+      dst[4 * i + 1] = __uint_as_float(v.x & 0xffff0000u);
+      dst[4 * i + 2] = __uint_as_float(v.y << 16);
+      dst[4 * i + 3] = __uint_as_float(v.y & 0xffff0000u);
+    }
+    for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = ldf(src + i);
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = ldf(src + i);
+  }
+}
+__device__ __forceinline__ void tile_store(float *dst, const float *src, int n) {
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int n4 = n >> 2;
+    float4 *d4 = reinterpret_cast<float4 *>(dst);
+    const float4 *s4 = reinterpret_cast<const float4 *>(src);
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
+    for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+  }
+}
+__device__ __forceinline__ void tile_store(uint16_t *dst, const float *src, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) stf(dst + i, src[i]);
+}
+
 struct OvOut {
   float v;
   float g[4];  // d v / d b1 (x1, y1, x2, y2)
@@ -218,8 +261,7 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
   const int P = a.P, C = a.C;
   const int np = min(kLTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
-  const T *sbase = scores + rbase * C;
-  for (int i = tid; i < np * C; i += kLTile) s_sc[i] = ldf(sbase + i);
+  tile_load(s_sc, scores + rbase * C, np * C);
   const float n = static_cast<float>(*a.npos_total);
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
   const bool grad = gsc != nullptr;
@@ -244,7 +286,11 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
     // ---------------- box regression
     float gl[4] = {0.f, 0.f, 0.f, 0.f};
     if (pos) {
-      const Box4 lc{ldf(locs + 4 * i), ldf(locs + 4 * i + 1), ldf(locs + 4 * i + 2), ldf(locs + 4 * i + 3)};
+      Box4 lc;
+      if constexpr (sizeof(T) == 4)
+        lc = ld4(reinterpret_cast<const float *>(locs) + 4 * i);
+      else
+        lc = Box4{ldf(locs + 4 * i), ldf(locs + 4 * i + 1), ldf(locs + 4 * i + 2), ldf(locs + 4 * i + 3)};
       const Box4 pri_cxcy = ld4(a.priors + 4 * static_cast<int64_t>(p));
       const Box4 tb = ld4(a.gt + 4 * static_cast<int64_t>(g));
       if (a.reg == SBOD_REG_DIOU) {  // SSD512.py:579-581: IouLoss(Diou) on decoded boxes
@@ -282,8 +328,12 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
       }
     }
     if (glocs) {
+      if constexpr (sizeof(T) == 4) {
+        st4(reinterpret_cast<float *>(glocs) + 4 * i, Box4{gl[0], gl[1], gl[2], gl[3]});
+      } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
+        for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
+      }
     }
     // ---------------- classification
     float *row = s_sc + tid * C;
@@ -325,10 +375,7 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
     }
   }
   __syncthreads();
-  if (grad) {
-    T *gbase = gsc + rbase * C;
-    for (int i = tid; i < np * C; i += kLTile) stf(gbase + i, s_sc[i]);
-  }
+  if (grad) tile_store(gsc + rbase * C, s_sc, np * C);
   conf_l = block_sum(conf_l, s_red);
   loc_l = block_sum(loc_l, s_red + 8);
   if (tid == 0) {

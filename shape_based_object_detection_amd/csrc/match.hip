@@ -68,20 +68,32 @@ __device__ __forceinline__ Anchor load_anchor(const float *anchors, const float 
   return Anchor{a.a, a.b, a.c, a.d, ax * ay, (ax < kIouEps) && (ay < kIouEps)};
 }
 
-// Phase 1: per prior the best object (first index on ties); per object the best prior as a
-// packed (ord(overlap) << 32 | ~prior) key reduced with atomicMax (max is order independent, so
-// the result is deterministic and equals torch's first-index argmax).
-template <bool kOdm>
+// Phase 1 (B x P/256 workgroups): per prior the best object (first index on ties) and the
+// tile's positive count before the forced match; per object the tile's best prior as a packed
+// (ord(overlap) << 32 | ~prior) key — waves reduce through LDS and each tile writes its own
+// partial row (no global atomics: the per-object argmax is finished deterministically by
+// phase 2, equal to torch's first-index argmax because max is order independent).
+constexpr int kMaxGLds = 256;   // objects per image whose per-wave partials stay in LDS
+
+template <bool kOdm, int kFlags>
 __global__ __launch_bounds__(kTile) void k_match_tile(
-    const float *__restrict__ gt, const int32_t *__restrict__ off, const float *__restrict__ anchors,
-    const float *__restrict__ priors, int P, int Gmax, int32_t *__restrict__ obj,
-    float *__restrict__ ovl, unsigned long long *__restrict__ objbest, int32_t *__restrict__ npos,
+    const float *__restrict__ gt, const int64_t *__restrict__ labels,
+    const int32_t *__restrict__ off, const float *__restrict__ anchors,
+    const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
+    float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
+    unsigned long long *__restrict__ part, int32_t *__restrict__ tcount, int32_t *__restrict__ npos,
     int B) {
   extern __shared__ GtTile s_gt[];
-  const int b = blockIdx.y;
+  __shared__ unsigned long long s_key[kTile / 64][kMaxGLds];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) npos[B] = 0;  // phase 2 accumulates
+  __shared__ int32_t s_lab[kMaxGLds];
+  __shared__ int s_red[16];
+  const int b = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ntile = gridDim.x;
   const int g0 = off[b], G = off[b + 1] - g0;
-  if (blockIdx.x == 0 && b == 0 && threadIdx.x == 0) npos[B] = 0;
   load_gt_tile(s_gt, gt, g0, G);
+  for (int i = threadIdx.x; i < G && i < kMaxGLds; i += blockDim.x)
+    s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
   __syncthreads();
   const int p = blockIdx.x * kTile + threadIdx.x;
   const bool valid = p < P;
@@ -90,81 +102,147 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
   float best = 0.f;
   int bi = 0;
   const unsigned long long low = 0xffffffffull - static_cast<uint32_t>(p);
+  unsigned long long *prow = part + (static_cast<int64_t>(b) * ntile + blockIdx.x) * Gmax;
   for (int g = 0; g < G; ++g) {
-    float ov = iou_metrics(s_gt[g], a.x1, a.y1, a.x2, a.y2, a.area, a.zero);
+    const float ov = iou_metrics(s_gt[g], a.x1, a.y1, a.x2, a.y2, a.area, a.zero);
     if (g == 0 || ov > best) {
       best = ov;
       bi = g;
     }
-    unsigned long long key =
-        valid ? ((static_cast<unsigned long long>(f2ord(ov)) << 32) | low) : 0ull;
+    unsigned long long key = valid ? ((static_cast<unsigned long long>(f2ord(ov)) << 32) | low) : 0ull;
     key = wave_max_u64(key);
-    if ((threadIdx.x & 63) == 0 && key) atomicMax(objbest + static_cast<int64_t>(b) * Gmax + g, key);
+    if (lane == 0) {
+      if (G <= kMaxGLds) s_key[wv][g] = key;
+      else if (key) atomicMax(prow + g, key);   // very large G: partial row via atomics
+    }
   }
+  int pos = 0;
   if (valid) {
     obj[static_cast<int64_t>(b) * P + p] = bi;
     ovl[static_cast<int64_t>(b) * P + p] = best;
+    const int lab = G <= kMaxGLds ? s_lab[bi] : static_cast<int>(labels[g0 + bi]);
+    int c = best < thr ? 0 : lab;
+    if ((kFlags & SBOD_MATCH_BINARY) != 0) c = c > 0;
+    pos = c > 0;
+    if constexpr (kOdm) {
+      const int64_t i = static_cast<int64_t>(b) * P + p;
+      const float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
+      const float m = fmaxf(z0, z1);
+      const float e0 = expf(z0 - m), e1 = expf(z1 - m);
+      if (e1 / (e0 + e1) < theta) pos = 0;
+    }
   }
+  pos = block_sum(pos, s_red);  // contains __syncthreads: s_key complete after it
+  if (G <= kMaxGLds) {
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+      unsigned long long k = s_key[0][g];
+      for (int w = 1; w < kTile / 64; ++w) k = s_key[w][g] > k ? s_key[w][g] : k;
+      prow[g] = k;
+    }
+  }
+  if (threadIdx.x == 0) tcount[b * ntile + blockIdx.x] = pos;
 }
 
-// Phase 2 (one workgroup per image): the forced match of models/SSD512.py:546-553 —
-// filter objects whose best overlap > 0, set overlap 1.0 and object j (the FILTERED position,
-// last writer wins) — then count positives for the loss normalisers.
+// Phase 2 (one wave per image): finish the per-object argmax over the tiles, then the forced
+// match of models/SSD512.py:546-553 applied serially — filter objects whose best overlap > 0,
+// overlap 1.0 and object j (the FILTERED position, last writer wins) — adjusting the positive
+// count for exactly the priors it rewrites.
 template <int kFlags>
-__global__ __launch_bounds__(1024) void k_match_final(
+__global__ __launch_bounds__(256) void k_match_final(
     const int64_t *__restrict__ labels, const int32_t *__restrict__ off,
-    const unsigned long long *__restrict__ objbest, int Gmax, int P, float thr,
-    const float *__restrict__ arm_scores, float theta, int32_t *__restrict__ obj,
-    float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
-  extern __shared__ int32_t s_i[];
-  int32_t *s_fp = s_i;             // forced prior per filtered j
-  int32_t *s_lab = s_i + Gmax;     // labels
-  __shared__ int s_nf;
+    const unsigned long long *__restrict__ part, const int32_t *__restrict__ tcount, int ntile,
+    int Gmax, int P, float thr, const float *__restrict__ arm_scores, float theta,
+    int32_t *__restrict__ obj, float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
+  // LDS per object g: best key, its prior, the prior's phase-1 (obj, ovl), easy flag, label
+  extern __shared__ unsigned long long s_best[];
+  int32_t *s_pr = reinterpret_cast<int32_t *>(s_best + Gmax);
+  int32_t *s_o0 = s_pr + Gmax;
+  float *s_v0 = reinterpret_cast<float *>(s_o0 + Gmax);
+  int32_t *s_lab = reinterpret_cast<int32_t *>(s_v0 + Gmax);
+  int32_t *s_easy = s_lab + Gmax;
+  int32_t *s_new = s_easy + Gmax;     // final object written for this g's prior, -1 = superseded
   __shared__ int s_red[16];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x;
   const int g0 = off[b], G = off[b + 1] - g0;
-  for (int i = threadIdx.x; i < G; i += blockDim.x) s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
-  if (threadIdx.x == 0) {
-    int nf = 0;
-    for (int g = 0; g < G; ++g) {
-      unsigned long long k = objbest[static_cast<int64_t>(b) * Gmax + g];
-      if (ord2f(static_cast<uint32_t>(k >> 32)) > 0.f)
-        s_fp[nf++] = static_cast<int32_t>(0xffffffffu - static_cast<uint32_t>(k));
-    }
-    s_nf = nf;
+  const unsigned long long *pb = part + static_cast<int64_t>(b) * ntile * Gmax;
+  for (int g = tid; g < G; g += blockDim.x) {
+    s_best[g] = 0ull;
+    s_lab[g] = static_cast<int32_t>(labels[g0 + g]);
   }
   __syncthreads();
-  const int nf = s_nf;
-  int cnt = 0;
-  for (int p = threadIdx.x; p < P; p += blockDim.x) {
-    const int64_t i = static_cast<int64_t>(b) * P + p;
-    int o = obj[i];
-    float v = ovl[i];
-    bool hit = false;
-    for (int f = 0; f < nf; ++f)
-      if (s_fp[f] == p) {
-        o = f;
-        hit = true;
-      }
-    if (hit) {
-      v = 1.0f;
-      obj[i] = o;
-      ovl[i] = v;
-    }
-    int c = v < thr ? 0 : s_lab[o];
-    bool pos = c > 0;
-    if constexpr ((kFlags & SBOD_MATCH_ODM) != 0) {
-      float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
-      float m = fmaxf(z0, z1);
-      float e0 = expf(z0 - m), e1 = expf(z1 - m);
-      if (e1 / (e0 + e1) < theta) pos = false;
-    }
-    cnt += pos ? 1 : 0;
+  for (int it = tid; it < G * ntile; it += blockDim.x) {   // all tile partials in flight at once
+    const int g = it / ntile, t = it - g * ntile;
+    atomicMax(&s_best[g], pb[static_cast<int64_t>(t) * Gmax + g]);
   }
+  int cnt = 0;
+  for (int t = tid; t < ntile; t += blockDim.x) cnt += tcount[b * ntile + t];
   cnt = block_sum(cnt, s_red);
-  if (threadIdx.x == 0) {
-    npos[b] = cnt;
-    atomicAdd(npos + B, cnt);
+  for (int g = tid; g < G; g += blockDim.x) {
+    const unsigned long long k = s_best[g];
+    int p = -1;
+    if (ord2f(static_cast<uint32_t>(k >> 32)) > 0.f) {
+      p = static_cast<int>(0xffffffffu - static_cast<uint32_t>(k));
+      const int64_t i = static_cast<int64_t>(b) * P + p;
+      s_o0[g] = obj[i];
+      s_v0[g] = ovl[i];
+      int easy = 0;
+      if constexpr ((kFlags & SBOD_MATCH_ODM) != 0) {
+        const float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
+        const float m = fmaxf(z0, z1);
+        const float e0 = expf(z0 - m), e1 = expf(z1 - m);
+        easy = e1 / (e0 + e1) < theta;
+      }
+      s_easy[g] = easy;
+    }
+    s_pr[g] = p;
+  }
+  __syncthreads();
+  // The forced match (SSD512.py:546-553) without a serial loop: object g's filtered position j_g
+  // is the number of valid objects before it; a prior forced more than once keeps its LAST
+  // writer, and each writer's "old" state is the previous writer's (or the phase-1 state).
+  for (int g = tid; g < G; g += blockDim.x) {
+    int j = 0, prev = -1;
+    const int p = s_pr[g];
+    for (int h = 0; h < g; ++h) {
+      const int ph = s_pr[h];
+      if (ph >= 0) {
+        ++j;
+        if (ph == p) prev = h;
+      }
+    }
+    s_o0[g] = p >= 0 ? s_o0[g] : 0;
+    s_new[g] = p >= 0 ? j : -1;
+    s_easy[g] = (s_easy[g] & 1) | (prev >= 0 ? ((prev + 1) << 1) : 0);  // pack prev into easy
+  }
+  __syncthreads();
+  auto is_pos = [&](int o, float v, int easy) {
+    int c = v < thr ? 0 : s_lab[o];
+    if ((kFlags & SBOD_MATCH_BINARY) != 0) c = c > 0;
+    return c > 0 && !easy;
+  };
+  int delta = 0;
+  for (int g = tid; g < G; g += blockDim.x) {
+    if (s_pr[g] < 0) continue;
+    const int easy = s_easy[g] & 1, prev = (s_easy[g] >> 1) - 1;
+    const int o_old = prev >= 0 ? s_new[prev] : s_o0[g];
+    const float v_old = prev >= 0 ? 1.0f : s_v0[g];
+    delta += (is_pos(s_new[g], 1.0f, easy) ? 1 : 0) - (is_pos(o_old, v_old, easy) ? 1 : 0);
+  }
+  delta = block_sum(delta, s_red);
+  for (int g = tid; g < G; g += blockDim.x) {
+    const int p = s_pr[g];
+    if (p < 0) continue;
+    bool last = true;                                  // superseded by a later writer?
+    for (int h = g + 1; h < G && last; ++h)
+      if (s_pr[h] == p) last = false;
+    if (!last) continue;
+    const int64_t i = static_cast<int64_t>(b) * P + p;
+    obj[i] = s_new[g];
+    ovl[i] = 1.0f;
+  }
+  if (tid == 0) {
+    npos[b] = cnt + delta;
+    atomicAdd(npos + B, cnt + delta);
   }
 }
 
@@ -314,10 +392,36 @@ __global__ __launch_bounds__(1024) void k_ssd_match_final(
 
 using namespace sbod;
 
+namespace {
+struct MatchWs {
+  unsigned long long *part, *best;
+  int32_t *tcount;
+  size_t bytes;
+};
+MatchWs carve_match(void *w, int B, int Gmax, int P) {
+  const size_t ntile = (P + kTile - 1) / kTile;
+  char *c = static_cast<char *>(w);
+  MatchWs r;
+  size_t o = 0;
+  r.part = reinterpret_cast<unsigned long long *>(c + o);
+  o += align_up(static_cast<size_t>(B) * ntile * Gmax * 8);
+  r.best = reinterpret_cast<unsigned long long *>(c + o);
+  o += align_up(static_cast<size_t>(B) * Gmax * 8);
+  r.tcount = reinterpret_cast<int32_t *>(c + o);
+  o += align_up(static_cast<size_t>(B) * ntile * 4);
+  r.bytes = o;
+  return r;
+}
+}  // namespace
+
 extern "C" {
 
+size_t sbod_match_workspace_bytes_p(int B, int Gmax, int P) {
+  return carve_match(nullptr, B, Gmax > 0 ? Gmax : 1, P > 0 ? P : 1).bytes;
+}
+
 size_t sbod_match_workspace_bytes(int B, int Gmax) {
-  return align_up(static_cast<size_t>(B) * (Gmax > 0 ? Gmax : 1) * sizeof(unsigned long long));
+  return sbod_match_workspace_bytes_p(B, Gmax, 1 << 20);
 }
 
 int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int B, int Gmax,
@@ -345,33 +449,41 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
   SBOD_REQUIRE(Gmax <= 4096, "sbod_match_f32: Gmax %d > 4096 unsupported", Gmax);
   const bool odm = (flags & SBOD_MATCH_ODM) != 0;
   SBOD_REQUIRE(!odm || (priors_cxcy && arm_scores), "sbod_match_f32: ODM needs priors and arm_scores");
-  if (workspace_bytes < sbod_match_workspace_bytes(B, Gmax)) {
-    set_error("sbod_match_f32: workspace %zu < %zu", workspace_bytes, sbod_match_workspace_bytes(B, Gmax));
+  const size_t need = sbod_match_workspace_bytes_p(B, Gmax, P);
+  if (workspace_bytes < need) {
+    set_error("sbod_match_f32: workspace %zu < %zu", workspace_bytes, need);
     return SBOD_E_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
-  auto *objbest = static_cast<unsigned long long *>(workspace);
-  if (hipMemsetAsync(objbest, 0, static_cast<size_t>(B) * Gmax * 8, s) != hipSuccess)
+  const int ntile = (P + kTile - 1) / kTile;
+  MatchWs w = carve_match(workspace, B, Gmax, P);
+  if (Gmax > kMaxGLds &&
+      hipMemsetAsync(w.part, 0, static_cast<size_t>(B) * ntile * Gmax * 8, s) != hipSuccess)
     return launch_status("hipMemsetAsync(match)");
-  dim3 grid((P + kTile - 1) / kTile, B);
+  dim3 grid(ntile, B);
   const size_t lds = Gmax * sizeof(GtTile);
-  if (odm)
-    hipLaunchKernelGGL(k_match_tile<true>, grid, dim3(kTile), lds, s, gt_boxes, gt_offsets,
-                       anchors, priors_cxcy, P, Gmax, obj, ovl, objbest, n_pos, B);
-  else
-    hipLaunchKernelGGL(k_match_tile<false>, grid, dim3(kTile), lds, s, gt_boxes, gt_offsets,
-                       anchors, priors_cxcy, P, Gmax, obj, ovl, objbest, n_pos, B);
-  SBOD_LAUNCHED("k_match_tile");
-  const size_t lds2 = 2 * Gmax * sizeof(int32_t);
-  if (odm)
-    hipLaunchKernelGGL(k_match_final<SBOD_MATCH_ODM>, dim3(B), dim3(1024), lds2, s, gt_labels,
-                       gt_offsets, objbest, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B);
-  else if (flags & SBOD_MATCH_BINARY)
-    hipLaunchKernelGGL(k_match_final<SBOD_MATCH_BINARY>, dim3(B), dim3(1024), lds2, s, gt_labels,
-                       gt_offsets, objbest, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B);
-  else
-    hipLaunchKernelGGL(k_match_final<0>, dim3(B), dim3(1024), lds2, s, gt_labels, gt_offsets,
-                       objbest, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B);
+#define SBOD_TILE(ODM, FL)                                                                      \
+  hipLaunchKernelGGL((k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, gt_boxes, gt_labels,     \
+                     gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, \
+                     ovl, w.part, w.tcount, n_pos, B)
+#define SBOD_FINAL(FL)                                                                          \
+  hipLaunchKernelGGL((k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, gt_labels, gt_offsets,  \
+                     w.part, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B)
+  if (odm) {
+    SBOD_TILE(true, SBOD_MATCH_ODM);
+    SBOD_LAUNCHED("k_match_tile");
+    SBOD_FINAL(SBOD_MATCH_ODM);
+  } else if (flags & SBOD_MATCH_BINARY) {
+    SBOD_TILE(false, SBOD_MATCH_BINARY);
+    SBOD_LAUNCHED("k_match_tile");
+    SBOD_FINAL(SBOD_MATCH_BINARY);
+  } else {
+    SBOD_TILE(false, 0);
+    SBOD_LAUNCHED("k_match_tile");
+    SBOD_FINAL(0);
+  }
+#undef SBOD_TILE
+#undef SBOD_FINAL
   SBOD_LAUNCHED("k_match_final");
   return SBOD_OK;
 }

@@ -25,7 +25,7 @@ constexpr int kDTile = 256;
 constexpr int kSegThreads = 256;
 constexpr int kMaxWindow = 4096;   // LDS-resident window (keys + boxes + areas + flags)
 constexpr int kMergeThreads = 1024;
-constexpr int kMergeStage = 3072;  // merged entries staged for the final class-agnostic NMS
+constexpr int kMergeStage = 2048;  // merged entries ordered for the final class-agnostic NMS (general path)
 
 __device__ __forceinline__ unsigned long long make_key(float score, uint32_t low) {
   return (static_cast<unsigned long long>(f2ord(score)) << 32) | (0xffffffffu - low);
@@ -45,7 +45,13 @@ __device__ __forceinline__ bool suppresses(const Box4 &bi, float ai, const Box4 
   const float w = fmaxf(xx2 - xx1, 0.f), h = fmaxf(yy2 - yy1, 0.f);
   const float inter = w * h;
   if constexpr (V == SBOD_NMS_TV) {
-    return inter / ((ai + aj) - inter) > thr;
+    const float u = (ai + aj) - inter;
+    if (u > 0.f && u < 3.0e38f) {       // decide without dividing unless within 2^-18 of thr
+      const float t = thr * u;
+      if (inter > t * (1.f + 3.8147e-6f)) return true;
+      if (inter < t * (1.f - 3.8147e-6f)) return false;
+    }
+    return inter / u > thr;
   } else {
     float iou = inter / ((aj - inter) + ai);
     if constexpr (V == SBOD_NMS_DIOU) {
@@ -63,19 +69,26 @@ __device__ __forceinline__ bool suppresses(const Box4 &bi, float ai, const Box4 
   }
 }
 
-// Descending bitonic sort of N (power of two) 64-bit keys in LDS.
+__device__ __forceinline__ int next_pow2(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Descending bitonic sort of N (power of two) 64-bit keys in LDS; every thread owns whole
+// compare-exchange pairs (no idle lanes).
 __device__ void bitonic_desc(unsigned long long *s, int N) {
+  const int half = N >> 1;
   for (int k = 2; k <= N; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long a = s[i], b = s[ixj];
-          const bool up = (i & k) == 0;
-          if (up ? (a < b) : (a > b)) {
-            s[i] = b;
-            s[ixj] = a;
-          }
+      for (int q = threadIdx.x; q < half; q += blockDim.x) {
+        const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));   // lower index of pair q
+        const int ixj = i | j;
+        const unsigned long long a = s[i], b = s[ixj];
+        const bool up = (i & k) == 0;
+        if (up ? (a < b) : (a > b)) {
+          s[i] = b;
+          s[ixj] = a;
         }
       }
       __syncthreads();
@@ -83,10 +96,76 @@ __device__ void bitonic_desc(unsigned long long *s, int N) {
   }
 }
 
-__device__ __forceinline__ int next_pow2(int x) {
-  int p = 1;
-  while (p < x) p <<= 1;
-  return p;
+// Top-R of n unique 64-bit keys held in LDS `in` (n > R): an 11-bit, 3-pass radix select on the
+// score half (bits 63..32) finds the R-th largest score T; every key with score >= T (R plus
+// ties at T) is gathered into `out` and bitonic-sorted.  Returns how many were gathered
+// (>= R; the first R of `out` are the exact top-R).  hist: 2048 u32 of LDS.
+__device__ int block_topk_lds(const unsigned long long *in, int n, int R, unsigned long long *out,
+                              int out_cap, uint32_t *hist, int *s_misc /* 4 */) {
+  uint32_t prefix = 0, mask = 0;
+  int kk = R;
+  const int shifts[3] = {21, 10, 0};
+  const int widths[3] = {11, 11, 10};
+  for (int level = 0; level < 3; ++level) {
+    const int sh = shifts[level], nb = 1 << widths[level];
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t u = static_cast<uint32_t>(in[i] >> 32);
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> sh) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    // suffix scan from the top bin: wave 0, 32 bins per lane
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x, per = nb / 64;
+      uint32_t mine = 0;
+      for (int t = 0; t < per; ++t) mine += hist[nb - 1 - (lane * per + t)];
+      uint32_t incl = mine;  // inclusive prefix over lanes (lane 0 = top bins)
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+      }
+      const uint32_t excl = incl - mine;
+      const bool hit = excl < static_cast<uint32_t>(kk) && incl >= static_cast<uint32_t>(kk);
+      if (hit) {
+        uint32_t acc = excl;
+        int bin = nb - 1 - lane * per;
+        for (int t = 0; t < per; ++t, --bin) {
+          const uint32_t h = hist[bin];
+          if (acc + h >= static_cast<uint32_t>(kk)) break;
+          acc += h;
+        }
+        s_misc[0] = bin;
+        s_misc[1] = kk - static_cast<int>(acc);
+      }
+    }
+    __syncthreads();
+    const int bin = s_misc[0];
+    const int left = s_misc[1];
+    prefix |= static_cast<uint32_t>(bin) << sh;
+    mask |= static_cast<uint32_t>(nb - 1) << sh;
+    // everything at or above this bin fits the output: stop refining, gather and sort it
+    const bool enough = (R - left) + static_cast<int>(hist[bin]) <= out_cap;
+    kk = left;
+    __syncthreads();
+    if (enough) break;
+  }
+  if (threadIdx.x == 0) s_misc[2] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const unsigned long long k = in[i];
+    if ((static_cast<uint32_t>(k >> 32) & mask) >= prefix) {
+      const int slot = atomicAdd(&s_misc[2], 1);
+      if (slot < out_cap) out[slot] = k;
+    }
+  }
+  __syncthreads();
+  const int m = s_misc[2];
+  const int N = next_pow2(max(min(m, out_cap), 2));
+  for (int i = min(m, out_cap) + threadIdx.x; i < N; i += blockDim.x) out[i] = 0ull;
+  __syncthreads();
+  bitonic_desc(out, N);
+  return m;
 }
 
 // Radix select over unique 64-bit keys in global memory: the largest T with
@@ -122,15 +201,19 @@ __device__ unsigned long long radix_select_desc(const unsigned long long *g, int
   return prefix;
 }
 
-// Block-level greedy NMS over n boxes sorted by descending score (LDS arrays).  Chunks of 64:
-// every wave tests the chunk against a slice of the already-kept boxes, then wave 0 resolves
-// the chunk's internal order with ballots.  keep[i] = 1 for kept.  Returns the kept count
-// (also the length of klist, kept positions in order).
+// Block-level greedy NMS over n boxes sorted by descending score (LDS arrays).  Chunks of 64
+// candidates: (A) every wave tests the chunk against a slice of the already-kept boxes, (B) the
+// 64 x 64 intra-chunk suppression matrix is split by rows over the waves, then (C) wave 0
+// resolves the chunk's greedy order with 64 wave-uniform column masks (ballots) — exactly the
+// sequential greedy result.  keep[i] = 1 for kept.  Returns the kept count; klist = kept
+// positions in order.  Stops at the first chunk boundary with >= stop_after kept.
 template <int V>
 __device__ int block_greedy(const Box4 *sb, const float *sa, int n, float thr, float beta,
-                            uint8_t *keep, int *klist, unsigned long long *s_flag /* 64 */,
-                            int *s_nk, int stop_after = 0x7fffffff) {
+                            uint8_t *keep, int *klist, unsigned long long *s_flag /* 16 */,
+                            unsigned long long *s_m /* 16 x 64 */, int *s_nk,
+                            int stop_after = 0x7fffffff) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int rpw = 64 / nw;  // chunk rows tested per wave
   if (threadIdx.x == 0) *s_nk = 0;
   __syncthreads();
   for (int s0 = 0; s0 < n; s0 += 64) {
@@ -138,37 +221,36 @@ __device__ int block_greedy(const Box4 *sb, const float *sa, int n, float thr, f
     if (nk >= stop_after) break;
     const int j = s0 + lane;
     const bool valid = j < n;
-    // phase A: against kept boxes of earlier chunks (waves split the kept list)
     bool sup = false;
+    unsigned long long m = 0;
     if (valid) {
       const Box4 bj = sb[j];
       const float aj = sa[j];
-      for (int k = wv; k < nk; k += nw) {
+      for (int k = wv; k < nk; k += nw) {          // (A)
         const int i = klist[k];
         if (suppresses<V>(sb[i], sa[i], bj, aj, thr, beta)) {
           sup = true;
           break;
         }
       }
+      const int i0 = wv * rpw, i1 = min(i0 + rpw, lane);
+      for (int i = i0; i < i1; ++i)                  // (B)
+        if (suppresses<V>(sb[s0 + i], sa[s0 + i], bj, aj, thr, beta)) m |= 1ull << i;
     }
     const unsigned long long bal = __ballot(sup);
     if (lane == 0) s_flag[wv] = bal;
+    s_m[wv * 64 + lane] = m;
     __syncthreads();
-    if (wv == 0) {
-      unsigned long long dead = 0;
-      for (int w = 0; w < nw; ++w) dead |= s_flag[w];
-      // phase B: intra-chunk, lane j collects which earlier chunk members would suppress it
-      unsigned long long m = 0;
-      if (valid) {
-        const Box4 bj = sb[j];
-        const float aj = sa[j];
-        for (int i = 0; i < lane; ++i)
-          if (suppresses<V>(sb[s0 + i], sa[s0 + i], bj, aj, thr, beta)) m |= 1ull << i;
+    if (wv == 0) {                                   // (C)
+      unsigned long long dead = 0, mm = 0;
+      for (int w = 0; w < nw; ++w) {
+        dead |= s_flag[w];
+        mm |= s_m[w * 64 + lane];
       }
       unsigned long long alive = __ballot(valid) & ~dead;
       unsigned long long kept = 0;
       for (int i = 0; i < 64; ++i) {
-        const unsigned long long col = __ballot((m >> i) & 1ull);  // members suppressed by i
+        const unsigned long long col = __ballot((mm >> i) & 1ull);  // members suppressed by i
         if ((alive >> i) & 1ull) {
           kept |= 1ull << i;
           alive &= ~col;
@@ -182,6 +264,64 @@ __device__ int block_greedy(const Box4 *sb, const float *sa, int n, float thr, f
     }
     __syncthreads();
   }
+  return *s_nk;
+}
+
+// Greedy NMS for n <= kMatrixMax sorted boxes: the upper-triangular suppression bit matrix is
+// computed fully in parallel (one thread per (row, 64-column block) item, 64 tests each, no
+// barriers), then wave 0 sweeps the rows in order with one alive bitset word per lane —
+// exactly the sequential greedy result.  keep/klist as block_greedy; stops after stop_after.
+constexpr int kMatrixMax = 512;
+
+template <int V>
+__device__ int block_greedy_matrix(const Box4 *sb, const float *sa, int n, float thr, float beta,
+                                   uint8_t *keep, int *klist,
+                                   unsigned long long *mat /* n x (kMatrixMax/64) */, int *s_nk,
+                                   int stop_after = 0x7fffffff) {
+  const int nb = (n + 63) >> 6;
+  const int W = nb;   // row stride in words
+  const int items = n * nb;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int i = it / nb, cb = it - i * nb;
+    unsigned long long bits = 0;
+    if (cb >= (i >> 6)) {
+      const Box4 bi = sb[i];
+      const float ai = sa[i];
+      const int j0 = max(cb << 6, i + 1), j1 = min((cb + 1) << 6, n);
+      for (int jj = j0; jj < j1; ++jj)
+        if (suppresses<V>(bi, ai, sb[jj], sa[jj], thr, beta)) bits |= 1ull << (jj & 63);
+    }
+    mat[i * W + cb] = bits;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const bool own = lane < nb;
+    unsigned long long alive = own ? (lane == nb - 1 && (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull) : 0ull;
+    unsigned long long row = own ? mat[lane] : 0ull;  // row 0, prefetched
+    int nk = 0;
+    for (int i = 0; i < n; ++i) {
+      const unsigned long long next = (own && i + 1 < n) ? mat[(i + 1) * W + lane] : 0ull;
+      const int wl = i >> 6;
+      const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(alive), wl);
+      const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(alive >> 32), wl);
+      const unsigned long long aw = (static_cast<unsigned long long>(hi) << 32) | lo;
+      const bool alive_i = (aw >> (i & 63)) & 1ull;
+      if (lane == 0) keep[i] = alive_i ? 1 : 0;
+      if (alive_i) {
+        if (lane == 0) klist[nk] = i;
+        ++nk;
+        if (nk >= stop_after) {
+          for (int r = i + 1 + lane; r < n; r += 64) keep[r] = 0;
+          break;
+        }
+        alive &= ~row;
+      }
+      row = next;
+    }
+  if (lane == 0) *s_nk = nk;
+  }
+  __syncthreads();
   return *s_nk;
 }
 
@@ -200,11 +340,13 @@ struct DetArgs {
 __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__restrict__ locs,
                                                         const float *__restrict__ scores) {
   extern __shared__ float s_sc[];
+  __shared__ unsigned long long s_bal[kDTile / 64][256];
+  __shared__ uint32_t s_base[256];
   const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
   const int P = a.P, C = a.C;
   const int np = min(kDTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
-  for (int i = tid; i < np * C; i += kDTile) s_sc[i] = scores[rbase * C + i];
+  tile_load_f32(s_sc, scores + rbase * C, np * C);
   __syncthreads();
   const bool valid = tid < np;
   const int p = p0 + tid;
@@ -238,19 +380,29 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
       for (int k = 0; k < C; ++k) row[k] = 1.f / (1.f + expf(-row[k]));
     }
   }
+  // candidate compaction: ballots per (wave, class) -> ONE atomic per (workgroup, class), all
+  // classes' atomics in flight together -> slots (order inside a segment is irrelevant: keys
+  // are unique and sorted later)
   const bool allowed = valid && (a.pos == nullptr || a.pos[i] != 0);
+  const int wv = tid >> 6;
   for (int c = 1; c < C; ++c) {
-    const float pc = valid ? row[c] : 0.f;
-    const bool take = allowed && pc > a.min_score;
+    const bool take = allowed && row[c] > a.min_score;
     const unsigned long long bal = __ballot(take);
-    if (bal == 0ull) continue;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(a.cand_count + b * C + c, static_cast<uint32_t>(__popcll(bal)));
-    base = __shfl(base, 0, 64);
-    if (take) {
-      const uint32_t slot = base + __popcll(bal & ((1ull << lane) - 1ull));
-      a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(pc, static_cast<uint32_t>(p));
-    }
+    if (lane == 0) s_bal[wv][c] = bal;
+  }
+  __syncthreads();
+  for (int c = tid + 1; c < C; c += kDTile) {
+    uint32_t n = 0;
+    for (int w = 0; w < kDTile / 64; ++w) n += __popcll(s_bal[w][c]);
+    s_base[c] = n ? atomicAdd(a.cand_count + b * C + c, n) : 0u;
+  }
+  __syncthreads();
+  for (int c = 1; c < C; ++c) {
+    const unsigned long long bal = s_bal[wv][c];
+    if (!((bal >> lane) & 1ull)) continue;
+    uint32_t slot = s_base[c] + __popcll(bal & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wv; ++w) slot += __popcll(s_bal[w][c]);
+    a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(row[c], static_cast<uint32_t>(p));
   }
   if (a.dbg_probs) {
     __syncthreads();
@@ -265,25 +417,35 @@ struct SegOut {
   unsigned long long *lastkey;// [B,C] the window's last candidate key when truncated, else 0
 };
 
+constexpr int kSegSortCap = 2048;  // segments up to this size are selected in LDS
+
 __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
-    const float *__restrict__ boxes_ws, int P, int C, int window, float thr, SegOut o) {
+    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
+    const int32_t *__restrict__ need) {
   extern __shared__ unsigned char s_raw[];
-  __shared__ uint32_t s_hist[256];
+  __shared__ uint32_t s_hist[2048];
   __shared__ unsigned long long s_st[2];
   __shared__ unsigned long long s_flag[16];
-  __shared__ int s_nk, s_cnt;
+  __shared__ unsigned long long s_m[kSegThreads];
+  __shared__ int s_nk, s_cnt, s_misc[4];
   const int c = blockIdx.x + 1, b = blockIdx.y;
   const int64_t seg = static_cast<int64_t>(b) * C + c;
+  // second pass: only the truncated classes of images whose merge could not decide
+  if (need != nullptr && (need[b] == 0 || o.lastkey[seg] == 0ull)) return;
   const int n = static_cast<int>(cand_count[seg]);
   const unsigned long long *g = cand + seg * P;
   const int q = min(n, window);
-  const int N = next_pow2(max(q, 2));
-  unsigned long long *sk = reinterpret_cast<unsigned long long *>(s_raw);   // [N]
-  Box4 *sb = reinterpret_cast<Box4 *>(sk + N);                                // [q]
-  float *sa = reinterpret_cast<float *>(sb + window);                         // [q]
-  int *kl = reinterpret_cast<int *>(sa + window);                             // [q]
-  uint8_t *kf = reinterpret_cast<uint8_t *>(kl + window);                     // [q]
+  // LDS: raw keys [kSegSortCap] | window keys [pow2(window)] | boxes, areas, klist, keep, matrix
+  unsigned long long *raw = reinterpret_cast<unsigned long long *>(s_raw);
+  const int WN = next_pow2(max(window, 2));
+  unsigned long long *sk = raw + kSegSortCap;
+  Box4 *sb = reinterpret_cast<Box4 *>(sk + WN);
+  float *sa = reinterpret_cast<float *>(sb + window);
+  int *kl = reinterpret_cast<int *>(sa + window);
+  uint8_t *kf = reinterpret_cast<uint8_t *>(kl + window);
+  unsigned long long *mat = reinterpret_cast<unsigned long long *>(
+      reinterpret_cast<uintptr_t>(kf + window + 15) & ~static_cast<uintptr_t>(15));
   if (n == 0) {
     if (threadIdx.x == 0) {
       o.kc[seg] = 0;
@@ -291,10 +453,26 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     }
     return;
   }
-  if (n <= window) {
+  if (n <= q) {  // whole segment fits the window
+    const int N = next_pow2(max(n, 2));
     for (int i = threadIdx.x; i < N; i += blockDim.x) sk[i] = i < n ? g[i] : 0ull;
+    __syncthreads();
+    bitonic_desc(sk, N);
+  } else if (n <= kSegSortCap) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) raw[i] = g[i];
+    __syncthreads();
+    const int m = block_topk_lds(raw, n, q, sk, WN, s_hist, s_misc);
+    if (m > WN) {  // pathological ties at the threshold: sort the whole segment instead
+      const int N = next_pow2(n);
+      for (int i = threadIdx.x; i < N; i += blockDim.x) raw[i] = i < n ? g[i] : 0ull;
+      __syncthreads();
+      bitonic_desc(raw, N);
+      for (int i = threadIdx.x; i < q; i += blockDim.x) sk[i] = raw[i];
+      __syncthreads();
+    }
   } else {
     const unsigned long long T = radix_select_desc(g, n, q, s_hist, s_st);
+    const int N = next_pow2(max(q, 2));
     if (threadIdx.x == 0) s_cnt = 0;
     for (int i = threadIdx.x; i < N; i += blockDim.x) sk[i] = 0ull;
     __syncthreads();
@@ -302,9 +480,9 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
       const unsigned long long k = g[i];
       if (k >= T) sk[atomicAdd(&s_cnt, 1)] = k;
     }
+    __syncthreads();
+    bitonic_desc(sk, N);
   }
-  __syncthreads();
-  bitonic_desc(sk, N);
   for (int i = threadIdx.x; i < q; i += blockDim.x) {
     const uint32_t p = key_low(sk[i]);
     const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
@@ -312,8 +490,10 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     sa[i] = (bx.c - bx.a) * (bx.d - bx.b);
   }
   __syncthreads();
-  const int nk = block_greedy<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, s_flag, &s_nk);
-  unsigned long long *ko = o.kept + seg * window;
+  const int nk = q <= kMatrixMax
+                     ? block_greedy_matrix<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, mat, &s_nk)
+                     : block_greedy<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, s_flag, s_m, &s_nk);
+  unsigned long long *ko = o.kept + seg * stride;
   for (int k = threadIdx.x; k < nk; k += blockDim.x) ko[k] = sk[kl[k]];
   if (threadIdx.x == 0) {
     o.kc[seg] = nk;
@@ -322,42 +502,80 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
 }
 
 // ----------------------------------------------------------------------------- K3
-constexpr int kMergeLdsKeys = 8192;  // merged keys sorted in LDS; beyond, radix-select first
+constexpr int kMergeLdsKeys = 8192;   // general path: merged keys sorted in LDS (radix-select first)
+constexpr int kRankScores = 8192;     // fast path: staged class-prefix merged keys
+constexpr int kFastOut = 1024;        // fast path: selected top-R (+ ties) keys
+constexpr int kFastStage = 512;       // fast path: merged prefix ordered for the final NMS
 
+// Count of entries of a non-increasing score list that precede score s in the merged order:
+// scores > s, plus scores == s when the list's class is lower (the concatenation is in class order).
+__device__ __forceinline__ int count_before(const float *a, int n, float s, bool ties_before) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const float v = a[mid];
+    if (v > s || (ties_before && v == s)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// pass: 0 = single pass (invalid -> count -1), 1 = first of two (invalid -> need[b] = 1),
+// 2 = second (only images with need[b]; invalid -> count -1).
 __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     const unsigned long long *__restrict__ kept, const uint32_t *__restrict__ kc,
     const unsigned long long *__restrict__ lastkey, const float *__restrict__ boxes_ws, int P,
-    int C, int window, int top_k, float final_nms, unsigned long long *__restrict__ scratch,
-    float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
-    int32_t *__restrict__ out_count) {
+    int C, int window, int top_k, float final_nms, int general, int pass,
+    int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
+    float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
+    float *__restrict__ out_scores, int32_t *__restrict__ out_count) {
   extern __shared__ unsigned char s_raw[];
-  __shared__ uint32_t s_off[257];
-  __shared__ uint32_t s_hist[256];
+  __shared__ uint32_t s_off[257], s_zoff[257];
+  __shared__ uint32_t s_hist[2048];
+  __shared__ int s_misc[4];
   __shared__ unsigned long long s_st[2];
   __shared__ float s_trunc;
   __shared__ int s_any_trunc, s_cnt;
   __shared__ unsigned long long s_flag[16];
+  __shared__ unsigned long long s_m[kMergeThreads];
   __shared__ int s_nk;
+  __shared__ uint32_t s_kc[256];
+  __shared__ float s_lk[256];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int64_t sb0 = static_cast<int64_t>(b) * C;
+  if (pass == 2 && need[b] == 0) return;
+  const int window_stride = window;
+  for (int c = tid; c < C; c += blockDim.x) {   // all per-class loads in flight together
+    s_kc[c] = c == 0 ? 0u : kc[sb0 + c];
+    const unsigned long long lk = c == 0 ? 0ull : lastkey[sb0 + c];
+    s_lk[c] = lk != 0ull ? key_score(lk) : __builtin_nanf("");
+  }
+  __syncthreads();
   if (tid == 0) {
     uint32_t acc = 0;
     float tr = -__builtin_inff();
     int any = 0;
     s_off[0] = 0;
     for (int c = 0; c < C; ++c) {
-      const uint32_t k = c == 0 ? 0u : kc[sb0 + c];
-      acc += k;
+      acc += s_kc[c];
       s_off[c + 1] = acc;
-      if (c > 0 && lastkey[sb0 + c] != 0ull) {
+      if (s_lk[c] == s_lk[c]) {
         any = 1;
-        tr = fmaxf(tr, key_score(lastkey[sb0 + c]));
+        tr = fmaxf(tr, s_lk[c]);
       }
     }
     s_trunc = tr;
     s_any_trunc = any;
   }
   __syncthreads();
+  // an undecidable image: ask for the second pass (pass 1) or report -1
+  auto undecided = [&]() {
+    if (tid == 0) {
+      if (pass == 1) need[b] = 1;
+      out_count[b] = -1;
+    }
+  };
+  if (pass == 1 && tid == 0) need[b] = 0;
   const int total = static_cast<int>(s_off[C]);
   const bool any_trunc = s_any_trunc != 0;
   const float trunc_score = s_trunc;
@@ -370,111 +588,164 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     ol[r] = c;
     os[r] = key_score(key);
   };
-  auto class_of = [&](int i) {
+  auto class_of = [&](const uint32_t *off, int i) {
     int c = 1;
-    while (s_off[c + 1] <= static_cast<uint32_t>(i)) ++c;
+    while (off[c + 1] <= static_cast<uint32_t>(i)) ++c;
     return c;
   };
+  auto ck_of = [&](int c, int pos) { return kept[(sb0 + c) * window_stride + pos]; };
   if (total == 0) {  // models/utils.py:274-277 placeholder
-    if (tid == 0) {
-      if (any_trunc) {
-        out_count[b] = -1;
-      } else {
-        st4(ob, Box4{0.f, 0.f, 1.f, 1.f});
-        ol[0] = 0;
-        os[0] = 0.f;
-        out_count[b] = 1;
-      }
+    if (any_trunc) {
+      undecided();
+    } else if (tid == 0) {
+      st4(ob, Box4{0.f, 0.f, 1.f, 1.f});
+      ol[0] = 0;
+      os[0] = 0.f;
+      out_count[b] = 1;
     }
     return;
   }
   if (final_nms < 0.f && !any_trunc && total <= top_k) {  // all kept, in class order
     for (int r = tid; r < total; r += blockDim.x) {
-      const int c = class_of(r);
-      emit(r, c, kept[(sb0 + c) * window + (r - s_off[c])]);
+      const int c = class_of(s_off, r);
+      emit(r, c, ck_of(c, r - s_off[c]));
     }
     if (tid == 0) out_count[b] = total;
     return;
   }
   if (final_nms < 0.f && total <= top_k) {  // a truncated window hides how many more exist
-    if (tid == 0) out_count[b] = -1;
+    undecided();
     return;
   }
-  // merged key = ord(score) << 32 | ~(class << 24 | position): the stable order of the
-  // class-order concatenation (models/utils.py:280-290, detect_tools.py:202)
-  auto merged_key = [&](int i) {
-    const int c = class_of(i);
-    const uint32_t pos = i - s_off[c];
-    const unsigned long long ck = kept[(sb0 + c) * window + pos];
-    return (ck & 0xffffffff00000000ull) | (0xffffffffu - ((static_cast<uint32_t>(c) << 24) | pos));
-  };
-  const int R = final_nms < 0.f ? min(total, top_k) : min(total, kMergeStage);
-  unsigned long long *sk = reinterpret_cast<unsigned long long *>(s_raw);
-  int N;
-  if (total <= kMergeLdsKeys) {
-    N = next_pow2(max(total, 2));
-    for (int i = tid; i < N; i += blockDim.x) sk[i] = i < total ? merged_key(i) : 0ull;
-  } else {
-    unsigned long long *g = scratch + static_cast<int64_t>(b) * (C - 1) * window;
-    for (int i = tid; i < total; i += blockDim.x) g[i] = merged_key(i);
-    __threadfence_block();
-    __syncthreads();
-    const unsigned long long T = radix_select_desc(g, total, R, s_hist, s_st);
-    N = next_pow2(max(R, 2));
-    if (tid == 0) s_cnt = 0;
-    for (int i = tid; i < N; i += blockDim.x) sk[i] = 0ull;
-    __syncthreads();
-    for (int i = tid; i < total; i += blockDim.x) {
-      const unsigned long long k = g[i];
-      if (k >= T) sk[atomicAdd(&s_cnt, 1)] = k;
+  // R = how many leading entries of the merged order are needed
+  const int R = final_nms < 0.f ? top_k : min(total, general ? kMergeStage : kFastStage);
+  int *ord = nullptr;          // ord[r] = class << 24 | position, r < R
+  unsigned long long *sk = nullptr;
+  bool fast = !general;
+  if (fast) {
+    if (tid == 0) {
+      uint32_t acc = 0;
+      s_zoff[0] = 0;
+      for (int c = 0; c < C; ++c) {
+        const uint32_t k = c == 0 ? 0u : min(kc[sb0 + c], static_cast<uint32_t>(R));
+        acc += k;
+        s_zoff[c + 1] = acc;
+      }
     }
+    __syncthreads();
+    fast = s_zoff[C] <= static_cast<uint32_t>(kRankScores);
   }
-  __syncthreads();
-  bitonic_desc(sk, N);
-  auto entry_key = [&](unsigned long long mk, int &c) {
-    const uint32_t lo = 0xffffffffu - static_cast<uint32_t>(mk);
-    c = static_cast<int>(lo >> 24);
-    return kept[(sb0 + c) * window + (lo & 0xffffffu)];
-  };
-  if (final_nms < 0.f) {  // n_objects > top_k: the top_k by score (models/utils.py:286-290)
-    if (any_trunc && !(key_score(sk[top_k - 1]) > trunc_score)) {
+  if (fast) {
+    // class prefixes (<= R each) -> LDS, then the exact top-R of their merged keys
+    unsigned long long *mk = reinterpret_cast<unsigned long long *>(s_raw);     // [kRankScores]
+    unsigned long long *top = mk + kRankScores;                                // [kFastOut]
+    ord = reinterpret_cast<int *>(top + kFastOut);                             // [R]
+    const int nz = static_cast<int>(s_zoff[C]);
+    for (int e = tid; e < nz; e += blockDim.x) {
+      const int c = class_of(s_zoff, e);
+      const uint32_t pos = e - s_zoff[c];
+      mk[e] = (ck_of(c, pos) & 0xffffffff00000000ull) |
+              (0xffffffffu - ((static_cast<uint32_t>(c) << 24) | pos));
+    }
+    __syncthreads();
+    int m;
+    if (nz <= R) {
+      const int N = next_pow2(max(nz, 2));
+      for (int i = tid; i < N; i += blockDim.x) top[i] = i < nz ? mk[i] : 0ull;
+      __syncthreads();
+      bitonic_desc(top, N);
+      m = nz;
+    } else {
+      m = block_topk_lds(mk, nz, R, top, kFastOut, s_hist, s_misc);
+    }
+    if (m > kFastOut) {  // pathological ties: re-run on the general path
       if (tid == 0) out_count[b] = -1;
       return;
     }
+    for (int r = tid; r < R; r += blockDim.x) ord[r] = static_cast<int>(0xffffffffu - static_cast<uint32_t>(top[r]));
+    __syncthreads();
+  } else {
+    // general path: sort merged keys (radix-select the leading R first when they do not fit)
+    sk = reinterpret_cast<unsigned long long *>(s_raw);
+    auto merged_key = [&](int i) {
+      const int c = class_of(s_off, i);
+      const uint32_t pos = i - s_off[c];
+      return (ck_of(c, pos) & 0xffffffff00000000ull) |
+             (0xffffffffu - ((static_cast<uint32_t>(c) << 24) | pos));
+    };
+    int N;
+    if (total <= kMergeLdsKeys) {
+      N = next_pow2(max(total, 2));
+      for (int i = tid; i < N; i += blockDim.x) sk[i] = i < total ? merged_key(i) : 0ull;
+    } else {
+      unsigned long long *g = scratch + static_cast<int64_t>(b) * C * window_stride;
+      for (int i = tid; i < total; i += blockDim.x) g[i] = merged_key(i);
+      __threadfence_block();
+      __syncthreads();
+      const unsigned long long T = radix_select_desc(g, total, R, s_hist, s_st);
+      N = next_pow2(max(R, 2));
+      if (tid == 0) s_cnt = 0;
+      for (int i = tid; i < N; i += blockDim.x) sk[i] = 0ull;
+      __syncthreads();
+      for (int i = tid; i < total; i += blockDim.x) {
+        const unsigned long long k = g[i];
+        if (k >= T) sk[atomicAdd(&s_cnt, 1)] = k;
+      }
+    }
+    __syncthreads();
+    bitonic_desc(sk, N);
+    ord = reinterpret_cast<int *>(sk + kMergeLdsKeys);
+    for (int r = tid; r < R; r += blockDim.x) ord[r] = static_cast<int>(0xffffffffu - static_cast<uint32_t>(sk[r]));
+    __syncthreads();
+  }
+  auto entry = [&](int r, int &c) {
+    const int v = ord[r];
+    c = v >> 24;
+    return ck_of(c, v & 0xffffff);
+  };
+  if (final_nms < 0.f) {  // n_objects > top_k: the top_k by score (models/utils.py:286-290)
+    int c;
+    if (any_trunc && !(key_score(entry(top_k - 1, c)) > trunc_score)) {
+      undecided();
+      return;
+    }
     for (int r = tid; r < top_k; r += blockDim.x) {
-      int c;
-      const unsigned long long ck = entry_key(sk[r], c);
+      const unsigned long long ck = entry(r, c);
       emit(r, c, ck);
     }
     if (tid == 0) out_count[b] = top_k;
     return;
   }
   // detect_tools: class-agnostic greedy NMS at final_nms over the merged order, first top_k
-  const int M = R;
-  Box4 *bx = reinterpret_cast<Box4 *>(sk + kMergeLdsKeys);
-  float *ar = reinterpret_cast<float *>(bx + kMergeStage);
-  int *kl = reinterpret_cast<int *>(ar + kMergeStage);
-  uint8_t *kf = reinterpret_cast<uint8_t *>(kl + kMergeStage);
-  for (int i = tid; i < M; i += blockDim.x) {
+  Box4 *bx = reinterpret_cast<Box4 *>(ord + kMergeStage);
+  float *ar = reinterpret_cast<float *>(bx + R);
+  int *kl = reinterpret_cast<int *>(ar + R);
+  uint8_t *kf = reinterpret_cast<uint8_t *>(kl + R);
+  unsigned long long *mat = reinterpret_cast<unsigned long long *>(
+      reinterpret_cast<uintptr_t>(kf + R + 15) & ~static_cast<uintptr_t>(15));
+  for (int i = tid; i < R; i += blockDim.x) {
     int c;
-    const unsigned long long ck = entry_key(sk[i], c);
+    const unsigned long long ck = entry(i, c);
     const Box4 q = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(ck)));
     bx[i] = q;
     ar[i] = (q.c - q.a) * (q.d - q.b);
   }
   __syncthreads();
-  const int nk = block_greedy<SBOD_NMS_TV>(bx, ar, M, final_nms, 1.f, kf, kl, s_flag, &s_nk, top_k);
+  const int nk = R <= kMatrixMax
+                     ? block_greedy_matrix<SBOD_NMS_TV>(bx, ar, R, final_nms, 1.f, kf, kl, mat, &s_nk, top_k)
+                     : block_greedy<SBOD_NMS_TV>(bx, ar, R, final_nms, 1.f, kf, kl, s_flag, s_m, &s_nk, top_k);
   const int nout = min(nk, top_k);
-  // complete if every candidate that could precede the top_k-th survivor was merged
-  const bool enough = nk >= top_k || (M == total && !any_trunc);
-  const bool ok = enough && (!any_trunc || key_score(sk[kl[top_k - 1]]) > trunc_score);
+  // complete if every candidate that could precede the top_k-th survivor was ordered
+  const bool enough = nk >= top_k || (R == total && !any_trunc);
+  int c0;
+  const bool ok = enough && (!any_trunc || key_score(entry(kl[top_k - 1], c0)) > trunc_score);
   if (!ok) {
-    if (tid == 0) out_count[b] = -1;
+    undecided();
     return;
   }
   for (int r = tid; r < nout; r += blockDim.x) {
     int c;
-    const unsigned long long ck = entry_key(sk[kl[r]], c);
+    const unsigned long long ck = entry(kl[r], c);
     emit(r, c, ck);
   }
   if (tid == 0) out_count[b] = nout;
@@ -492,6 +763,7 @@ __global__ __launch_bounds__(1024) void k_nms_single(const float *__restrict__ b
   __shared__ uint32_t s_hist[256];
   __shared__ unsigned long long s_st[2];
   __shared__ unsigned long long s_flag[16];
+  __shared__ unsigned long long s_m[1024];
   __shared__ int s_nk, s_cnt;
   const int N = next_pow2(max(q, 2));
   unsigned long long *sk = reinterpret_cast<unsigned long long *>(s_raw);
@@ -522,13 +794,19 @@ __global__ __launch_bounds__(1024) void k_nms_single(const float *__restrict__ b
     sa[i] = (bx.c - bx.a) * (bx.d - bx.b);
   }
   __syncthreads();
-  const int nk = block_greedy<V>(sb, sa, q, thr, beta, kf, kl, s_flag, &s_nk);
+  const int nk = block_greedy<V>(sb, sa, q, thr, beta, kf, kl, s_flag, s_m, &s_nk);
   for (int k = threadIdx.x; k < n; k += blockDim.x) keep[k] = k < nk ? static_cast<int64_t>(key_low(sk[kl[k]])) : 0;
   if (threadIdx.x == 0) *count = nk;
 }
 
 size_t seg_lds(int window) {
-  return static_cast<size_t>(next_pow2_host(window)) * 8 + static_cast<size_t>(window) * (16 + 4 + 4 + 1) + 64;
+  const size_t wn = next_pow2_host(window < 2 ? 2 : window);
+  const size_t mat = window <= kMatrixMax ? static_cast<size_t>(window) * ((window + 63) / 64) * 8 : 0;
+  return static_cast<size_t>(kSegSortCap) * 8 + wn * 8 + static_cast<size_t>(window) * (16 + 4 + 4 + 1) + 16 + mat;
+}
+
+size_t single_lds(int q) {
+  return static_cast<size_t>(next_pow2_host(q < 2 ? 2 : q)) * 8 + static_cast<size_t>(q) * (16 + 4 + 4 + 1) + 64;
 }
 
 }  // namespace sbod
@@ -540,6 +818,7 @@ struct DetWs {
   float *boxes;
   unsigned long long *cand, *kept, *lastkey, *scratch;
   uint32_t *count, *kc;
+  int32_t *need;
   size_t bytes;
 };
 DetWs carve_det(void *w, int B, int P, int C, int window) {
@@ -560,21 +839,23 @@ DetWs carve_det(void *w, int B, int P, int C, int window) {
   o += align_up(static_cast<size_t>(B) * C * 8);
   r.scratch = reinterpret_cast<unsigned long long *>(c + o);
   o += align_up(static_cast<size_t>(B) * C * window * 8);
+  r.need = reinterpret_cast<int32_t *>(c + o);
+  o += align_up(static_cast<size_t>(B) * 4);
   r.bytes = o;
   return r;
 }
-int window_for(int P, int top_k, int window) {
-  int w = window > 0 ? window : next_pow2_host(top_k + 1 > 64 ? top_k + 1 : 64);
+constexpr int kFirstWindow = 64;
+int clampw(int w, int P) {
   if (w > kMaxWindow) w = kMaxWindow;
   if (w > P) w = P < 1 ? 1 : P;
-  return w;
+  return w < 1 ? 1 : w;
 }
 }  // namespace
 
 extern "C" {
 
 size_t sbod_detect_workspace_bytes(int B, int P, int C) {
-  return carve_det(nullptr, B, P, C, kMaxWindow < P ? kMaxWindow : P).bytes;
+  return carve_det(nullptr, B, P, C, clampw(kMaxWindow, P)).bytes;
 }
 
 int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
@@ -589,15 +870,26 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   SBOD_REQUIRE(box_type != SBOD_BOX_OFFSET || priors_cxcy, "sbod_detect_f32: offset boxes need priors");
   SBOD_REQUIRE(C * kDTile * 4 <= 160 * 1024, "sbod_detect_f32: C=%d too large", C);
   SBOD_REQUIRE(P < (1 << 24), "sbod_detect_f32: P=%d >= 2^24 unsupported", P);
-  const int w = window_for(P, top_k, window);
-  DetWs ws = carve_det(workspace, B, P, C, w);
+  // window 0 (auto): a first window of 64 candidates per class, then next_pow2(top_k + 1) for
+  // the truncated classes of images the first merge could not decide; window > 0: one pass.
+  const bool two = window <= 0;
+  const int w2 = clampw(two ? next_pow2_host(top_k + 1 > 64 ? top_k + 1 : 64) : window, P);
+  const int w1 = two ? clampw(kFirstWindow < w2 ? kFirstWindow : w2, P) : w2;
+  DetWs ws = carve_det(workspace, B, P, C, w2);
   if (workspace_bytes < ws.bytes) {
     set_error("sbod_detect_f32: workspace %zu < %zu", workspace_bytes, ws.bytes);
     return SBOD_E_WORKSPACE;
   }
-  SBOD_REQUIRE(top_k <= kMergeLdsKeys, "sbod_detect_f32: top_k %d > %d unsupported", top_k, kMergeLdsKeys);
-  const size_t merge_lds = static_cast<size_t>(kMergeLdsKeys) * 8 +
-                           (final_nms >= 0.f ? static_cast<size_t>(kMergeStage) * 25 : 0);
+  SBOD_REQUIRE(top_k <= kMergeStage, "sbod_detect_f32: top_k %d > %d unsupported", top_k, kMergeStage);
+  const int general = w2 >= kMaxWindow ? 1 : 0;   // the retry window takes the general merge
+  // fast path: keys [kRankScores] + top [kFastOut] | general: keys [kMergeLdsKeys]; then ord
+  // [kMergeStage] and, for the final NMS, boxes/areas/klist/keep [R] + the bit matrix
+  const size_t head = static_cast<size_t>(kRankScores + kFastOut) * 8 > static_cast<size_t>(kMergeLdsKeys) * 8
+                          ? static_cast<size_t>(kRankScores + kFastOut) * 8 : static_cast<size_t>(kMergeLdsKeys) * 8;
+  const size_t tools_general = static_cast<size_t>(kMergeStage) * 25;
+  const size_t tools_fast = static_cast<size_t>(kMatrixMax) * 25 + 16 + static_cast<size_t>(kMatrixMax) * (kMatrixMax / 64) * 8;
+  const size_t merge_lds = head + static_cast<size_t>(kMergeStage) * 4 +
+                           (final_nms >= 0.f ? (tools_general > tools_fast ? tools_general : tools_fast) : 0);
   hipStream_t s = as_stream(stream);
   if (hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4, s) != hipSuccess)
     return launch_status("hipMemsetAsync(detect)");
@@ -607,13 +899,22 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                      static_cast<size_t>(kDTile) * C * 4, s, a, locs, scores);
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
-  hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w), s, ws.cand,
-                     ws.count, ws.boxes, P, C, w, max_overlap, so);
+  hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
+                     ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
   SBOD_LAUNCHED("k_det_segment");
   hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
-                     ws.lastkey, ws.boxes, P, C, w, top_k, final_nms, ws.scratch, det_boxes,
-                     det_labels, det_scores, det_count);
+                     ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
+                     ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count);
   SBOD_LAUNCHED("k_det_merge");
+  if (two) {
+    hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w2), s, ws.cand,
+                       ws.count, ws.boxes, P, C, w2, w2, max_overlap, so, ws.need);
+    SBOD_LAUNCHED("k_det_segment(pass 2)");
+    hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
+                       ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, general, 2, ws.need,
+                       ws.scratch, det_boxes, det_labels, det_scores, det_count);
+    SBOD_LAUNCHED("k_det_merge(pass 2)");
+  }
   return SBOD_OK;
 }
 
@@ -641,7 +942,7 @@ int sbod_nms_f32(const float *boxes, const float *scores, int64_t n, float overl
     set_error("sbod_nms_f32: workspace %zu < %zu", workspace_bytes, sbod_nms_workspace_bytes(n));
     return SBOD_E_WORKSPACE;
   }
-  const size_t lds = seg_lds(q);
+  const size_t lds = single_lds(q);
   auto *gk = static_cast<unsigned long long *>(workspace);
   if (variant == SBOD_NMS_TV)
     hipLaunchKernelGGL(k_nms_single<SBOD_NMS_TV>, dim3(1), dim3(1024), lds, s, boxes, scores,
