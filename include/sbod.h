@@ -147,6 +147,8 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
  * Used by backward to apply the upstream gradient to gradients produced by the fused
  * forward. */
 int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, void *stream);
+int sbod_scale2_inplace(void *a, int64_t na, void *b, int64_t nb, int dtype, const float *scale,
+                        void *stream);  /* both buffers, one launch */
 
 /* ---------------------------------------------------------------- a5/a6/a7/a8/a9 standalone
  * The operators.Loss / iou_utils API on already-selected rows.  Each call writes the per-row

@@ -156,31 +156,40 @@ def _hnm_sum(ce, pool_mask, n_hard):
     return tot
 
 
+def local_npos(priors_cxcy, boxes, labels, threshold=0.5):
+    """Positives of this (shard of the) batch — the quantity data parallelism all-reduces."""
+    _, cls, _ = _assign(priors_cxcy, boxes, labels, threshold)
+    return int((cls > 0).sum())
+
+
 def criterion(kind, priors_cxcy, locs, scores, boxes, labels, reg_loss, cls_loss,
-              threshold=0.5, neg_pos_ratio=3, reg_weights=1.0):
+              threshold=0.5, neg_pos_ratio=3, reg_weights=1.0, npos_total=None):
     """kind: 'ssd512' (``models/SSD512.py:508-626``), 'ssd300' (``SSD300.py:477-594``),
-    'retina' (``RetinaNet.py:385-506``).  ``locs``/``scores`` are autograd leaves."""
+    'retina' (``RetinaNet.py:385-506``).  ``locs``/``scores`` are autograd leaves.
+    ``npos_total`` overrides the batch positive count in every normaliser (a data-parallel shard
+    normalised by the global count; summing shard losses gives the full-batch loss)."""
     B, P, C = scores.shape
     obj, cls, neg = _assign(priors_cxcy, boxes, labels, threshold)
     pos = cls > 0
     negm = neg == -1
     n_pos = pos.sum(1)
+    n_tot = n_pos.sum().float() if npos_total is None else torch.tensor(float(npos_total))
     if reg_loss.upper() == 'DIOU':
         dec = torch.stack([_decode_t(locs[b], priors_cxcy) for b in range(B)])
         tl = torch.stack([boxes[b][torch.from_numpy(obj[b])] for b in range(B)])
-        loc_loss = iou_loss('diou', dec[pos].view(-1, 4), tl[pos].view(-1, 4))
+        loc_loss = (1.0 - aligned_overlap('diou', dec[pos].view(-1, 4), tl[pos].view(-1, 4))).sum() / n_tot
     else:
         enc = torch.stack([_encode_t(boxes[b][torch.from_numpy(obj[b])], priors_cxcy) for b in range(B)])
         if kind == 'ssd300':
-            loc_loss = F.l1_loss(locs[pos].view(-1, 4), enc[pos].view(-1, 4))
+            loc_loss = (locs[pos].view(-1, 4) - enc[pos].view(-1, 4)).abs().sum() / (4 * n_tot)
         else:
-            loc_loss = smooth_l1(locs[pos].view(-1, 4), enc[pos].view(-1, 4))
+            loc_loss = smooth_l1(locs[pos].view(-1, 4), enc[pos].view(-1, 4), reduction='sum') / n_tot
     if cls_loss.upper() == 'FOCAL':
         rows = torch.cat([scores[pos], scores[negm]], 0)
         tgt = torch.cat([cls[pos], cls[negm]], 0)
         conf = focal_softmax(rows.view(-1, C), tgt.view(-1))
         if kind == 'retina':
-            conf = conf / n_pos.sum().float()
+            conf = conf / n_tot
     else:
         ce = F.cross_entropy(scores.view(-1, C), cls.view(-1), reduction='none').view(B, P)
         n_hard = neg_pos_ratio * n_pos
@@ -192,7 +201,7 @@ def criterion(kind, priors_cxcy, locs, scores, boxes, labels, reg_loss, cls_loss
             hard = _hnm_sum(ce, negm, n_hard)
         else:
             hard = _hnm_sum(ce, ~pos, n_hard)
-        conf = (hard + ce[pos].sum()) / n_pos.sum().float()
+        conf = (hard + ce[pos].sum()) / n_tot
     return conf + reg_weights * loc_loss
 
 

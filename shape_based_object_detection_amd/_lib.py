@@ -34,6 +34,7 @@ SIGNATURES = {
     'sbod_multibox_loss': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, P, F32, F32,
                                  F32, I32, I32, I32, I32, F32, F32, F32, P, P, P, P, SZ, P]),
     'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),
+    'sbod_scale2_inplace': (I32, [P, I64, P, I64, I32, P, P]),
     'sbod_aligned_overlap_f32': (I32, [I32, P, P, I64, P, P, P]),
     'sbod_smooth_l1_f32': (I32, [P, P, I64, F32, P, P, P]),
     'sbod_focal_f32': (I32, [I32, P, P, I64, I32, F32, F32, F32, P, P, P]),
@@ -107,8 +108,12 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+
+
 def stream_of(t):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    """hipStream_t (as int) of torch's current stream on t's device (no Stream object built)."""
+    return _raw_stream(t.get_device())
 
 
 def require_device(*tensors, what='sbod'):

@@ -44,14 +44,14 @@ def pack_gt(boxes, labels, device=None, allow_empty=False):
     does (``overlap.max(dim=0)`` of an empty matrix, models/SSD512.py:538)."""
     if len(boxes) != len(labels):
         raise ValueError('boxes and labels must have the same length')
-    counts = [int(b.shape[0]) for b in boxes]
-    if not allow_empty and any(c == 0 for c in counts):
+    counts = [len(b) for b in boxes]
+    if not allow_empty and 0 in counts:
         raise RuntimeError('max(): Expected reduction dim 0 to have non-zero size (an image has no '
                            'ground-truth objects, as in the reference criterion)')
     device = device or boxes[0].device
-    L.require_device(*boxes, *labels, what='pack_gt')
     gb = torch.cat(boxes if boxes[0].dim() == 2 else [b.reshape(-1, 4) for b in boxes])
     gl = torch.cat(labels if labels[0].dim() == 1 else [l.reshape(-1) for l in labels])
+    L.require_device(gb, gl, what='pack_gt')   # torch.cat already rejects mixed devices
     if gb.dtype != torch.float32:
         gb = gb.float()
     if gl.dtype != torch.int64:
@@ -65,8 +65,9 @@ _WS = {}
 def workspace(nbytes, device, slot='default'):
     """Device scratch, cached per (device, current stream, slot) and grown on demand.  Reuse is
     safe because every user of a slot runs in stream order on that stream."""
-    dev = torch.device(device)
-    key = (dev, torch.cuda.current_stream(dev).cuda_stream if dev.type == 'cuda' else 0, slot)
+    dev = device if isinstance(device, torch.device) else torch.device(device)
+    key = (dev, L._raw_stream(dev.index if dev.index is not None else torch.cuda.current_device())
+           if dev.type == 'cuda' else 0, slot)
     buf = _WS.get(key)
     n = max(int(nbytes), 1)
     if buf is None or buf.numel() < n:
@@ -169,10 +170,10 @@ class _FusedLoss(torch.autograd.Function):
         gl, gs = ctx.saved_tensors
         if g is None or gl is None:
             return None, None, None, None
-        g = g.detach().to(torch.float32).reshape(1).contiguous()
-        for t in (gl, gs):
-            L.call('sbod_scale_inplace', L.ptr(t), L.DT_F32 if t.dtype == torch.float32 else L.DT_BF16,
-                   t.numel(), L.ptr(g), L.stream_of(t))
+        if g.dtype != torch.float32 or not g.is_contiguous():
+            g = g.detach().to(torch.float32).contiguous()
+        L.call('sbod_scale2_inplace', L.ptr(gl), gl.numel(), L.ptr(gs), gs.numel(),
+               L.DT_F32 if gl.dtype == torch.float32 else L.DT_BF16, L.ptr(g), L.stream_of(gl))
         return gl, gs, None, None
 
 
@@ -264,11 +265,14 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
                           'top-%d outputs exactly (pathological suppression); unsupported' % top_k)
     if in_place and lc is not locs:
         locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
-    sizes = []
-    for n in counts:
-        sizes += [n, top_k - n]
-    res = (list(out_b.view(B * top_k, 4).split(sizes)[0::2]), list(out_l.view(-1).split(sizes)[0::2]),
-           list(out_s.view(-1).split(sizes)[0::2]))
+    if min(counts) == top_k:     # every image full (the usual eval case): one view op each
+        res = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
+    else:
+        sizes = []
+        for n in counts:
+            sizes += [n, top_k - n]
+        res = (list(out_b.view(B * top_k, 4).split(sizes)[0::2]),
+               list(out_l.view(-1).split(sizes)[0::2]), list(out_s.view(-1).split(sizes)[0::2]))
     if debug:
         return res, dbg_p, dbg_b
     return res

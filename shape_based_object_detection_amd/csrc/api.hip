@@ -42,6 +42,26 @@ __global__ __launch_bounds__(256) void k_scale(T *__restrict__ g, int64_t n, con
   }
 }
 
+// Two buffers in one launch (the fused criterion's grad_locs and grad_scores).
+template <typename T>
+__global__ __launch_bounds__(256) void k_scale2(T *__restrict__ a, int64_t na, T *__restrict__ b,
+                                                int64_t nb, const float *scale) {
+  const float s = *scale;
+  if (s == 1.0f) return;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < na + nb; i += stride) {
+    T *p = i < na ? a + i : b + (i - na);
+    if constexpr (sizeof(T) == 4) {
+      *p = *p * s;
+    } else {
+      float v = __uint_as_float(static_cast<uint32_t>(*p) << 16) * s;
+      uint32_t u = __float_as_uint(v);
+      u += 0x7fffu + ((u >> 16) & 1u);
+      *p = static_cast<T>(u >> 16);
+    }
+  }
+}
+
 }  // namespace sbod
 
 extern "C" {
@@ -62,6 +82,23 @@ int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, voi
     hipLaunchKernelGGL(sbod::k_scale<uint16_t>, dim3(blocks), dim3(256), 0,
                        sbod::as_stream(stream), static_cast<uint16_t *>(grad), n, scale);
   SBOD_LAUNCHED("sbod_scale_inplace");
+  return SBOD_OK;
+}
+
+int sbod_scale2_inplace(void *a, int64_t na, void *b, int64_t nb, int dtype, const float *scale,
+                        void *stream) {
+  SBOD_REQUIRE(na >= 0 && nb >= 0 && scale != nullptr, "sbod_scale2_inplace: bad arguments");
+  const int64_t n = na + nb;
+  if (n == 0) return SBOD_OK;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (dtype == SBOD_DT_F32)
+    hipLaunchKernelGGL(sbod::k_scale2<float>, dim3(blocks), dim3(256), 0, sbod::as_stream(stream),
+                       static_cast<float *>(a), na, static_cast<float *>(b), nb, scale);
+  else
+    hipLaunchKernelGGL(sbod::k_scale2<uint16_t>, dim3(blocks), dim3(256), 0, sbod::as_stream(stream),
+                       static_cast<uint16_t *>(a), na, static_cast<uint16_t *>(b), nb, scale);
+  SBOD_LAUNCHED("sbod_scale2_inplace");
   return SBOD_OK;
 }
 

@@ -53,6 +53,14 @@ class _AnchorCriterion(nn.Module):
         self.threshold += increment
 
     def _spec(self):
+        key = (str(_cfg(self.config, 'reg_loss', 'smoothl1')), str(_cfg(self.config, 'cls_loss', 'ce')),
+               self.neg_pos_ratio, self.alpha, self.distributed)
+        if getattr(self, '_spec_key', None) != key:
+            self._spec_cache = self._build_spec()
+            self._spec_key = key
+        return self._spec_cache
+
+    def _build_spec(self):
         reg_loss = str(_cfg(self.config, 'reg_loss', 'smoothl1')).upper()
         cls_loss = str(_cfg(self.config, 'cls_loss', 'ce')).upper()
         if reg_loss == 'DIOU':
@@ -73,7 +81,8 @@ class _AnchorCriterion(nn.Module):
         return core.CriterionSpec(reg, cls, flags, self.neg_pos_ratio, float(self.alpha))
 
     def forward(self, predicted_locs, predicted_scores, boxes, labels):
-        L.require_device(predicted_locs, predicted_scores, what=type(self).__name__)
+        if not (predicted_locs.is_cuda and predicted_scores.is_cuda):
+            L.require_device(predicted_locs, predicted_scores, what=type(self).__name__)
         B, P, _ = predicted_scores.shape
         n_priors = self.priors_cxcy.size(0)
         assert n_priors == predicted_locs.size(1) == predicted_scores.size(1)
