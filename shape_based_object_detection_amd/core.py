@@ -371,3 +371,59 @@ def focal_rows(kind, logits, target, alpha_fg, alpha_bg, gamma):
 
     want = torch.is_grad_enabled() and logits.requires_grad
     return _RowOp.apply(z, run, want)
+
+
+# ----------------------------------------------------------------------------- a14: DeformConv2d
+class _DeformConv(torch.autograd.Function):
+    """out = DCN(x, offset, sigmoid(mask_logits), weight) on the HIP path; backward produces the
+    gradients of all four inputs from one coefficient pass + two MFMA kernels (dcn.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, offset, mask_logits, weight, ks, padding, stride):
+        B, C, H, W = x.shape
+        O = weight.shape[0]
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        if tuple(offset.shape) != (B, 2 * ks * ks, Ho, Wo):
+            raise ValueError('DeformConv2d: offset shape %s, expected %s'
+                             % (tuple(offset.shape), (B, 2 * ks * ks, Ho, Wo)))
+        if mask_logits is not None and tuple(mask_logits.shape) != (B, ks * ks, Ho, Wo):
+            raise ValueError('DeformConv2d: mask shape %s' % (tuple(mask_logits.shape),))
+        if tuple(weight.shape) != (O, C, ks, ks):
+            raise ValueError('DeformConv2d: weight shape %s' % (tuple(weight.shape),))
+        out = torch.empty(B, O, Ho, Wo, dtype=torch.float32, device=x.device)
+        nb = L.lib().sbod_dcn_workspace_bytes(B, C, H, W, O, ks, stride, padding)
+        ws = workspace(nb, x.device, 'dcn')
+        L.call('sbod_dcn_fwd_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight),
+               B, C, H, W, O, ks, stride, padding, L.ptr(out), L.ptr(ws), nb, L.stream_of(x))
+        ctx.save_for_backward(x, offset, mask_logits, weight)
+        ctx.cfg = (ks, padding, stride)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, offset, mask_logits, weight = ctx.saved_tensors
+        ks, padding, stride = ctx.cfg
+        B, C, H, W = x.shape
+        O = weight.shape[0]
+        g = gout.contiguous().float()
+        need = ctx.needs_input_grad
+        gx = torch.empty_like(x) if need[0] else None
+        goff = torch.empty_like(offset) if need[1] else None
+        gm = torch.empty_like(mask_logits) if (mask_logits is not None and need[2]) else None
+        gw = torch.empty_like(weight) if need[3] else None
+        nb = L.lib().sbod_dcn_workspace_bytes(B, C, H, W, O, ks, stride, padding)
+        ws = workspace(nb, x.device, 'dcn')
+        L.call('sbod_dcn_bwd_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight),
+               L.ptr(g), B, C, H, W, O, ks, stride, padding, L.ptr(gx), L.ptr(goff), L.ptr(gm),
+               L.ptr(gw), L.ptr(ws), nb, L.stream_of(x))
+        return gx, goff, gm, gw, None, None, None
+
+
+def deform_conv2d(x, offset, mask_logits, weight, ks=3, padding=1, stride=1):
+    """Modulated deformable conv (Deformable_convolution.py:33-91) given the p_conv output
+    ``offset`` [B,2k²,Ho,Wo] and the m_conv output BEFORE sigmoid ``mask_logits`` [B,k²,Ho,Wo]
+    (None: modulation=False).  fp32 in, fp32 out."""
+    L.require_device(x, offset, weight, what='DeformConv2d')
+    c = lambda t: None if t is None else t.contiguous().float()
+    return _DeformConv.apply(c(x), c(offset), c(mask_logits), c(weight), int(ks), int(padding),
+                             int(stride))
