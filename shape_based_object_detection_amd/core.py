@@ -406,6 +406,8 @@ class _DeformConv(torch.autograd.Function):
         B, C, H, W = x.shape
         O = weight.shape[0]
         g = gout.contiguous().float()
+        if g.data_ptr() % 16:          # the weight-gradient kernel reads grad_out as float4
+            g = g.clone()
         need = ctx.needs_input_grad
         gx = torch.empty_like(x) if need[0] else None
         goff = torch.empty_like(offset) if need[1] else None

@@ -4,14 +4,17 @@
 //
 // The contraction runs on fp32 MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, one rounding
 // per step) so results stay within fp32 tolerance of the reference.  GEMM views, with
-// M = B*Ho*Wo output pixels, K = C*k*k (c-major, the flattening of conv.weight [O,C,k,k]):
-//   forward      out[o, m]  = sum_K W[o, K] * cols[K, m]
-//   backward     dcols[K,m] = sum_o W[o, K] * dout[o, m]   -> dx (atomics), d_offset, d_mask
-//                dW[o, K]   = sum_m dout[o, m] * cols[K, m]
-// cols[K, m] = sigmoid(mask) * sum_q g_q * x_pad[corner_q] is never materialised: it is built
-// per K-tile into LDS from per-(pixel, kernel point) coefficients computed once (k_dcn_coef),
-// so the bilinear gathers are shared by every output channel of the tile.
-// Roofline: MFMA-bound (2*M*O*K flops forward, 4*M*O*K backward).
+// M = B*Ho*Wo output pixels, N = k*k kernel points and the reduction index ordered K' = n*C + c
+// (a permutation of conv.weight's c*N + n, applied to the weight copies below):
+//   forward      out[o, m]   = sum_K' Wf[o, K'] * cols[K', m]
+//   backward     dcols[m, c] = sum_o dout[o, m] * Wb[n, o, c]   (per n) -> dx, d_offset, d_mask
+//                dWp[o,n,c]  = sum_m dout[o, m] * cols[(n,c), m]
+// cols[(n,c), m] = sigmoid(mask) * sum_q g_q * x[corner_q] is never materialised: it is built per
+// 32-channel K'-tile into LDS from per-(pixel, kernel point) coefficients computed once
+// (k_dcn_coef), reading x channels-last (xt) so the four corner gathers of a pixel are
+// contiguous channel vectors, and it is shared by every output channel of the tile.
+// dx is accumulated channels-last with float atomics whose 32-lane groups cover 128 contiguous
+// bytes, then transposed back.  Roofline: MFMA-bound (2*M*O*C*N flops forward, 2x backward).
 #include "sbod_common.h"
 
 namespace sbod {
@@ -21,7 +24,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kDcnThreads = 256;
 constexpr int kMaxN = 49;      // k*k <= 49 (k <= 7)
 
-// Per (pixel m, kernel point n): corner offsets in the (b, c) plane (-1 outside the original
+// Per (pixel m, kernel point n): corner offsets in the image plane (-1 outside the original
 // map: zero padding), bilinear weights g (unmodulated), mask value, and the derivative terms.
 struct Coef {
   int idx[4];          // lt, rb, lb, rt
@@ -83,27 +86,70 @@ __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__res
   coef[t] = c;
 }
 
-// Modulated sample cols[K = c*N + n, m]; the sum order of the reference (lt + rb + lb + rt) * m.
-__device__ __forceinline__ float sample(const float *__restrict__ xplane, const Coef &c) {
-  float v[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = c.idx[q] >= 0 ? xplane[c.idx[q]] : 0.f;
-  return (((c.g[0] * v[0] + c.g[1] * v[1]) + c.g[2] * v[2]) + c.g[3] * v[3]) * c.mval;
+
+// Batched transpose in [nb][R][S] -> out [nb][S][R] (64 x 64 LDS tiles).
+__global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ in, float *__restrict__ out,
+                                                   int R, int S) {
+  __shared__ float t[64][65];
+  const int s0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  const int64_t base = static_cast<int64_t>(blockIdx.z) * R * S;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, s = s0 + tx;
+    t[i][tx] = (r < R && s < S) ? in[base + static_cast<int64_t>(r) * S + s] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int s = s0 + i, r = r0 + tx;
+    if (r < R && s < S) out[base + static_cast<int64_t>(s) * R + r] = t[tx][i];
+  }
+}
+
+// Bilinear combination in the reference's order: ((lt + rb) + lb) + rt, then * mask.
+__device__ __forceinline__ float combine(const float g[4], float m, float x0, float x1, float x2, float x3) {
+  return (((g[0] * x0 + g[1] * x1) + g[2] * x2) + g[3] * x3) * m;
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float *p, bool ok, float *v) {
+  if (VEC == 4) {
+    const float4 t = ok ? *reinterpret_cast<const float4 *>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = ok ? *p : 0.f;
+  }
 }
 
 // ----------------------------------------------------------------------------- forward
-// Block = 64 pixels x 256 output channels (4 waves x 64 channels, 2 x 2 tiles of 32 x 32).
-constexpr int kFM = 64, kFO = 256, kFK = 32;
+// Block: 64 pixels x 256 output channels, 4 waves x (64 channels x 64 pixels) = 2 x 2 MFMA tiles.
+// K'-tiles of 32 channels of one kernel point; blockIdx.z takes a contiguous share of them
+// (split-K for small maps, combined with float atomics).  One tile of gathers is in flight while
+// the previous tile's MFMAs run (double-buffered LDS, one barrier per tile).
+constexpr int kFM = 64, kFKC = 32, kFLD = kFM + 2;
 
-__global__ __launch_bounds__(kDcnThreads) void k_dcn_fwd(DcnShape s, const float *__restrict__ x,
-                                                         const Coef *__restrict__ coef,
-                                                         const float *__restrict__ wt,
-                                                         float *__restrict__ out) {
-  __shared__ float s_cols[kFK][kFM];         // B operand [k][m]
-  __shared__ float s_w[kFO][kFK + 1];        // A operand [o][k]
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int m0 = blockIdx.x * kFM, o0 = blockIdx.y * kFO;
-  const int HW = s.H * s.W, HWo = s.Ho * s.Wo;
+template <int VEC>
+__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd(DcnShape s, const float *__restrict__ xt,
+                                                            const Coef *__restrict__ coef,
+                                                            const float *__restrict__ wf,
+                                                            float *__restrict__ out, int atomic_out) {
+  __shared__ float s_cols[2][kFKC][kFLD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const int m0 = blockIdx.x * kFM, o0 = blockIdx.y * 256;
+  const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
+  const int CT = (s.C + kFKC - 1) / kFKC, T = s.N * CT;
+  const int t0 = static_cast<int>(static_cast<int64_t>(blockIdx.z) * T / gridDim.z);
+  const int t1 = static_cast<int>(static_cast<int64_t>(blockIdx.z + 1) * T / gridDim.z);
+  // sampler role: pixel mm, 8 channels starting at 8 * cq
+  const int mm = tid & 63, cq = tid >> 6;
+  const int ms = m0 + mm;
+  const bool mvalid = ms < s.M;
+  const int bs = mvalid ? ms / HWo : 0;
+  const float *xb = xt + static_cast<int64_t>(bs) * HW * s.C;
+  int cur_n = -1;
+  int cidx[4] = {-1, -1, -1, -1};
+  float cg[4] = {0.f, 0.f, 0.f, 0.f}, cm = 0.f;
+  float X[4][8];
+  float acur[2][16], anext[2][16];
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -111,160 +157,278 @@ __global__ __launch_bounds__(kDcnThreads) void k_dcn_fwd(DcnShape s, const float
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  for (int k0 = 0; k0 < s.K; k0 += kFK) {
-    __syncthreads();
-    for (int e = tid; e < kFK * kFM; e += kDcnThreads) {
-      const int kk = e / kFM, mm = e - kk * kFM;
-      const int K = k0 + kk, m = m0 + mm;
-      float v = 0.f;
-      if (K < s.K && m < s.M) {
-        const int c = K / s.N, n = K - c * s.N;
-        const int b = m / HWo;
-        v = sample(x + (static_cast<int64_t>(b) * s.C + c) * HW, coef[static_cast<int64_t>(m) * s.N + n]);
+
+  auto gather = [&](int t) {
+    const int n = t / CT, c0 = (t - n * CT) * kFKC + 8 * cq;
+    if (n != cur_n) {
+      cur_n = n;
+      if (mvalid) {
+        const Coef cf = coef[static_cast<int64_t>(ms) * s.N + n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { cidx[q] = cf.idx[q]; cg[q] = cf.g[q]; }
+        cm = cf.mval;
       }
-      s_cols[kk][mm] = v;
     }
-    for (int e = tid; e < kFO * kFK; e += kDcnThreads) {
-      const int o = e / kFK, kk = e - o * kFK;
-      const int K = k0 + kk;
-      s_w[o][kk] = (o0 + o < s.O && K < s.K) ? wt[static_cast<int64_t>(o0 + o) * s.K + K] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float *p = xb + static_cast<int64_t>(cidx[q]) * s.C;
+#pragma unroll
+      for (int v = 0; v < 8; v += VEC) {
+        const int c = c0 + v;
+        load_vec<VEC>(p + c, mvalid && cidx[q] >= 0 && c < s.C, &X[q][v]);
+      }
+    }
+  };
+  auto store_cols = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v)
+      s_cols[buf][8 * cq + v][mm] = combine(cg, cm, X[0][v], X[1][v], X[2][v], X[3][v]);
+  };
+  auto load_a = [&](int t, float (&a)[2][16]) {
+    const int n = t / CT, c0 = (t - n * CT) * kFKC + 16 * h;
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int o = o0 + 64 * wv + 32 * ri + l31;
+      const float *p = wf + static_cast<int64_t>(o) * s.K + static_cast<int64_t>(n) * s.C;
+#pragma unroll
+      for (int v = 0; v < 16; v += VEC) load_vec<VEC>(p + c0 + v, o < s.O && c0 + v < s.C, &a[ri][v]);
+    }
+  };
+
+  if (t0 < t1) {
+    gather(t0);
+    store_cols(0);
+    load_a(t0, acur);
+  }
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const int buf = (t - t0) & 1;
+    const bool more = t + 1 < t1;
+    if (more) {
+      gather(t + 1);
+      load_a(t + 1, anext);
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const float b0 = s_cols[buf][16 * h + st][l31];
+      const float b1 = s_cols[buf][16 * h + st][32 + l31];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      store_cols(buf ^ 1);
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acur[ri][v] = anext[ri][v];
     }
     __syncthreads();
-#pragma unroll 4
-    for (int st = 0; st < kFK / 2; ++st) {
-      const int kk = 2 * st + (lane >> 5);
-      const float a0 = s_w[64 * wv + (lane & 31)][kk];
-      const float a1 = s_w[64 * wv + 32 + (lane & 31)][kk];
-      const float b0 = s_cols[kk][lane & 31];
-      const float b1 = s_cols[kk][32 + (lane & 31)];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
   }
   // C/D map (gfx950, dtype independent): col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int bq = 0; bq < 2; ++bq) {
+    const int m = m0 + 32 * bq + l31;
+    if (m >= s.M) continue;
+    const int b = m / HWo, pix = m - b * HWo;
 #pragma unroll
-    for (int bq = 0; bq < 2; ++bq) {
-      const int m = m0 + 32 * bq + (lane & 31);
-      if (m >= s.M) continue;
-      const int b = m / HWo, pix = m - b * HWo;
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (o < s.O) out[(static_cast<int64_t>(b) * s.O + o) * HWo + pix] = acc[a][bq][r];
+        const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o >= s.O) continue;
+        float *dst = out + (static_cast<int64_t>(b) * s.O + o) * HWo + pix;
+        if (atomic_out) atomicAdd(dst, acc[a][bq][r]);
+        else *dst = acc[a][bq][r];
       }
-    }
+  }
 }
 
 // ----------------------------------------------------------------------------- backward (data)
-// Block = 64 pixels; per K-tile of 128 (4 waves x 32 rows) dcols = W^T dout over all O, then the
-// epilogue turns each dcols element into dx (atomics) and per-(pixel, n) sums of d_mask and
-// d_p (LDS), written once at the end (clamp masks applied, sigmoid derivative applied).
-constexpr int kBM = 64, kBK = 128, kBO = 64;
+// Block: 64 pixels x 256 channels for ONE kernel point n (blockIdx.z).  dcols[m, c] =
+// sum_o dout[o, m] Wb[n, o, c] on MFMA (dout staged in 32-channel chunks, Wb read straight
+// from L2 with lanes along c), then per element: corner values (channels-last, coalesced), dx
+// atomics (128-B segments), and d_mask / d_p partial sums reduced over c across the 32 lanes
+// of a row and the 4 waves before one write per (pixel, n).
+constexpr int kBM = 64, kBOC = 32, kBLD = kBM + 2;
 
-__global__ __launch_bounds__(kDcnThreads) void k_dcn_bwd_data(
-    DcnShape s, const float *__restrict__ x, const Coef *__restrict__ coef,
-    const float *__restrict__ wt, const float *__restrict__ gout, float *__restrict__ gx,
-    float *__restrict__ goff, float *__restrict__ gmlog) {
-  __shared__ float s_dout[kBO][kBM];           // B operand [o][m]
-  __shared__ float s_wt[kBK][kBO + 1];         // A operand [K][o]
-  __shared__ float s_acc[3][kBM][kMaxN];       // d_mask, d_px, d_py per (pixel, n)
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int m0 = blockIdx.x * kBM;
-  const int HW = s.H * s.W, HWo = s.Ho * s.Wo;
-  for (int e = tid; e < 3 * kBM * kMaxN; e += kDcnThreads) (&s_acc[0][0][0])[e] = 0.f;
-  for (int K0 = 0; K0 < s.K; K0 += kBK) {
-    f32x16 acc[2];
+__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
+    DcnShape s, const float *__restrict__ xt, const Coef *__restrict__ coef,
+    const float *__restrict__ wb, const float *__restrict__ gout, float *__restrict__ gxt,
+    float *__restrict__ goff, float *__restrict__ gmlog, int atomic_small) {
+  __shared__ float s_dout[2][kBOC][kBLD];     // A operand [o][m]
+  __shared__ Coef s_cf[kBM];
+  __shared__ float s_red[3][kBM];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const int m0 = blockIdx.x * kBM, cgb = blockIdx.y * 256, n = blockIdx.z;
+  const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
+  if (tid < kBM) {
+    const int m = m0 + tid;
+    if (m < s.M) s_cf[tid] = coef[static_cast<int64_t>(m) * s.N + n];
+  }
+  if (tid < 3 * kBM) (&s_red[0][0])[tid] = 0.f;
+  const int OT = (s.O + kBOC - 1) / kBOC;
+  float dstage[8];
+  float bcur[2][16], bnext[2][16];
+  auto load_dout = [&](int oc) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][r] = acc[1][r] = 0.f;
-    for (int o0 = 0; o0 < s.O; o0 += kBO) {
-      __syncthreads();
-      for (int e = tid; e < kBO * kBM; e += kDcnThreads) {
-        const int oo = e / kBM, mm = e - oo * kBM;
-        const int o = o0 + oo, m = m0 + mm;
-        float v = 0.f;
-        if (o < s.O && m < s.M) {
-          const int b = m / HWo, pix = m - b * HWo;
-          v = gout[(static_cast<int64_t>(b) * s.O + o) * HWo + pix];
-        }
-        s_dout[oo][mm] = v;
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + kDcnThreads * i;
+      const int ol = e >> 6, mm = e & 63;
+      const int o = oc * kBOC + ol, m = m0 + mm;
+      float v = 0.f;
+      if (o < s.O && m < s.M) {
+        const int b = m / HWo, pix = m - b * HWo;
+        v = gout[(static_cast<int64_t>(b) * s.O + o) * HWo + pix];
       }
-      for (int e = tid; e < kBO * kBK; e += kDcnThreads) {
-        const int oo = e / kBK, kk = e - oo * kBK;
-        const int o = o0 + oo, K = K0 + kk;
-        s_wt[kk][oo] = (o < s.O && K < s.K) ? wt[static_cast<int64_t>(o) * s.K + K] : 0.f;
-      }
-      __syncthreads();
-#pragma unroll 4
-      for (int st = 0; st < kBO / 2; ++st) {
-        const int oo = 2 * st + (lane >> 5);
-        const float a = s_wt[32 * wv + (lane & 31)][oo];
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s_dout[oo][lane & 31], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s_dout[oo][32 + (lane & 31)], acc[1], 0, 0, 0);
+      dstage[i] = v;
+    }
+  };
+  auto store_dout = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + kDcnThreads * i;
+      s_dout[buf][e >> 6][e & 63] = dstage[i];
+    }
+  };
+  auto load_b = [&](int oc, float (&bb)[2][16]) {
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci) {
+      const int c = cgb + 64 * wv + 32 * ci + l31;
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int o = oc * kBOC + 16 * h + st;
+        bb[ci][st] = (o < s.O && c < s.C) ? wb[(static_cast<int64_t>(n) * s.O + o) * s.C + c] : 0.f;
       }
     }
-    // epilogue: element (K, m) of this wave's 32 x 64 slab
+  };
+  f32x16 acc[2][2];
 #pragma unroll
-    for (int bq = 0; bq < 2; ++bq) {
-      const int mm = 32 * bq + (lane & 31), m = m0 + mm;
-      if (m >= s.M) continue;
-      const int b = m / HWo;
-#pragma unroll 4
-      for (int r = 0; r < 16; ++r) {
-        const int K = K0 + 32 * wv + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (K >= s.K) continue;
-        const int c = K / s.N, n = K - c * s.N;
-        const Coef cf = coef[static_cast<int64_t>(m) * s.N + n];
-        const int64_t plane = (static_cast<int64_t>(b) * s.C + c) * HW;
-        float v[4];
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = cf.idx[q] >= 0 ? x[plane + cf.idx[q]] : 0.f;
-        const float dcol = acc[bq][r];
-        const float raw = ((cf.g[0] * v[0] + cf.g[1] * v[1]) + cf.g[2] * v[2]) + cf.g[3] * v[3];
-        const float dval = dcol * cf.mval;
-        if (gx) {
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (cf.idx[q] >= 0) atomicAdd(gx + plane + cf.idx[q], dval * cf.g[q]);
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  load_dout(0);
+  store_dout(0);
+  load_b(0, bcur);
+  __syncthreads();
+  for (int oc = 0; oc < OT; ++oc) {
+    const int buf = oc & 1;
+    const bool more = oc + 1 < OT;
+    if (more) {
+      load_dout(oc + 1);
+      load_b(oc + 1, bnext);
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const float a0 = s_dout[buf][16 * h + st][l31];
+      const float a1 = s_dout[buf][16 * h + st][32 + l31];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bcur[0][st], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bcur[1][st], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bcur[0][st], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bcur[1][st], acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      store_dout(buf ^ 1);
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+        for (int st = 0; st < 16; ++st) bcur[ci][st] = bnext[ci][st];
+    }
+    __syncthreads();
+  }
+  // epilogue: row m = 32 ri + (r&3) + 8 (r>>2) + 4 h, column c = cgb + 64 wv + 32 ci + l31
+#pragma unroll
+  for (int ri = 0; ri < 2; ++ri) {
+#pragma unroll 2
+    for (int r = 0; r < 16; ++r) {
+      const int mm = 32 * ri + (r & 3) + 8 * (r >> 2) + 4 * h, m = m0 + mm;
+      float pm = 0.f, ppx = 0.f, ppy = 0.f;
+      if (m < s.M) {
+        const Coef &cf = s_cf[mm];
+        const int b = m / HWo;
+        const int64_t ib = static_cast<int64_t>(b) * HW;
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci) {
+          const int c = cgb + 64 * wv + 32 * ci + l31;
+          if (c >= s.C) continue;
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = cf.idx[q] >= 0 ? xt[(ib + cf.idx[q]) * s.C + c] : 0.f;
+          const float dcol = acc[ri][ci][r];
+          const float raw = ((cf.g[0] * v[0] + cf.g[1] * v[1]) + cf.g[2] * v[2]) + cf.g[3] * v[3];
+          const float dval = dcol * cf.mval;
+          if (gxt) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (cf.idx[q] >= 0) atomicAdd(gxt + (ib + cf.idx[q]) * s.C + c, dval * cf.g[q]);
+          }
+          pm += dcol * raw;
+          ppx += dval * (-(1.f + cf.tly) * v[0] + (1.f - cf.rby) * v[1] - (1.f - cf.rby) * v[2] + (1.f + cf.tly) * v[3]);
+          ppy += dval * (-(1.f + cf.tlx) * v[0] + (1.f - cf.rbx) * v[1] + (1.f + cf.tlx) * v[2] - (1.f - cf.rbx) * v[3]);
         }
-        const float dpx = -(1.f + cf.tly) * v[0] + (1.f - cf.rby) * v[1] - (1.f - cf.rby) * v[2] + (1.f + cf.tly) * v[3];
-        const float dpy = -(1.f + cf.tlx) * v[0] + (1.f - cf.rbx) * v[1] + (1.f + cf.tlx) * v[2] - (1.f - cf.rbx) * v[3];
-        atomicAdd(&s_acc[0][mm][n], dcol * raw);
-        atomicAdd(&s_acc[1][mm][n], dval * dpx);
-        atomicAdd(&s_acc[2][mm][n], dval * dpy);
+      }
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) {
+        pm += __shfl_xor(pm, off, 32);
+        ppx += __shfl_xor(ppx, off, 32);
+        ppy += __shfl_xor(ppy, off, 32);
+      }
+      if (l31 == 0 && m < s.M) {
+        atomicAdd(&s_red[0][mm], pm);
+        atomicAdd(&s_red[1][mm], ppx);
+        atomicAdd(&s_red[2][mm], ppy);
       }
     }
   }
   __syncthreads();
-  for (int e = tid; e < kBM * s.N; e += kDcnThreads) {
-    const int mm = e / s.N, n = e - mm * s.N, m = m0 + mm;
-    if (m >= s.M) continue;
-    const Coef cf = coef[static_cast<int64_t>(m) * s.N + n];
-    const int b = m / HWo, pix = m - b * HWo;
-    if (goff) {
-      goff[(static_cast<int64_t>(b) * 2 * s.N + n) * HWo + pix] = (cf.inr & 1) ? s_acc[1][mm][n] : 0.f;
-      goff[(static_cast<int64_t>(b) * 2 * s.N + s.N + n) * HWo + pix] = (cf.inr & 2) ? s_acc[2][mm][n] : 0.f;
+  if (tid < kBM) {
+    const int mm = tid, m = m0 + mm;
+    if (m < s.M) {
+      const Coef &cf = s_cf[mm];
+      const int b = m / HWo, pix = m - b * HWo;
+      const float vx = (cf.inr & 1) ? s_red[1][mm] : 0.f;
+      const float vy = (cf.inr & 2) ? s_red[2][mm] : 0.f;
+      const float vm = s_red[0][mm] * cf.mval * (1.f - cf.mval);
+      float *px = goff ? goff + (static_cast<int64_t>(b) * 2 * s.N + n) * HWo + pix : nullptr;
+      float *py = goff ? goff + (static_cast<int64_t>(b) * 2 * s.N + s.N + n) * HWo + pix : nullptr;
+      float *pmk = gmlog ? gmlog + (static_cast<int64_t>(b) * s.N + n) * HWo + pix : nullptr;
+      if (atomic_small) {
+        if (px) { atomicAdd(px, vx); atomicAdd(py, vy); }
+        if (pmk) atomicAdd(pmk, vm);
+      } else {
+        if (px) { *px = vx; *py = vy; }
+        if (pmk) *pmk = vm;
+      }
     }
-    if (gmlog) gmlog[(static_cast<int64_t>(b) * s.N + n) * HWo + pix] = s_acc[0][mm][n] * cf.mval * (1.f - cf.mval);
   }
 }
 
 // ----------------------------------------------------------------------------- backward (weight)
-// Block = (64-wide K tile, a slice of kWSlice pixels), 256 output channels (4 waves x 64).
-// dW partial sums are added with float atomics (one 64 x 64 tile per wave at the end).
-constexpr int kWK = 64, kWO = 256, kWMs = 32, kWSlice = 2048;
+// Block: one kernel point n x 64 channels (blockIdx.x), a slice of pixels (blockIdx.y), 256
+// output channels (blockIdx.z): dWp[o, n, c] += sum_m dout[o, m] cols[(n, c), m].  The mirror of
+// the forward kernel: dout rows go straight from HBM into the MFMA A registers (float4 when a
+// 32-pixel chunk never straddles two images), the columns are re-sampled channels-last into
+// double-buffered LDS, and the next chunk's gathers are in flight during the current MFMAs.
+constexpr int kWC = 64, kWMs = 32, kWLD = kWC + 2;
 
-__global__ __launch_bounds__(kDcnThreads) void k_dcn_bwd_weight(
-    DcnShape s, const float *__restrict__ x, const Coef *__restrict__ coef,
-    const float *__restrict__ gout, float *__restrict__ gw) {
-  __shared__ float s_cols[kWMs][kWK];          // B operand [m][K]
-  __shared__ float s_dout[kWO][kWMs + 1];      // A operand [o][m]
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int K0 = blockIdx.x * kWK, ms0 = blockIdx.y * kWSlice, o0 = blockIdx.z * kWO;
-  const int HW = s.H * s.W, HWo = s.Ho * s.Wo;
+template <int VEC, bool AVEC>
+__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
+    DcnShape s, const float *__restrict__ xt, const Coef *__restrict__ coef,
+    const float *__restrict__ gout, float *__restrict__ gwp, int m_slice) {
+  __shared__ float s_cols[2][kWMs][kWLD];      // B operand [m][c]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const int CTw = (s.C + kWC - 1) / kWC;
+  const int n = blockIdx.x / CTw, c0 = (blockIdx.x - n * CTw) * kWC;
+  const int ms0 = blockIdx.y * m_slice, o0 = blockIdx.z * 256;
+  const int mend = min(ms0 + m_slice, s.M);
+  const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
+  const int smm = tid >> 3, scg = (tid & 7) * 8;
+  float X[4][8];
+  float cg[4] = {0.f, 0.f, 0.f, 0.f}, cm = 0.f;
+  float acur[2][16], anext[2][16];
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -272,54 +436,96 @@ __global__ __launch_bounds__(kDcnThreads) void k_dcn_bwd_weight(
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  const int mend = min(ms0 + kWSlice, s.M);
-  for (int m0 = ms0; m0 < mend; m0 += kWMs) {
-    __syncthreads();
-    for (int e = tid; e < kWMs * kWK; e += kDcnThreads) {
-      const int mm = e / kWK, kk = e - mm * kWK;
-      const int m = m0 + mm, K = K0 + kk;
-      float v = 0.f;
-      if (m < mend && K < s.K) {
-        const int c = K / s.N, n = K - c * s.N;
-        const int b = m / HWo;
-        v = sample(x + (static_cast<int64_t>(b) * s.C + c) * HW, coef[static_cast<int64_t>(m) * s.N + n]);
+
+  auto gather = [&](int m0) {
+    const int m = m0 + smm;
+    const bool ok = m < mend;
+    int idx[4] = {-1, -1, -1, -1};
+    if (ok) {
+      const Coef cf = coef[static_cast<int64_t>(m) * s.N + n];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { idx[q] = cf.idx[q]; cg[q] = cf.g[q]; }
+      cm = cf.mval;
+    }
+    const float *xb = xt + static_cast<int64_t>(ok ? m / HWo : 0) * HW * s.C + c0 + scg;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 8; v += VEC)
+        load_vec<VEC>(xb + static_cast<int64_t>(idx[q]) * s.C + v, idx[q] >= 0 && c0 + scg + v < s.C, &X[q][v]);
+  };
+  auto store_cols = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v)
+      s_cols[buf][smm][scg + v] = combine(cg, cm, X[0][v], X[1][v], X[2][v], X[3][v]);
+  };
+  auto load_a = [&](int m0, float (&a)[2][16]) {
+    const int mb = m0 + 16 * h;
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int o = o0 + 64 * wv + 32 * ri + l31;
+      if (AVEC) {
+        const int b = mb / HWo, pix = mb - b * HWo;
+        const float *p = gout + (static_cast<int64_t>(b) * s.O + o) * HWo + pix;
+#pragma unroll
+        for (int v = 0; v < 16; v += 4) load_vec<4>(p + v, o < s.O && mb + v < mend, &a[ri][v]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = mb + v;
+          float val = 0.f;
+          if (o < s.O && m < mend) {
+            const int b = m / HWo, pix = m - b * HWo;
+            val = gout[(static_cast<int64_t>(b) * s.O + o) * HWo + pix];
+          }
+          a[ri][v] = val;
+        }
       }
-      s_cols[mm][kk] = v;
     }
-    for (int e = tid; e < kWO * kWMs; e += kDcnThreads) {
-      const int oo = e / kWMs, mm = e - oo * kWMs;
-      const int o = o0 + oo, m = m0 + mm;
-      float v = 0.f;
-      if (o < s.O && m < mend) {
-        const int b = m / HWo, pix = m - b * HWo;
-        v = gout[(static_cast<int64_t>(b) * s.O + o) * HWo + pix];
-      }
-      s_dout[oo][mm] = v;
+  };
+
+  if (ms0 < mend) {
+    gather(ms0);
+    store_cols(0);
+    load_a(ms0, acur);
+  }
+  __syncthreads();
+  int it = 0;
+  for (int m0 = ms0; m0 < mend; m0 += kWMs, ++it) {
+    const int buf = it & 1;
+    const bool more = m0 + kWMs < mend;
+    if (more) {
+      gather(m0 + kWMs);
+      load_a(m0 + kWMs, anext);
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const float b0 = s_cols[buf][16 * h + st][l31];
+      const float b1 = s_cols[buf][16 * h + st][32 + l31];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      store_cols(buf ^ 1);
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acur[ri][v] = anext[ri][v];
     }
     __syncthreads();
-#pragma unroll 4
-    for (int st = 0; st < kWMs / 2; ++st) {
-      const int mm = 2 * st + (lane >> 5);
-      const float a0 = s_dout[64 * wv + (lane & 31)][mm];
-      const float a1 = s_dout[64 * wv + 32 + (lane & 31)][mm];
-      const float b0 = s_cols[mm][lane & 31];
-      const float b1 = s_cols[mm][32 + (lane & 31)];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
   }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int bq = 0; bq < 2; ++bq) {
-      const int K = K0 + 32 * bq + (lane & 31);
-      if (K >= s.K) continue;
+      const int c = c0 + 32 * bq + l31;
+      if (c >= s.C) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (o < s.O) atomicAdd(gw + static_cast<int64_t>(o) * s.K + K, acc[a][bq][r]);
+        const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.N + n) * s.C + c, acc[a][bq][r]);
       }
     }
 }
@@ -337,6 +543,31 @@ DcnShape make_shape(int B, int C, int H, int W, int O, int k, int stride, int pa
   return s;
 }
 
+struct DcnWs {
+  Coef *coef;
+  float *xt, *gxt, *wt, *gwp;
+};
+
+size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w) {
+  char *p = static_cast<char *>(base);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char *r = p ? p + off : nullptr; off += align_up(bytes); return r; };
+  const size_t xbytes = static_cast<size_t>(s.B) * s.C * s.H * s.W * 4;
+  const size_t wbytes = static_cast<size_t>(s.O) * s.K * 4;
+  DcnWs t;
+  t.coef = reinterpret_cast<Coef *>(take(static_cast<size_t>(s.M) * s.N * sizeof(Coef)));
+  t.xt = reinterpret_cast<float *>(take(xbytes));
+  t.gxt = reinterpret_cast<float *>(take(xbytes));
+  t.wt = reinterpret_cast<float *>(take(wbytes));
+  t.gwp = reinterpret_cast<float *>(take(wbytes));
+  if (w) *w = t;
+  return off;
+}
+
+void launch_transpose(const float *in, float *out, int nb, int R, int S, hipStream_t hs) {
+  hipLaunchKernelGGL(k_transpose, dim3((S + 63) / 64, (R + 63) / 64, nb), dim3(256), 0, hs, in, out, R, S);
+}
+
 }  // namespace sbod
 
 using namespace sbod;
@@ -344,8 +575,7 @@ using namespace sbod;
 extern "C" {
 
 size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
-  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
-  return align_up(static_cast<size_t>(s.M) * s.N * sizeof(Coef));
+  return dcn_carve(make_shape(B, C, H, W, O, k, stride, pad), nullptr, nullptr);
 }
 
 static int dcn_check(const DcnShape &s, const float *x, const float *offset, const float *weight) {
@@ -353,8 +583,25 @@ static int dcn_check(const DcnShape &s, const float *x, const float *offset, con
                    s.k > 0 && s.stride > 0 && s.pad >= 0,
                "sbod_dcn: bad arguments");
   SBOD_REQUIRE(s.N <= kMaxN, "sbod_dcn: kernel_size %d > 7 unsupported", s.k);
-  SBOD_REQUIRE(static_cast<int64_t>(s.M) * s.N < (1ll << 31) && static_cast<int64_t>(s.C) * s.H * s.W < (1ll << 31),
+  SBOD_REQUIRE(static_cast<int64_t>(s.M) * s.N < (1ll << 31) && static_cast<int64_t>(s.C) * s.H * s.W < (1ll << 31) &&
+                   static_cast<int64_t>(s.O) * s.K < (1ll << 31) && s.H < 65536 * 64 && s.W < 65536,
                "sbod_dcn: sizes overflow 32-bit indexing");
+  return SBOD_OK;
+}
+
+static int dcn_prepare(const DcnShape &s, const float *x, const float *offset, const float *mask_logits,
+                       void *workspace, size_t workspace_bytes, DcnWs *w, hipStream_t hs, const char *who) {
+  const size_t need = dcn_carve(s, nullptr, nullptr);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("%s: workspace %zu < %zu", who, workspace_bytes, need);
+    return SBOD_E_WORKSPACE;
+  }
+  dcn_carve(s, workspace, w);
+  const int64_t nc = static_cast<int64_t>(s.M) * s.N;
+  hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, w->coef);
+  SBOD_LAUNCHED("k_dcn_coef");
+  launch_transpose(x, w->xt, s.B, s.C, s.H * s.W, hs);   // x [B][C][HW] -> xt [B][HW][C]
+  SBOD_LAUNCHED("k_transpose(x)");
   return SBOD_OK;
 }
 
@@ -365,18 +612,23 @@ int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logi
   int st = dcn_check(s, x, offset, weight);
   if (st != SBOD_OK) return st;
   SBOD_REQUIRE(out != nullptr, "sbod_dcn_fwd_f32: out is NULL");
-  const size_t need = sbod_dcn_workspace_bytes(B, C, H, W, O, k, stride, pad);
-  if (workspace_bytes < need) {
-    set_error("sbod_dcn_fwd_f32: workspace %zu < %zu", workspace_bytes, need);
-    return SBOD_E_WORKSPACE;
-  }
   hipStream_t hs = as_stream(stream);
-  Coef *coef = static_cast<Coef *>(workspace);
-  const int64_t nc = static_cast<int64_t>(s.M) * s.N;
-  hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, coef);
-  SBOD_LAUNCHED("k_dcn_coef");
-  hipLaunchKernelGGL(k_dcn_fwd, dim3((s.M + kFM - 1) / kFM, (s.O + kFO - 1) / kFO), dim3(kDcnThreads), 0,
-                     hs, s, x, coef, weight, out);
+  DcnWs w;
+  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_fwd_f32");
+  if (st != SBOD_OK) return st;
+  launch_transpose(weight, w.wt, s.O, s.C, s.N, hs);   // W [O][C][N] -> Wf [O][N][C]
+  SBOD_LAUNCHED("k_transpose(w)");
+  const int mt = (s.M + kFM - 1) / kFM, og = (s.O + 255) / 256;
+  const int T = s.N * ((s.C + kFKC - 1) / kFKC);
+  int split = 1;
+  while (split * 2 <= T && mt * og * split < 512 && split < 64) split *= 2;
+  if (split > 1 && hipMemsetAsync(out, 0, static_cast<size_t>(s.M) * s.O * 4, hs) != hipSuccess)
+    return launch_status("hipMemsetAsync(dcn out)");
+  const dim3 grid(mt, og, split);
+  if (s.C % 4 == 0)
+    hipLaunchKernelGGL(k_dcn_fwd<4>, grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_dcn_fwd<1>, grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
   SBOD_LAUNCHED("k_dcn_fwd");
   return SBOD_OK;
 }
@@ -390,31 +642,52 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
   int st = dcn_check(s, x, offset, weight);
   if (st != SBOD_OK) return st;
   SBOD_REQUIRE(grad_out != nullptr, "sbod_dcn_bwd_f32: grad_out is NULL");
-  const size_t need = sbod_dcn_workspace_bytes(B, C, H, W, O, k, stride, pad);
-  if (workspace_bytes < need) {
-    set_error("sbod_dcn_bwd_f32: workspace %zu < %zu", workspace_bytes, need);
-    return SBOD_E_WORKSPACE;
-  }
   hipStream_t hs = as_stream(stream);
-  Coef *coef = static_cast<Coef *>(workspace);
-  const int64_t nc = static_cast<int64_t>(s.M) * s.N;
-  hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, coef);
-  SBOD_LAUNCHED("k_dcn_coef");
+  DcnWs w;
+  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_bwd_f32");
+  if (st != SBOD_OK) return st;
+  if (!mask_logits) grad_mask_logits = nullptr;
+  const size_t xbytes = static_cast<size_t>(B) * C * H * W * 4;
   if (grad_x || grad_offset || grad_mask_logits) {
-    float *gx = grad_x;
-    if (gx && hipMemsetAsync(gx, 0, static_cast<size_t>(B) * C * H * W * 4, hs) != hipSuccess)
-      return launch_status("hipMemsetAsync(dcn dx)");
-    hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM), dim3(kDcnThreads), 0, hs, s, x, coef,
-                       weight, grad_out, gx, grad_offset, mask_logits ? grad_mask_logits : nullptr);
+    launch_transpose(weight, w.wt, 1, s.O * s.C, s.N, hs);   // W [O*C][N] -> Wb [N][O][C]
+    SBOD_LAUNCHED("k_transpose(wb)");
+    if (grad_x && hipMemsetAsync(w.gxt, 0, xbytes, hs) != hipSuccess) return launch_status("hipMemsetAsync(dcn dx)");
+    const int cgs = (s.C + 255) / 256;
+    const size_t ob = static_cast<size_t>(s.M) * s.N * 4;
+    if (cgs > 1) {
+      if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob, hs) != hipSuccess) return launch_status("memset");
+      if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob, hs) != hipSuccess) return launch_status("memset");
+    }
+    hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, cgs, s.N), dim3(kDcnThreads), 0, hs, s,
+                       w.xt, w.coef, w.wt, grad_out, grad_x ? w.gxt : nullptr, grad_offset, grad_mask_logits,
+                       cgs > 1 ? 1 : 0);
     SBOD_LAUNCHED("k_dcn_bwd_data");
+    if (grad_x) {
+      launch_transpose(w.gxt, grad_x, s.B, s.H * s.W, s.C, hs);   // [B][HW][C] -> [B][C][HW]
+      SBOD_LAUNCHED("k_transpose(dx)");
+    }
   }
   if (grad_weight) {
-    if (hipMemsetAsync(grad_weight, 0, static_cast<size_t>(O) * s.K * 4, hs) != hipSuccess)
+    if (hipMemsetAsync(w.gwp, 0, static_cast<size_t>(O) * s.K * 4, hs) != hipSuccess)
       return launch_status("hipMemsetAsync(dcn dw)");
-    hipLaunchKernelGGL(k_dcn_bwd_weight,
-                       dim3((s.K + kWK - 1) / kWK, (s.M + kWSlice - 1) / kWSlice, (s.O + kWO - 1) / kWO),
-                       dim3(kDcnThreads), 0, hs, s, x, coef, grad_out, grad_weight);
+    const int gx = s.N * ((s.C + kWC - 1) / kWC), gz = (s.O + 255) / 256;
+    // one round of resident blocks (256 CUs x 2): a partial second round would double the time
+    int slices = std::max(1, 512 / (gx * gz));
+    slices = std::max(1, std::min(slices, (s.M + kWMs - 1) / kWMs));
+    int m_slice = (s.M + slices - 1) / slices;
+    m_slice = (m_slice + kWMs - 1) / kWMs * kWMs;
+    slices = (s.M + m_slice - 1) / m_slice;
+    const dim3 grid(gx, slices, gz);
+    const bool avec = (s.Ho * s.Wo) % kWMs == 0;   // 32-pixel chunks never straddle images
+    if (s.C % 4 == 0 && avec)
+      hipLaunchKernelGGL((k_dcn_bwd_weight<4, true>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+    else if (s.C % 4 == 0)
+      hipLaunchKernelGGL((k_dcn_bwd_weight<4, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+    else
+      hipLaunchKernelGGL((k_dcn_bwd_weight<1, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
     SBOD_LAUNCHED("k_dcn_bwd_weight");
+    launch_transpose(w.gwp, grad_weight, s.O, s.N, s.C, hs);   // [O][N][C] -> [O][C][N]
+    SBOD_LAUNCHED("k_transpose(dw)");
   }
   return SBOD_OK;
 }
