@@ -67,6 +67,35 @@ def bytes_per_step(B, P, C):
     return B * P * 2 * (4 + C) * 4 + 16 * P
 
 
+# Algorithmic HBM bytes per launch of the streaming (HBM-bound) kernels of one step (DESIGN.md
+# "Kernels"): every input read once, every output written once.  w = workload constants.
+ALGO_BYTES = {
+    # scores [B,P,C] + locs [B,P,4] + priors [P,4] read; decoded boxes [B,P,4] and the
+    # candidate keys (8 B each) + per-(image, class) counts written
+    'k_det_prepare': lambda w: w['B'] * w['P'] * (4 * w['C'] + 16 + 16) + 16 * w['P']
+                               + 8 * w['n_cand'] + 4 * w['B'] * w['C'],
+    # locs + scores read, their gradients written, matcher obj (i32) + overlap (f32) read,
+    # the hard-negative pool (f32) written, priors read once
+    'k_multibox': lambda w: w['B'] * w['P'] * (2 * (16 + 4 * w['C']) + 12) + 16 * w['P'],
+    # priors read per image tile, obj + overlap written, per-tile per-object partial keys (u64)
+    'k_match_tile': lambda w: w['B'] * w['P'] * (16 + 8) + w['B'] * ((w['P'] + 255) // 256) * w['Gmax'] * 8,
+}
+HBM_KERNELS = tuple(ALGO_BYTES)
+ALL_KERNELS = HBM_KERNELS + ('k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm')
+PMC_FILE = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (FETCH_SIZE and
+    WRITE_SIZE collected in separate passes; FETCH doubled on gfx950, KB -> bytes), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        return d['kernels'][kernel]['traffic_bytes_per_launch']
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(B_sample, threads):
     """The oracle (CPU restatement of the reference, pinned by tests/golden) on host cores:
     criterion fwd+bwd on B_sample images + detect on B_sample images.  kind = 'port'."""
@@ -135,8 +164,26 @@ def main():
         det = MU.detect(locs.detach(), det_scores, 0.01, 0.45, 200, priors, cfg)
         return loss, det
 
-    for _ in range(a.warmup):
+    # workload constants for the algorithmic byte counts (computed before any timing)
+    with torch.no_grad():
+        n_cand = int((torch.softmax(det_scores, 2)[:, :, 1:] > 0.01).sum().item())
+    wl = {'B': B, 'P': P, 'C': N_CLASSES, 'n_cand': n_cand, 'Gmax': max(int(b.shape[0]) for b in boxes)}
+
+    for _ in range(max(a.warmup - 1, 0)):
         step()
+    # one more untimed step with every instrumented kernel bracketed by HIP events: the
+    # per-kernel table, and the dominant HBM-bound kernel that is timed live below
+    torch.cuda.synchronize()
+    L.timing_enable('*')
+    step()
+    torch.cuda.synchronize()
+    kernel_us = {}
+    for k in ALL_KERNELS:
+        n, ms = L.timing_query(k)
+        if n:
+            kernel_us[k] = round(ms * 1e3, 1)
+    dominant = max(HBM_KERNELS, key=lambda k: kernel_us.get(k, 0.0))
+    L.timing_enable(dominant)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -151,6 +198,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    dom_n, dom_ms = L.timing_query(dominant)
+    L.timing_enable(None)
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -178,6 +227,17 @@ def main():
         'criterion_fwd_bwd_ms_median': round(crit_ms_med, 4),
         'criterion_GBps_algorithmic': round(nbytes / (crit_ms_med * 1e-3) / 1e9, 1),
     }
+    avg_s = dom_ms / max(dom_n, 1) * 1e-3
+    algo = ALGO_BYTES[dominant](wl)
+    achieved = algo / avg_s / 1e9
+    traffic = pmc_traffic(dominant)
+    line['roofline'] = {
+        'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+        'kernel': dominant, 'launches': dom_n, 'avg_us': round(avg_s * 1e6, 2),
+        'algorithmic_bytes_per_launch': algo,
+    }
+    line['kernel_us_per_step'] = kernel_us
     if not a.no_cpu_baseline:
         threads = min(os.cpu_count() or 1, 16)
         line['cpu_baseline'] = cpu_baseline(a.cpu_sample_images, threads)

@@ -44,6 +44,13 @@ const char *sbod_version(void);
 int sbod_abi_version(void);
 const char *sbod_last_error(void);
 
+/* Kernel timing for benchmarks: kernel_filter = a kernel name ("k_det_prepare"), "*" for every
+ * instrumented kernel, or NULL / "" to stop.  Each call clears previous records.  Matching
+ * launches are bracketed by HIP events on their own stream; sbod_timing_query() waits for them
+ * and returns the number of timed launches and their summed duration in milliseconds. */
+int sbod_timing_enable(const char *kernel_filter);
+int sbod_timing_query(const char *kernel, int *launches, double *total_ms);
+
 /* ---------------------------------------------------------------- a1 / a4: pairwise IoU
  * Replaces metrics.find_jaccard_overlap (metrics.py:208-252; mode SBOD_IOU_METRICS: +1e-5
  * denominator, zero-GT -> 0, zero-anchor -> -1) and iou_utils.jaccard (iou_utils.py:215-233;
@@ -108,7 +115,7 @@ int sbod_codec_f32(int op, const float *in, const float *priors, int64_t n, int6
                    float var0, float var1, float *out, void *stream);
 
 /* ---------------------------------------------------------------- a5-a10: fused criterion
- * One pass over the predictions of every criterion in models/*.py: per prior the label is
+ * One pass over the predictions of every criterion in models/ (*.py): per prior the label is
  * derived from the matcher, the box loss (a5/a6) and class loss (a7/a10) and their gradients
  * are produced together (one read of locs/scores, one write of their gradients).
  *   reg:  SBOD_REG_SMOOTHL1 (Loss.py:203-226, beta 1/9, mean over positive rows),

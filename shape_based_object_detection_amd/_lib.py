@@ -43,6 +43,8 @@ SIGNATURES = {
                               P, P, P, P, SZ, P]),
     'sbod_nms_workspace_bytes': (SZ, [I64]),
     'sbod_nms_f32': (I32, [P, P, I64, F32, I32, I32, F32, P, P, P, SZ, P]),
+    'sbod_timing_enable': (I32, [ctypes.c_char_p]),
+    'sbod_timing_query': (I32, [ctypes.c_char_p, P, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
     'sbod_dcn_fwd_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),
     'sbod_dcn_bwd_f32': (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, P,
@@ -122,3 +124,16 @@ def require_device(*tensors, what='sbod'):
         if t is not None and not t.is_cuda:
             raise SbodError('%s: expected ROCm device tensors, got a %s tensor. The sbod hot path '
                             'has no CPU implementation; move inputs to the GPU.' % (what, t.device))
+
+
+def timing_enable(kernel_filter):
+    """Bracket launches of ``kernel_filter`` (a kernel name, '*' = all instrumented kernels,
+    None = off) with HIP events on their launch stream; clears earlier records."""
+    call('sbod_timing_enable', None if kernel_filter is None else kernel_filter.encode())
+
+
+def timing_query(kernel):
+    """(launches, total_ms) recorded for ``kernel`` since timing_enable (waits for the events)."""
+    n, ms = ctypes.c_int(0), ctypes.c_double(0.0)
+    call('sbod_timing_query', kernel.encode(), ctypes.byref(n), ctypes.byref(ms))
+    return n.value, ms.value

@@ -1,6 +1,9 @@
 // Library plumbing: version, thread-local error string, launch checks, device-side grad scale.
 #include <cstdarg>
 #include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
 
 #include "sbod_common.h"
 
@@ -62,9 +65,78 @@ __global__ __launch_bounds__(256) void k_scale2(T *__restrict__ a, int64_t na, T
   }
 }
 
+// ---------------------------------------------------------------- kernel timing (bench aid)
+// When a filter is set, KernelTimer brackets matching launches with HIP events recorded on the
+// launch stream; sbod_timing_query() synchronises them and sums the elapsed times.  Events are
+// pooled, so steady-state cost is two hipEventRecord calls per timed launch.
+namespace {
+std::mutex g_tmu;
+std::string g_filter;
+struct TimingRec {
+  const char *name;
+  hipEvent_t a, b;
+};
+std::vector<TimingRec> g_recs;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t pooled_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+}  // namespace
+
+KernelTimer::KernelTimer(const char *name, hipStream_t s) : name_(name), stream_(s) {
+  std::lock_guard<std::mutex> g(g_tmu);
+  if (g_filter.empty() || (g_filter != "*" && g_filter != name)) return;
+  start_ = pooled_event();
+  if (start_ && hipEventRecord(start_, s) != hipSuccess) start_ = nullptr;
+}
+
+KernelTimer::~KernelTimer() {
+  if (!start_) return;
+  std::lock_guard<std::mutex> g(g_tmu);
+  hipEvent_t e = pooled_event();
+  if (e && hipEventRecord(e, stream_) == hipSuccess) g_recs.push_back({name_, start_, e});
+}
+
 }  // namespace sbod
 
 extern "C" {
+
+int sbod_timing_enable(const char *kernel_filter) {
+  std::lock_guard<std::mutex> g(sbod::g_tmu);
+  for (auto &r : sbod::g_recs) {
+    sbod::g_pool.push_back(r.a);
+    sbod::g_pool.push_back(r.b);
+  }
+  sbod::g_recs.clear();
+  sbod::g_filter = kernel_filter ? kernel_filter : "";
+  return SBOD_OK;
+}
+
+int sbod_timing_query(const char *kernel, int *launches, double *total_ms) {
+  SBOD_REQUIRE(kernel && launches && total_ms, "sbod_timing_query: bad arguments");
+  std::lock_guard<std::mutex> g(sbod::g_tmu);
+  int n = 0;
+  double tot = 0.0;
+  for (auto &r : sbod::g_recs) {
+    if (std::strcmp(r.name, kernel) != 0) continue;
+    float ms = 0.f;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess)
+      return sbod::launch_status("sbod_timing_query");
+    tot += ms;
+    ++n;
+  }
+  *launches = n;
+  *total_ms = tot;
+  return SBOD_OK;
+}
 
 const char *sbod_version(void) { return "sbod-hip 0.1.0 (gfx950)"; }
 int sbod_abi_version(void) { return SBOD_ABI_VERSION; }

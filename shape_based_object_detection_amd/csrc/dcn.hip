@@ -625,6 +625,7 @@ int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logi
   if (split > 1 && hipMemsetAsync(out, 0, static_cast<size_t>(s.M) * s.O * 4, hs) != hipSuccess)
     return launch_status("hipMemsetAsync(dcn out)");
   const dim3 grid(mt, og, split);
+  KernelTimer kt("k_dcn_fwd", hs);
   if (s.C % 4 == 0)
     hipLaunchKernelGGL(k_dcn_fwd<4>, grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
   else
@@ -658,9 +659,12 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
       if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob, hs) != hipSuccess) return launch_status("memset");
       if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob, hs) != hipSuccess) return launch_status("memset");
     }
-    hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, cgs, s.N), dim3(kDcnThreads), 0, hs, s,
-                       w.xt, w.coef, w.wt, grad_out, grad_x ? w.gxt : nullptr, grad_offset, grad_mask_logits,
-                       cgs > 1 ? 1 : 0);
+    {
+      KernelTimer kt("k_dcn_bwd_data", hs);
+      hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, cgs, s.N), dim3(kDcnThreads), 0, hs, s,
+                         w.xt, w.coef, w.wt, grad_out, grad_x ? w.gxt : nullptr, grad_offset, grad_mask_logits,
+                         cgs > 1 ? 1 : 0);
+    }
     SBOD_LAUNCHED("k_dcn_bwd_data");
     if (grad_x) {
       launch_transpose(w.gxt, grad_x, s.B, s.H * s.W, s.C, hs);   // [B][HW][C] -> [B][C][HW]
@@ -679,12 +683,15 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
     slices = (s.M + m_slice - 1) / m_slice;
     const dim3 grid(gx, slices, gz);
     const bool avec = (s.Ho * s.Wo) % kWMs == 0;   // 32-pixel chunks never straddle images
-    if (s.C % 4 == 0 && avec)
-      hipLaunchKernelGGL((k_dcn_bwd_weight<4, true>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
-    else if (s.C % 4 == 0)
-      hipLaunchKernelGGL((k_dcn_bwd_weight<4, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
-    else
-      hipLaunchKernelGGL((k_dcn_bwd_weight<1, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+    {
+      KernelTimer kt("k_dcn_bwd_weight", hs);
+      if (s.C % 4 == 0 && avec)
+        hipLaunchKernelGGL((k_dcn_bwd_weight<4, true>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+      else if (s.C % 4 == 0)
+        hipLaunchKernelGGL((k_dcn_bwd_weight<4, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+      else
+        hipLaunchKernelGGL((k_dcn_bwd_weight<1, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+    }
     SBOD_LAUNCHED("k_dcn_bwd_weight");
     launch_transpose(w.gwp, grad_weight, s.O, s.N, s.C, hs);   // [O][N][C] -> [O][C][N]
     SBOD_LAUNCHED("k_transpose(dw)");

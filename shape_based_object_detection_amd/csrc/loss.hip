@@ -36,31 +36,35 @@ __device__ __forceinline__ float dmax_a(float a, float b) { return a > b ? 1.f :
 __device__ __forceinline__ float dmin_a(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 
 // [n] floats global <-> LDS, 16 bytes per lane when the global side is 16-byte aligned.
-__device__ __forceinline__ void tile_load(float *dst, const float *src, int n) {
-  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-    const int n4 = n >> 2;
-    const float4 *s4 = reinterpret_cast<const float4 *>(src);
-    float4 *d4 = reinterpret_cast<float4 *>(dst);
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
-    for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
-  } else {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
-  }
-}
-__device__ __forceinline__ void tile_load(float *dst, const uint16_t *src, int n) {
+__device__ __forceinline__ void tile_load(float *dst, const float *src, int n) { tile_load_f32(dst, src, n); }
+// bf16 -> f32 staging, 8 requests in flight per thread before the LDS stores (see tile_load_f32)
+__device__ __forceinline__ void tile_load(float *__restrict__ dst, const uint16_t *__restrict__ src, int n) {
+  constexpr int kBatch = 8;
+  const int nt = blockDim.x;
   if ((reinterpret_cast<uintptr_t>(src) & 7) == 0) {
     const int n4 = n >> 2;
     const uint2 *s4 = reinterpret_cast<const uint2 *>(src);
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
-      const uint2 v = s4[i];
-      dst[4 * i] = __uint_as_float(v.x << 16);
-      dst[4 * i + 1] = __uint_as_float(v.x & 0xffff0000u);
-      dst[4 * i + 2] = __uint_as_float(v.y << 16);
-      dst[4 * i + 3] = __uint_as_float(v.y & 0xffff0000u);
+    for (int base = 0; base < n4; base += kBatch * nt) {
+      uint2 r[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int i = base + k * nt + threadIdx.x;
+        if (i < n4) r[k] = s4[i];
+      }
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int i = base + k * nt + threadIdx.x;
+        if (i < n4) {
+          dst[4 * i] = __uint_as_float(r[k].x << 16);
+          dst[4 * i + 1] = __uint_as_float(r[k].x & 0xffff0000u);
+          dst[4 * i + 2] = __uint_as_float(r[k].y << 16);
+          dst[4 * i + 3] = __uint_as_float(r[k].y & 0xffff0000u);
+        }
+      }
     }
-    for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = ldf(src + i);
+    for (int i = (n4 << 2) + threadIdx.x; i < n; i += nt) dst[i] = ldf(src + i);
   } else {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = ldf(src + i);
+    for (int i = threadIdx.x; i < n; i += nt) dst[i] = ldf(src + i);
   }
 }
 __device__ __forceinline__ void tile_store(float *dst, const float *src, int n) {
@@ -693,14 +697,17 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
              focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool};
   dim3 grid((P + kLTile - 1) / kLTile, B);
   const size_t lds = static_cast<size_t>(kLTile) * C * sizeof(float);
-  if (dtype == SBOD_DT_F32)
-    hipLaunchKernelGGL(k_multibox<float>, grid, dim3(kLTile), lds, s, a,
-                       static_cast<const float *>(locs), static_cast<const float *>(scores),
-                       static_cast<float *>(grad_locs), static_cast<float *>(grad_scores));
-  else
-    hipLaunchKernelGGL(k_multibox<uint16_t>, grid, dim3(kLTile), lds, s, a,
-                       static_cast<const uint16_t *>(locs), static_cast<const uint16_t *>(scores),
-                       static_cast<uint16_t *>(grad_locs), static_cast<uint16_t *>(grad_scores));
+  {
+    KernelTimer kt("k_multibox", s);
+    if (dtype == SBOD_DT_F32)
+      hipLaunchKernelGGL(k_multibox<float>, grid, dim3(kLTile), lds, s, a,
+                         static_cast<const float *>(locs), static_cast<const float *>(scores),
+                         static_cast<float *>(grad_locs), static_cast<float *>(grad_scores));
+    else
+      hipLaunchKernelGGL(k_multibox<uint16_t>, grid, dim3(kLTile), lds, s, a,
+                         static_cast<const uint16_t *>(locs), static_cast<const uint16_t *>(scores),
+                         static_cast<uint16_t *>(grad_locs), static_cast<uint16_t *>(grad_scores));
+  }
   SBOD_LAUNCHED("k_multibox");
   int nseg = 0;
   if (cls == SBOD_CLS_CE) {
@@ -710,9 +717,12 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
     const bool staged = segn <= kHStage;
     const size_t hl = staged ? segn * sizeof(float) : 0;
 #define SBOD_HNM(T, ST)                                                                         \
-  hipLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, ws.pool, P, B, global,    \
-                     n_pos, neg_pos_ratio, static_cast<const T *>(scores), static_cast<T *>(grad_scores), C, \
-                     npos_total, ws.hnm)
+  do {                                                                                          \
+    KernelTimer kt("k_hnm", s);                                                                 \
+    hipLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, ws.pool, P, B, global,  \
+                       n_pos, neg_pos_ratio, static_cast<const T *>(scores), static_cast<T *>(grad_scores), C, \
+                       npos_total, ws.hnm);                                                     \
+  } while (0)
     if (dtype == SBOD_DT_F32) {
       if (staged) SBOD_HNM(float, true); else SBOD_HNM(float, false);
     } else {

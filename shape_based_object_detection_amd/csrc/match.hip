@@ -463,12 +463,18 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
   dim3 grid(ntile, B);
   const size_t lds = Gmax * sizeof(GtTile);
 #define SBOD_TILE(ODM, FL)                                                                      \
-  hipLaunchKernelGGL((k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, gt_boxes, gt_labels,     \
-                     gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, \
-                     ovl, w.part, w.tcount, n_pos, B)
+  do {                                                                                          \
+    KernelTimer kt("k_match_tile", s);                                                          \
+    hipLaunchKernelGGL((k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, gt_boxes, gt_labels,   \
+                       gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, \
+                       ovl, w.part, w.tcount, n_pos, B);                                        \
+  } while (0)
 #define SBOD_FINAL(FL)                                                                          \
-  hipLaunchKernelGGL((k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, gt_labels, gt_offsets,  \
-                     w.part, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B)
+  do {                                                                                          \
+    KernelTimer kt("k_match_final", s);                                                         \
+    hipLaunchKernelGGL((k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, gt_labels, gt_offsets, \
+                       w.part, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B); \
+  } while (0)
   if (odm) {
     SBOD_TILE(true, SBOD_MATCH_ODM);
     SBOD_LAUNCHED("k_match_tile");

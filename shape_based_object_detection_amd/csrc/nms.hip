@@ -96,6 +96,27 @@ __device__ void bitonic_desc(unsigned long long *s, int N) {
   }
 }
 
+// Global -> LDS copy of n u64 keys, zero-padded to N (>= n): 8 loads in flight per thread before
+// the LDS stores (a plain copy loop waits one HBM round trip per element).
+__device__ __forceinline__ void block_copy_keys(unsigned long long *__restrict__ dst,
+                                                const unsigned long long *__restrict__ src, int n, int N) {
+  constexpr int kBatch = 8;
+  const int nt = blockDim.x;
+  for (int base = 0; base < N; base += kBatch * nt) {
+    unsigned long long r[kBatch];
+#pragma unroll
+    for (int k = 0; k < kBatch; ++k) {
+      const int i = base + k * nt + threadIdx.x;
+      r[k] = i < n ? src[i] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kBatch; ++k) {
+      const int i = base + k * nt + threadIdx.x;
+      if (i < N) dst[i] = r[k];
+    }
+  }
+}
+
 // Top-R of n unique 64-bit keys held in LDS `in` (n > R): an 11-bit, 3-pass radix select on the
 // score half (bits 63..32) finds the R-th largest score T; every key with score >= T (R plus
 // ties at T) is gathered into `out` and bitonic-sorted.  Returns how many were gathered
@@ -339,11 +360,14 @@ struct DetArgs {
 
 __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__restrict__ locs,
                                                         const float *__restrict__ scores) {
+  // dynamic LDS: score tile [kDTile][C] f32 | ballots [kDTile/64][C] u64 | slot bases [C] u32,
+  // sized to C so 6+ workgroups fit per CU (one round for B x ceil(P/256) workgroups at B=32)
   extern __shared__ float s_sc[];
-  __shared__ unsigned long long s_bal[kDTile / 64][256];
-  __shared__ uint32_t s_base[256];
   const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
   const int P = a.P, C = a.C;
+  unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_sc + kDTile * C);
+  uint32_t *s_base = reinterpret_cast<uint32_t *>(s_balf + (kDTile / 64) * C);
+#define s_bal(w, c) s_balf[(w) * C + (c)]
   const int np = min(kDTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
   tile_load_f32(s_sc, scores + rbase * C, np * C);
@@ -388,20 +412,20 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   for (int c = 1; c < C; ++c) {
     const bool take = allowed && row[c] > a.min_score;
     const unsigned long long bal = __ballot(take);
-    if (lane == 0) s_bal[wv][c] = bal;
+    if (lane == 0) s_bal(wv, c) = bal;
   }
   __syncthreads();
   for (int c = tid + 1; c < C; c += kDTile) {
     uint32_t n = 0;
-    for (int w = 0; w < kDTile / 64; ++w) n += __popcll(s_bal[w][c]);
+    for (int w = 0; w < kDTile / 64; ++w) n += __popcll(s_bal(w, c));
     s_base[c] = n ? atomicAdd(a.cand_count + b * C + c, n) : 0u;
   }
   __syncthreads();
   for (int c = 1; c < C; ++c) {
-    const unsigned long long bal = s_bal[wv][c];
+    const unsigned long long bal = s_bal(wv, c);
     if (!((bal >> lane) & 1ull)) continue;
     uint32_t slot = s_base[c] + __popcll(bal & ((1ull << lane) - 1ull));
-    for (int w = 0; w < wv; ++w) slot += __popcll(s_bal[w][c]);
+    for (int w = 0; w < wv; ++w) slot += __popcll(s_bal(w, c));
     a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(row[c], static_cast<uint32_t>(p));
   }
   if (a.dbg_probs) {
@@ -409,6 +433,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     for (int k = tid; k < np * C; k += kDTile) a.dbg_probs[rbase * C + k] = s_sc[k];
   }
 }
+#undef s_bal
 
 // ----------------------------------------------------------------------------- K2
 struct SegOut {
@@ -418,6 +443,13 @@ struct SegOut {
 };
 
 constexpr int kSegSortCap = 2048;  // segments up to this size are selected in LDS
+
+// Debug aid (off by default): -DSBOD_PHASE_CLOCKS prints per-phase cycle stamps of two blocks.
+#ifdef SBOD_PHASE_CLOCKS
+#define SEG_PHASE(i) do { __syncthreads(); if (threadIdx.x == 0) ph[i] = clock64(); } while (0)
+#else
+#define SEG_PHASE(i) do { } while (0)
+#endif
 
 __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
@@ -431,6 +463,10 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
   __shared__ int s_nk, s_cnt, s_misc[4];
   const int c = blockIdx.x + 1, b = blockIdx.y;
   const int64_t seg = static_cast<int64_t>(b) * C + c;
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  SEG_PHASE(0);
   // second pass: only the truncated classes of images whose merge could not decide
   if (need != nullptr && (need[b] == 0 || o.lastkey[seg] == 0ull)) return;
   const int n = static_cast<int>(cand_count[seg]);
@@ -453,18 +489,19 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     }
     return;
   }
+  SEG_PHASE(1);
   if (n <= q) {  // whole segment fits the window
     const int N = next_pow2(max(n, 2));
-    for (int i = threadIdx.x; i < N; i += blockDim.x) sk[i] = i < n ? g[i] : 0ull;
+    block_copy_keys(sk, g, n, N);
     __syncthreads();
     bitonic_desc(sk, N);
   } else if (n <= kSegSortCap) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) raw[i] = g[i];
+    block_copy_keys(raw, g, n, n);
     __syncthreads();
     const int m = block_topk_lds(raw, n, q, sk, WN, s_hist, s_misc);
     if (m > WN) {  // pathological ties at the threshold: sort the whole segment instead
       const int N = next_pow2(n);
-      for (int i = threadIdx.x; i < N; i += blockDim.x) raw[i] = i < n ? g[i] : 0ull;
+      block_copy_keys(raw, g, n, N);
       __syncthreads();
       bitonic_desc(raw, N);
       for (int i = threadIdx.x; i < q; i += blockDim.x) sk[i] = raw[i];
@@ -483,6 +520,7 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     __syncthreads();
     bitonic_desc(sk, N);
   }
+  SEG_PHASE(2);
   for (int i = threadIdx.x; i < q; i += blockDim.x) {
     const uint32_t p = key_low(sk[i]);
     const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
@@ -493,12 +531,19 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
   const int nk = q <= kMatrixMax
                      ? block_greedy_matrix<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, mat, &s_nk)
                      : block_greedy<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, s_flag, s_m, &s_nk);
+  SEG_PHASE(3);
   unsigned long long *ko = o.kept + seg * stride;
   for (int k = threadIdx.x; k < nk; k += blockDim.x) ko[k] = sk[kl[k]];
   if (threadIdx.x == 0) {
     o.kc[seg] = nk;
     o.lastkey[seg] = n > q ? sk[q - 1] : 0ull;
   }
+  SEG_PHASE(4);
+#ifdef SBOD_PHASE_CLOCKS
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 7) && (blockIdx.y == 0 || blockIdx.y == 5))
+    printf("seg w%d b%d c%d n=%d nk=%d: load %lld select %lld nms %lld store %lld total %lld\n", window, b, c, n,
+           nk, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[4] - ph[0]);
+#endif
 }
 
 // ----------------------------------------------------------------------------- K3
@@ -868,7 +913,7 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                    det_scores && det_count && top_k > 0,
                "sbod_detect_f32: bad arguments (B=%d P=%d C=%d top_k=%d)", B, P, C, top_k);
   SBOD_REQUIRE(box_type != SBOD_BOX_OFFSET || priors_cxcy, "sbod_detect_f32: offset boxes need priors");
-  SBOD_REQUIRE(C * kDTile * 4 <= 160 * 1024, "sbod_detect_f32: C=%d too large", C);
+  SBOD_REQUIRE(C * (kDTile * 4 + (kDTile / 64) * 8 + 4) <= 160 * 1024, "sbod_detect_f32: C=%d too large", C);
   SBOD_REQUIRE(P < (1 << 24), "sbod_detect_f32: P=%d >= 2^24 unsupported", P);
   // window 0 (auto): a first window of 64 candidates per class, then next_pow2(top_k + 1) for
   // the truncated classes of images the first merge could not decide; window > 0: one pass.
@@ -895,24 +940,39 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     return launch_status("hipMemsetAsync(detect)");
   DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.boxes, ws.cand, ws.count,
             debug_probs, debug_boxes};
-  hipLaunchKernelGGL(k_det_prepare, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
-                     static_cast<size_t>(kDTile) * C * 4, s, a, locs, scores);
+  {
+    KernelTimer kt("k_det_prepare", s);
+    hipLaunchKernelGGL(k_det_prepare, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
+                       static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 8 + C * 4, s, a, locs, scores);
+  }
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
-  hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
-                     ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
+  {
+    KernelTimer kt("k_det_segment", s);
+    hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
+                       ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
+  }
   SBOD_LAUNCHED("k_det_segment");
-  hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
-                     ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
-                     ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count);
+  {
+    KernelTimer kt("k_det_merge", s);
+    hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
+                       ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
+                       ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count);
+  }
   SBOD_LAUNCHED("k_det_merge");
   if (two) {
-    hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w2), s, ws.cand,
-                       ws.count, ws.boxes, P, C, w2, w2, max_overlap, so, ws.need);
+    {
+      KernelTimer kt("k_det_segment", s);
+      hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w2), s, ws.cand,
+                         ws.count, ws.boxes, P, C, w2, w2, max_overlap, so, ws.need);
+    }
     SBOD_LAUNCHED("k_det_segment(pass 2)");
-    hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
-                       ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, general, 2, ws.need,
-                       ws.scratch, det_boxes, det_labels, det_scores, det_count);
+    {
+      KernelTimer kt("k_det_merge", s);
+      hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
+                         ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, general, 2, ws.need,
+                         ws.scratch, det_boxes, det_labels, det_scores, det_count);
+    }
     SBOD_LAUNCHED("k_det_merge(pass 2)");
   }
   return SBOD_OK;

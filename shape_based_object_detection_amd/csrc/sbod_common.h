@@ -37,6 +37,20 @@ constexpr float kIouEps = 1e-5f;  // metrics.py:233 EPS (compared as float32, li
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Brackets a launch with HIP events on its stream when sbod_timing_enable() selected it.
+class KernelTimer {
+ public:
+  KernelTimer(const char *name, hipStream_t s);
+  ~KernelTimer();
+  KernelTimer(const KernelTimer &) = delete;
+  KernelTimer &operator=(const KernelTimer &) = delete;
+
+ private:
+  const char *name_;
+  hipStream_t stream_;
+  hipEvent_t start_ = nullptr;
+};
+
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 inline int next_pow2_host(int x) {
@@ -131,15 +145,44 @@ __device__ __forceinline__ void st4(float *p, Box4 b) {
 }
 
 // [n] floats global -> LDS, 16 bytes per lane when the source is 16-byte aligned.
-__device__ __forceinline__ void tile_load_f32(float *dst, const float *src, int n) {
+// Global -> LDS copy of n floats by the whole block.  Loads are issued in batches of 8 per
+// thread into registers before any LDS store, so a thread has 8 HBM requests in flight instead
+// of one round trip per element (the compiler cannot reorder loads past stores to `dst`).
+__device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const float *__restrict__ src, int n) {
+  constexpr int kBatch = 8;
+  const int nt = blockDim.x;
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
     const int n4 = n >> 2;
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
     float4 *d4 = reinterpret_cast<float4 *>(dst);
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
-    for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    for (int base = 0; base < n4; base += kBatch * nt) {
+      float4 r[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int i = base + k * nt + threadIdx.x;
+        if (i < n4) r[k] = s4[i];
+      }
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int i = base + k * nt + threadIdx.x;
+        if (i < n4) d4[i] = r[k];
+      }
+    }
+    for (int i = (n4 << 2) + threadIdx.x; i < n; i += nt) dst[i] = src[i];
   } else {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    for (int base = 0; base < n; base += kBatch * nt) {
+      float r[kBatch];
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int i = base + k * nt + threadIdx.x;
+        if (i < n) r[k] = src[i];
+      }
+#pragma unroll
+      for (int k = 0; k < kBatch; ++k) {
+        const int i = base + k * nt + threadIdx.x;
+        if (i < n) dst[i] = r[k];
+      }
+    }
   }
 }
 
