@@ -47,10 +47,7 @@ __device__ __forceinline__ void tile_load(float *__restrict__ dst, const uint16_
     for (int base = 0; base < n4; base += kBatch * nt) {
       uint2 r[kBatch];
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        const int i = base + k * nt + threadIdx.x;
-        if (i < n4) r[k] = s4[i];
-      }
+      for (int k = 0; k < kBatch; ++k) r[k] = s4[min(base + k * nt + static_cast<int>(threadIdx.x), n4 - 1)];
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) {
         const int i = base + k * nt + threadIdx.x;

@@ -107,7 +107,8 @@ __device__ __forceinline__ void block_copy_keys(unsigned long long *__restrict__
 #pragma unroll
     for (int k = 0; k < kBatch; ++k) {
       const int i = base + k * nt + threadIdx.x;
-      r[k] = i < n ? src[i] : 0ull;
+      const unsigned long long v = src[min(i, max(n - 1, 0))];   // unconditional: keeps r in VGPRs
+      r[k] = i < n ? v : 0ull;
     }
 #pragma unroll
     for (int k = 0; k < kBatch; ++k) {
@@ -121,14 +122,13 @@ __device__ __forceinline__ void block_copy_keys(unsigned long long *__restrict__
 // score half (bits 63..32) finds the R-th largest score T; every key with score >= T (R plus
 // ties at T) is gathered into `out` and bitonic-sorted.  Returns how many were gathered
 // (>= R; the first R of `out` are the exact top-R).  hist: 2048 u32 of LDS.
-__device__ int block_topk_lds(const unsigned long long *in, int n, int R, unsigned long long *out,
+__device__ __forceinline__ int block_topk_lds(const unsigned long long *in, int n, int R, unsigned long long *out,
                               int out_cap, uint32_t *hist, int *s_misc /* 4 */) {
   uint32_t prefix = 0, mask = 0;
   int kk = R;
-  const int shifts[3] = {21, 10, 0};
-  const int widths[3] = {11, 11, 10};
   for (int level = 0; level < 3; ++level) {
-    const int sh = shifts[level], nb = 1 << widths[level];
+    // digits: bits 31..21, 20..10, 9..0 (no runtime-indexed local arrays: they live in scratch)
+    const int sh = level == 0 ? 21 : (level == 1 ? 10 : 0), nb = level < 2 ? 2048 : 1024;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -138,9 +138,15 @@ __device__ int block_topk_lds(const unsigned long long *in, int n, int R, unsign
     __syncthreads();
     // suffix scan from the top bin: wave 0, 32 bins per lane
     if (threadIdx.x < 64) {
+      // each lane owns `per` (<= 32) consecutive bins from the top, held in registers
       const int lane = threadIdx.x, per = nb / 64;
+      uint32_t hv[32];
       uint32_t mine = 0;
-      for (int t = 0; t < per; ++t) mine += hist[nb - 1 - (lane * per + t)];
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        hv[t] = t < per ? hist[nb - 1 - (lane * per + t)] : 0u;
+        mine += hv[t];
+      }
       uint32_t incl = mine;  // inclusive prefix over lanes (lane 0 = top bins)
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t v = __shfl_up(incl, o, 64);
@@ -150,13 +156,20 @@ __device__ int block_topk_lds(const unsigned long long *in, int n, int R, unsign
       const bool hit = excl < static_cast<uint32_t>(kk) && incl >= static_cast<uint32_t>(kk);
       if (hit) {
         uint32_t acc = excl;
-        int bin = nb - 1 - lane * per;
-        for (int t = 0; t < per; ++t, --bin) {
-          const uint32_t h = hist[bin];
-          if (acc + h >= static_cast<uint32_t>(kk)) break;
-          acc += h;
+        int tb = per - 1;
+        bool done = false;
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+          if (!done && t < per) {
+            if (acc + hv[t] >= static_cast<uint32_t>(kk)) {
+              tb = t;
+              done = true;
+            } else {
+              acc += hv[t];
+            }
+          }
         }
-        s_misc[0] = bin;
+        s_misc[0] = nb - 1 - (lane * per + tb);
         s_misc[1] = kk - static_cast<int>(acc);
       }
     }
@@ -288,10 +301,12 @@ __device__ int block_greedy(const Box4 *sb, const float *sa, int n, float thr, f
   return *s_nk;
 }
 
-// Greedy NMS for n <= kMatrixMax sorted boxes: the upper-triangular suppression bit matrix is
-// computed fully in parallel (one thread per (row, 64-column block) item, 64 tests each, no
-// barriers), then wave 0 sweeps the rows in order with one alive bitset word per lane —
-// exactly the sequential greedy result.  keep/klist as block_greedy; stops after stop_after.
+// Greedy NMS for n <= kMatrixMax sorted boxes.  The upper-triangular suppression bit matrix is
+// built one 64-bit word per wave step: the row box is an LDS broadcast, the 64 lanes test the
+// 64 columns of the word and a ballot assembles it (all waves busy, no per-thread serial loops).
+// Then wave 0 sweeps the rows in order — for n <= 64 from registers (row i's word in lane i,
+// read with readlane), otherwise with one alive word per lane — exactly the sequential greedy
+// result.  keep/klist as block_greedy; stops after stop_after kept.
 constexpr int kMatrixMax = 512;
 
 template <int V>
@@ -302,45 +317,61 @@ __device__ int block_greedy_matrix(const Box4 *sb, const float *sa, int n, float
   const int nb = (n + 63) >> 6;
   const int W = nb;   // row stride in words
   const int items = n * nb;
-  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int it = wv; it < items; it += nw) {
     const int i = it / nb, cb = it - i * nb;
-    unsigned long long bits = 0;
-    if (cb >= (i >> 6)) {
-      const Box4 bi = sb[i];
-      const float ai = sa[i];
-      const int j0 = max(cb << 6, i + 1), j1 = min((cb + 1) << 6, n);
-      for (int jj = j0; jj < j1; ++jj)
-        if (suppresses<V>(bi, ai, sb[jj], sa[jj], thr, beta)) bits |= 1ull << (jj & 63);
-    }
-    mat[i * W + cb] = bits;
+    const int j = (cb << 6) + lane;
+    bool sup = false;
+    if (j > i && j < n) sup = suppresses<V>(sb[i], sa[i], sb[j], sa[j], thr, beta);
+    const unsigned long long bits = __ballot(sup);
+    if (lane == 0) mat[i * W + cb] = bits;
   }
   __syncthreads();
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const bool own = lane < nb;
-    unsigned long long alive = own ? (lane == nb - 1 && (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull) : 0ull;
-    unsigned long long row = own ? mat[lane] : 0ull;  // row 0, prefetched
     int nk = 0;
-    for (int i = 0; i < n; ++i) {
-      const unsigned long long next = (own && i + 1 < n) ? mat[(i + 1) * W + lane] : 0ull;
-      const int wl = i >> 6;
-      const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(alive), wl);
-      const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(alive >> 32), wl);
-      const unsigned long long aw = (static_cast<unsigned long long>(hi) << 32) | lo;
-      const bool alive_i = (aw >> (i & 63)) & 1ull;
-      if (lane == 0) keep[i] = alive_i ? 1 : 0;
-      if (alive_i) {
-        if (lane == 0) klist[nk] = i;
-        ++nk;
-        if (nk >= stop_after) {
-          for (int r = i + 1 + lane; r < n; r += 64) keep[r] = 0;
-          break;
-        }
-        alive &= ~row;
+    if (nb == 1) {
+      const unsigned long long row = lane < n ? mat[lane] : 0ull;
+      const uint32_t rlo = static_cast<uint32_t>(row), rhi = static_cast<uint32_t>(row >> 32);
+      unsigned long long alive = n == 64 ? ~0ull : ((1ull << n) - 1ull);
+      unsigned long long kept = 0;
+      for (int i = 0; i < n; ++i) {
+        if (!((alive >> i) & 1ull)) continue;
+        kept |= 1ull << i;
+        if (++nk >= stop_after) break;
+        const uint32_t lo = __builtin_amdgcn_readlane(rlo, i);
+        const uint32_t hi = __builtin_amdgcn_readlane(rhi, i);
+        alive &= ~((static_cast<unsigned long long>(hi) << 32) | lo);
       }
-      row = next;
+      if (lane < n) {
+        const bool k = (kept >> lane) & 1ull;
+        keep[lane] = k ? 1 : 0;
+        if (k) klist[__popcll(kept & ((1ull << lane) - 1ull))] = lane;
+      }
+    } else {
+      const bool own = lane < nb;
+      unsigned long long alive = own ? (lane == nb - 1 && (n & 63) ? ((1ull << (n & 63)) - 1ull) : ~0ull) : 0ull;
+      unsigned long long row = own ? mat[lane] : 0ull;  // row 0, prefetched
+      for (int i = 0; i < n; ++i) {
+        const unsigned long long next = (own && i + 1 < n) ? mat[(i + 1) * W + lane] : 0ull;
+        const int wl = i >> 6;
+        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(alive), wl);
+        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(alive >> 32), wl);
+        const unsigned long long aw = (static_cast<unsigned long long>(hi) << 32) | lo;
+        const bool alive_i = (aw >> (i & 63)) & 1ull;
+        if (lane == 0) keep[i] = alive_i ? 1 : 0;
+        if (alive_i) {
+          if (lane == 0) klist[nk] = i;
+          ++nk;
+          if (nk >= stop_after) {
+            for (int r = i + 1 + lane; r < n; r += 64) keep[r] = 0;
+            break;
+          }
+          alive &= ~row;
+        }
+        row = next;
+      }
     }
-  if (lane == 0) *s_nk = nk;
+    if (lane == 0) *s_nk = nk;
   }
   __syncthreads();
   return *s_nk;

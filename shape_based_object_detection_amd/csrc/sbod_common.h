@@ -155,13 +155,12 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
     const int n4 = n >> 2;
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
     float4 *d4 = reinterpret_cast<float4 *>(dst);
+    // loads are unconditional (index clamped) so the batch stays in registers — a
+    // conditionally written array is demoted to scratch memory by the compiler
     for (int base = 0; base < n4; base += kBatch * nt) {
       float4 r[kBatch];
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        const int i = base + k * nt + threadIdx.x;
-        if (i < n4) r[k] = s4[i];
-      }
+      for (int k = 0; k < kBatch; ++k) r[k] = s4[min(base + k * nt + static_cast<int>(threadIdx.x), n4 - 1)];
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) {
         const int i = base + k * nt + threadIdx.x;
@@ -173,10 +172,7 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
     for (int base = 0; base < n; base += kBatch * nt) {
       float r[kBatch];
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        const int i = base + k * nt + threadIdx.x;
-        if (i < n) r[k] = src[i];
-      }
+      for (int k = 0; k < kBatch; ++k) r[k] = src[min(base + k * nt + static_cast<int>(threadIdx.x), n - 1)];
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) {
         const int i = base + k * nt + threadIdx.x;
