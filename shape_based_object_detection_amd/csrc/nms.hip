@@ -377,6 +377,13 @@ __device__ int block_greedy_matrix(const Box4 *sb, const float *sa, int n, float
   return *s_nk;
 }
 
+// Debug aid (off by default): -DSBOD_PHASE_CLOCKS prints per-phase cycle stamps of two blocks.
+#ifdef SBOD_PHASE_CLOCKS
+#define SEG_PHASE(i) do { __syncthreads(); if (threadIdx.x == 0) ph[i] = clock64(); } while (0)
+#else
+#define SEG_PHASE(i) do { } while (0)
+#endif
+
 // ----------------------------------------------------------------------------- K1
 struct DetArgs {
   int B, P, C, box_type, act;
@@ -401,8 +408,13 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
 #define s_bal(w, c) s_balf[(w) * C + (c)]
   const int np = min(kDTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  SEG_PHASE(0);
   tile_load_f32(s_sc, scores + rbase * C, np * C);
   __syncthreads();
+  SEG_PHASE(1);
   const bool valid = tid < np;
   const int p = p0 + tid;
   const int64_t i = rbase + tid;
@@ -438,6 +450,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   // candidate compaction: ballots per (wave, class) -> ONE atomic per (workgroup, class), all
   // classes' atomics in flight together -> slots (order inside a segment is irrelevant: keys
   // are unique and sorted later)
+  SEG_PHASE(2);
   const bool allowed = valid && (a.pos == nullptr || a.pos[i] != 0);
   const int wv = tid >> 6;
   for (int c = 1; c < C; ++c) {
@@ -452,6 +465,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     s_base[c] = n ? atomicAdd(a.cand_count + b * C + c, n) : 0u;
   }
   __syncthreads();
+  SEG_PHASE(3);
   for (int c = 1; c < C; ++c) {
     const unsigned long long bal = s_bal(wv, c);
     if (!((bal >> lane) & 1ull)) continue;
@@ -459,6 +473,12 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     for (int w = 0; w < wv; ++w) slot += __popcll(s_bal(w, c));
     a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(row[c], static_cast<uint32_t>(p));
   }
+  SEG_PHASE(4);
+#ifdef SBOD_PHASE_CLOCKS
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 20) && (blockIdx.y == 0 || blockIdx.y == 5))
+    printf("prep x%d b%d: tile %lld compute %lld ballot+atomic %lld keys %lld total %lld\n", blockIdx.x, b,
+           ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[4] - ph[0]);
+#endif
   if (a.dbg_probs) {
     __syncthreads();
     for (int k = tid; k < np * C; k += kDTile) a.dbg_probs[rbase * C + k] = s_sc[k];
@@ -475,12 +495,6 @@ struct SegOut {
 
 constexpr int kSegSortCap = 2048;  // segments up to this size are selected in LDS
 
-// Debug aid (off by default): -DSBOD_PHASE_CLOCKS prints per-phase cycle stamps of two blocks.
-#ifdef SBOD_PHASE_CLOCKS
-#define SEG_PHASE(i) do { __syncthreads(); if (threadIdx.x == 0) ph[i] = clock64(); } while (0)
-#else
-#define SEG_PHASE(i) do { } while (0)
-#endif
 
 __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
@@ -575,6 +589,178 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     printf("seg w%d b%d c%d n=%d nk=%d: load %lld select %lld nms %lld store %lld total %lld\n", window, b, c, n,
            nk, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[4] - ph[0]);
 #endif
+}
+
+// ----------------------------------------------------------------------------- K2 (wave form)
+// Pass-1 segments (window <= 64): one wave per (image, class) segment, nothing block-wide.
+//   select: radix select of the q-th largest 64-bit key, 8-bit digits from the top, with a
+//           per-wave LDS histogram; stops at the first digit whose bin holds exactly the keys
+//           still needed.  Keys live in registers for n <= kWaveRegKeys, else are streamed.
+//   sort:   the q selected keys, one per lane, bitonic over lanes (shuffles).
+//   NMS:    greedy in rank order; a kept box broadcasts itself (readlane) and one ballot gives
+//           its suppression row, so rows are built only for boxes that survive.
+// Results are identical to k_det_segment (same keys, same rank order, same suppression test).
+constexpr int kWaveRegKeys = 2048;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__global__ __launch_bounds__(64) void k_det_segment_wave(
+    const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
+    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
+    const int32_t *__restrict__ need) {
+  __shared__ uint32_t s_hist[256];
+  __shared__ unsigned long long s_sel[64];
+  const int lane = threadIdx.x;
+  const int c = blockIdx.x + 1, b = blockIdx.y;
+  const int64_t seg = static_cast<int64_t>(b) * C + c;
+  if (need != nullptr && (need[b] == 0 || o.lastkey[seg] == 0ull)) return;
+  const int n = static_cast<int>(cand_count[seg]);
+  if (n == 0) {
+    if (lane == 0) {
+      o.kc[seg] = 0;
+      o.lastkey[seg] = 0;
+    }
+    return;
+  }
+  const unsigned long long *g = cand + seg * P;
+  const int q = min(n, window);
+  const bool regs = n <= kWaveRegKeys;
+  unsigned long long kr[kWaveRegKeys / 64];
+  if (regs) {
+#pragma unroll
+    for (int t = 0; t < kWaveRegKeys / 64; ++t) {
+      const int i = lane + 64 * t;
+      const unsigned long long v = g[min(i, n - 1)];
+      kr[t] = i < n ? v : 0ull;   // real keys are never 0 (score > 0)
+    }
+  }
+  // ---- select: keys with (key >> sh) >= (prefix >> sh) are exactly the top q
+  unsigned long long prefix = 0;
+  int sh = 64;
+  if (n > q) {
+    int kk = q;
+    for (int level = 0; level < 8; ++level) {
+      const int dsh = 56 - 8 * level;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s_hist[lane + 64 * j] = 0u;
+      wave_lds_sync();
+      auto count = [&](unsigned long long k) {
+        if (k != 0ull && (level == 0 || ((k ^ prefix) >> (dsh + 8)) == 0ull))
+          atomicAdd(&s_hist[(k >> dsh) & 255ull], 1u);
+      };
+      if (regs) {
+#pragma unroll
+        for (int t = 0; t < kWaveRegKeys / 64; ++t) count(kr[t]);
+      } else {
+        for (int i = lane; i < n; i += 64) count(g[i]);
+      }
+      wave_lds_sync();
+      // lane owns bins 255 - 4 lane - (0..3), top first
+      uint32_t hv[4], mine = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hv[j] = s_hist[255 - 4 * lane - j];
+        mine += hv[j];
+      }
+      uint32_t incl = mine;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+      }
+      const uint32_t excl = incl - mine;
+      const bool hit = excl < static_cast<uint32_t>(kk) && incl >= static_cast<uint32_t>(kk);
+      int bin = 0, left = 0, hb = 0;
+      if (hit) {
+        uint32_t acc = excl;
+        bool done = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!done) {
+            if (acc + hv[j] >= static_cast<uint32_t>(kk)) {
+              bin = 255 - 4 * lane - j;
+              left = kk - static_cast<int>(acc);
+              hb = static_cast<int>(hv[j]);
+              done = true;
+            } else {
+              acc += hv[j];
+            }
+          }
+        }
+      }
+      const unsigned long long hm = __ballot(hit);
+      const int hl = __ffsll(static_cast<long long>(hm)) - 1;
+      bin = __builtin_amdgcn_readlane(bin, hl);
+      left = __builtin_amdgcn_readlane(left, hl);
+      hb = __builtin_amdgcn_readlane(hb, hl);
+      prefix |= static_cast<unsigned long long>(bin) << dsh;
+      sh = dsh;
+      kk = left;
+      if (hb == left) break;   // the whole bin is selected: no finer digit needed
+      wave_lds_sync();
+    }
+  }
+  // ---- compact the selected keys (exactly q) into s_sel
+  {
+    int base = 0;
+    auto take = [&](unsigned long long k) {
+      const bool sel = k != 0ull && (sh >= 64 || (k >> sh) >= (prefix >> sh));
+      const unsigned long long bal = __ballot(sel);
+      if (sel) s_sel[base + __popcll(bal & ((1ull << lane) - 1ull))] = k;
+      base += __popcll(bal);
+    };
+    if (regs) {
+#pragma unroll
+      for (int t = 0; t < kWaveRegKeys / 64; ++t) take(kr[t]);
+    } else {
+      for (int i0 = 0; i0 < n; i0 += 64) take(lane + i0 < n ? g[lane + i0] : 0ull);
+    }
+  }
+  wave_lds_sync();
+  // ---- sort descending over lanes
+  unsigned long long v = lane < q ? s_sel[lane] : 0ull;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const unsigned long long w = shfl_xor_u64(v, j);
+      const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
+      v = keep_max ? (v > w ? v : w) : (v < w ? v : w);
+    }
+  }
+  // ---- greedy NMS over the q ranked boxes (torchvision suppression rule)
+  Box4 bx{0.f, 0.f, 0.f, 0.f};
+  float ar = 0.f;
+  if (lane < q) {
+    bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(v)));
+    ar = (bx.c - bx.a) * (bx.d - bx.b);
+  }
+  unsigned long long alive = q == 64 ? ~0ull : ((1ull << q) - 1ull);
+  unsigned long long kept = 0;
+  for (int i = 0; i < q; ++i) {
+    if (!((alive >> i) & 1ull)) continue;
+    kept |= 1ull << i;
+    const Box4 bi{readlane_f(bx.a, i), readlane_f(bx.b, i), readlane_f(bx.c, i), readlane_f(bx.d, i)};
+    const float ai = readlane_f(ar, i);
+    const bool sup = lane > i && lane < q && suppresses<SBOD_NMS_TV>(bi, ai, bx, ar, thr, 1.f);
+    alive &= ~__ballot(sup);
+  }
+  unsigned long long *ko = o.kept + seg * stride;
+  if ((kept >> lane) & 1ull) ko[__popcll(kept & ((1ull << lane) - 1ull))] = v;
+  const uint32_t llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), q - 1);
+  const uint32_t lhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), q - 1);
+  if (lane == 0) {
+    o.kc[seg] = __popcll(kept);
+    o.lastkey[seg] = n > q ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
+  }
 }
 
 // ----------------------------------------------------------------------------- K3
@@ -980,8 +1166,12 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   SegOut so{ws.kept, ws.kc, ws.lastkey};
   {
     KernelTimer kt("k_det_segment", s);
-    hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
-                       ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
+    if (w1 <= 64)
+      hipLaunchKernelGGL(k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, ws.boxes,
+                         P, C, w1, w2, max_overlap, so, nullptr);
+    else
+      hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
+                         ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
   }
   SBOD_LAUNCHED("k_det_segment");
   {
