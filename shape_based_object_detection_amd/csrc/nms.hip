@@ -22,6 +22,7 @@
 namespace sbod {
 
 constexpr int kDTile = 256;
+constexpr int kPrepRegC = 32;    // prepare: class rows up to this width are processed in registers
 constexpr int kSegThreads = 256;
 constexpr int kMaxWindow = 4096;   // LDS-resident window (keys + boxes + areas + flags)
 constexpr int kMergeThreads = 1024;
@@ -404,8 +405,9 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
   const int P = a.P, C = a.C;
   unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_sc + kDTile * C);
-  uint32_t *s_base = reinterpret_cast<uint32_t *>(s_balf + (kDTile / 64) * C);
+  uint32_t *s_wbf = reinterpret_cast<uint32_t *>(s_balf + (kDTile / 64) * C);   // per-wave slot bases
 #define s_bal(w, c) s_balf[(w) * C + (c)]
+#define s_wb(w, c) s_wbf[(w) * C + (c)]
   const int np = min(kDTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
 #ifdef SBOD_PHASE_CLOCKS
@@ -433,7 +435,30 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     if (a.box_type == SBOD_BOX_CORNER) st4(locs + 4 * i, d);  // models/utils.py:224 clamp_ in place
     st4(a.boxes_ws + 4 * i, d);
     if (a.dbg_boxes) st4(a.dbg_boxes + 4 * i, d);
-    if (a.act == SBOD_ACT_SOFTMAX) {
+    if (C <= kPrepRegC) {
+      // the row in registers (unconditional, fully unrolled loads): one LDS round trip, not 3C
+      float r[kPrepRegC];
+#pragma unroll
+      for (int k = 0; k < kPrepRegC; ++k) r[k] = row[min(k, C - 1)];
+      if (a.act == SBOD_ACT_SOFTMAX) {
+        float m = r[0];
+#pragma unroll
+        for (int k = 1; k < kPrepRegC; ++k) m = k < C ? fmaxf(m, r[k]) : m;
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < kPrepRegC; ++k) {
+          r[k] = expf(r[k] - m);
+          sum = k < C ? sum + r[k] : sum;
+        }
+#pragma unroll
+        for (int k = 0; k < kPrepRegC; ++k)
+          if (k < C) row[k] = r[k] / sum;
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPrepRegC; ++k)
+          if (k < C) row[k] = 1.f / (1.f + expf(-r[k]));
+      }
+    } else if (a.act == SBOD_ACT_SOFTMAX) {
       float m = row[0];
       for (int k = 1; k < C; ++k) m = fmaxf(m, row[k]);
       float s = 0.f;
@@ -460,18 +485,46 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   }
   __syncthreads();
   for (int c = tid + 1; c < C; c += kDTile) {
-    uint32_t n = 0;
-    for (int w = 0; w < kDTile / 64; ++w) n += __popcll(s_bal(w, c));
-    s_base[c] = n ? atomicAdd(a.cand_count + b * C + c, n) : 0u;
+    uint32_t nwv[kDTile / 64], n = 0;
+#pragma unroll
+    for (int w = 0; w < kDTile / 64; ++w) {
+      nwv[w] = __popcll(s_bal(w, c));
+      n += nwv[w];
+    }
+    uint32_t base = n ? atomicAdd(a.cand_count + b * C + c, n) : 0u;
+#pragma unroll
+    for (int w = 0; w < kDTile / 64; ++w) {
+      s_wb(w, c) = base;
+      base += nwv[w];
+    }
   }
   __syncthreads();
   SEG_PHASE(3);
-  for (int c = 1; c < C; ++c) {
-    const unsigned long long bal = s_bal(wv, c);
-    if (!((bal >> lane) & 1ull)) continue;
-    uint32_t slot = s_base[c] + __popcll(bal & ((1ull << lane) - 1ull));
-    for (int w = 0; w < wv; ++w) slot += __popcll(s_bal(w, c));
-    a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(row[c], static_cast<uint32_t>(p));
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  if (C <= 64) {
+    // lane c holds class c's ballot and slot base for this wave; the class loop reads them
+    // with readlane (no LDS round trips inside the loop)
+    const unsigned long long mybal = lane < C ? s_bal(wv, lane) : 0ull;
+    const uint32_t mywb = lane < C ? s_wb(wv, lane) : 0u;
+    const uint32_t blo = static_cast<uint32_t>(mybal), bhi = static_cast<uint32_t>(mybal >> 32);
+    for (int c = 1; c < C; ++c) {
+      // readlane returns int: go through uint32_t so the low word is not sign-extended
+      const uint32_t rl = static_cast<uint32_t>(__builtin_amdgcn_readlane(blo, c));
+      const uint32_t rh = static_cast<uint32_t>(__builtin_amdgcn_readlane(bhi, c));
+      const unsigned long long bal = (static_cast<unsigned long long>(rh) << 32) | rl;
+      if (bal == 0ull) continue;
+      const uint32_t wb = __builtin_amdgcn_readlane(mywb, c);
+      if ((bal >> lane) & 1ull)
+        a.cand[(static_cast<int64_t>(b) * C + c) * P + wb + __popcll(bal & lt)] =
+            make_key(row[c], static_cast<uint32_t>(p));
+    }
+  } else {
+    for (int c = 1; c < C; ++c) {
+      const unsigned long long bal = s_bal(wv, c);
+      if (!((bal >> lane) & 1ull)) continue;
+      a.cand[(static_cast<int64_t>(b) * C + c) * P + s_wb(wv, c) + __popcll(bal & lt)] =
+          make_key(row[c], static_cast<uint32_t>(p));
+    }
   }
   SEG_PHASE(4);
 #ifdef SBOD_PHASE_CLOCKS
@@ -485,6 +538,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   }
 }
 #undef s_bal
+#undef s_wb
 
 // ----------------------------------------------------------------------------- K2
 struct SegOut {
@@ -850,10 +904,14 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     ol[r] = c;
     os[r] = key_score(key);
   };
-  auto class_of = [&](const uint32_t *off, int i) {
-    int c = 1;
-    while (off[c + 1] <= static_cast<uint32_t>(i)) ++c;
-    return c;
+  auto class_of = [&](const uint32_t *off, int i) {   // largest c in [1, C-1] with off[c] <= i
+    int lo = 1, hi = C - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= static_cast<uint32_t>(i)) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
   };
   auto ck_of = [&](int c, int pos) { return kept[(sb0 + c) * window_stride + pos]; };
   if (total == 0) {  // models/utils.py:274-277 placeholder
@@ -889,7 +947,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
       uint32_t acc = 0;
       s_zoff[0] = 0;
       for (int c = 0; c < C; ++c) {
-        const uint32_t k = c == 0 ? 0u : min(kc[sb0 + c], static_cast<uint32_t>(R));
+        const uint32_t k = min(s_kc[c], static_cast<uint32_t>(R));   // s_kc[0] == 0 (LDS, not HBM)
         acc += k;
         s_zoff[c + 1] = acc;
       }
@@ -1130,7 +1188,7 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                    det_scores && det_count && top_k > 0,
                "sbod_detect_f32: bad arguments (B=%d P=%d C=%d top_k=%d)", B, P, C, top_k);
   SBOD_REQUIRE(box_type != SBOD_BOX_OFFSET || priors_cxcy, "sbod_detect_f32: offset boxes need priors");
-  SBOD_REQUIRE(C * (kDTile * 4 + (kDTile / 64) * 8 + 4) <= 160 * 1024, "sbod_detect_f32: C=%d too large", C);
+  SBOD_REQUIRE(C * (kDTile * 4 + (kDTile / 64) * 12) <= 160 * 1024, "sbod_detect_f32: C=%d too large", C);
   SBOD_REQUIRE(P < (1 << 24), "sbod_detect_f32: P=%d >= 2^24 unsupported", P);
   // window 0 (auto): a first window of 64 candidates per class, then next_pow2(top_k + 1) for
   // the truncated classes of images the first merge could not decide; window > 0: one pass.
@@ -1160,7 +1218,7 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   {
     KernelTimer kt("k_det_prepare", s);
     hipLaunchKernelGGL(k_det_prepare, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
-                       static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 8 + C * 4, s, a, locs, scores);
+                       static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, locs, scores);
   }
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
