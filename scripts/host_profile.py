@@ -40,4 +40,5 @@ for _ in range(200):
 torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
-st.sort_stats('tottime').print_stats(25)
+st.sort_stats("tottime").print_stats(40)
+st.sort_stats("cumulative").print_stats(40)

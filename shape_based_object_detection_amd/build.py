@@ -9,7 +9,9 @@ default IEEE fp32 division.
 import argparse
 import concurrent.futures as cf
 import glob
+import json
 import os
+import re
 import shutil
 import subprocess
 
@@ -19,6 +21,7 @@ CSRC = os.path.join(PKG, 'csrc')
 INCLUDE = os.path.join(REPO, 'include')
 OBJDIR = os.path.join(PKG, 'build')
 LIB = os.path.join(PKG, 'lib', 'libsbod_hip.so')
+RESOURCES = os.path.join(PKG, 'lib', 'kernel_resources.json')
 ARCH = os.environ.get('SBOD_OFFLOAD_ARCH', 'gfx950')
 
 CXXFLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-ffp-contract=off',
@@ -43,13 +46,32 @@ def _stale(target, sources):
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+_RES_RE = re.compile(r'remark: +(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|'
+                     r'LDS Size \[bytes/block\]): (\S+)')
+
+
+def _resource_usage(stderr):
+    """Per-kernel register / scratch / LDS / occupancy figures from -Rpass-analysis remarks."""
+    out, cur = {}, None
+    for m in _RES_RE.finditer(stderr):
+        key, val = m.group(1), m.group(2)
+        if key == 'Function Name':
+            cur = out.setdefault(val, {})
+        elif cur is not None:
+            cur[key.split(' ')[0]] = int(val)
+    return out
+
+
 def _compile(src, force):
     obj = os.path.join(OBJDIR, os.path.basename(src) + '.o')
-    if force or _stale(obj, [src] + _deps()):
-        cmd = [hipcc()] + CXXFLAGS + ['-c', src, '-o', obj]
+    res = obj + '.resources.json'
+    if force or _stale(obj, [src] + _deps()) or not os.path.exists(res):
+        cmd = [hipcc()] + CXXFLAGS + ['-Rpass-analysis=kernel-resource-usage', '-c', src, '-o', obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError('hipcc failed for %s:\n%s\n%s' % (src, ' '.join(cmd), r.stderr))
+        with open(res, 'w') as f:
+            json.dump(_resource_usage(r.stderr), f, indent=1, sort_keys=True)
     return obj
 
 
@@ -60,6 +82,12 @@ def build(force=False, jobs=8, verbose=True):
     srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, 16))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    usage = {}
+    for o in objs:
+        with open(o + '.resources.json') as f:
+            usage.update(json.load(f))
+    with open(RESOURCES, 'w') as f:     # kernel resource table (tests assert no scratch use)
+        json.dump(usage, f, indent=1, sort_keys=True)
     if force or _stale(LIB, objs):
         cmd = [hipcc(), '-shared', '-fPIC', '--offload-arch=' + ARCH, '-o', LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)

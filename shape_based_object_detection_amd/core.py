@@ -44,7 +44,7 @@ def pack_gt(boxes, labels, device=None, allow_empty=False):
     does (``overlap.max(dim=0)`` of an empty matrix, models/SSD512.py:538)."""
     if len(boxes) != len(labels):
         raise ValueError('boxes and labels must have the same length')
-    counts = [len(b) for b in boxes]
+    counts = [b.shape[0] for b in boxes]
     if not allow_empty and 0 in counts:
         raise RuntimeError('max(): Expected reduction dim 0 to have non-zero size (an image has no '
                            'ground-truth objects, as in the reference criterion)')
@@ -252,11 +252,16 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     nb = L.lib().sbod_detect_workspace_bytes(B, P, C)
     ws = workspace(nb, dev, 'detect')
     fn = -1.0 if final_nms is None else float(final_nms)
+    full = None
     for w in (window, 4096):
         L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
                L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(w), L.ptr(out_b),
                L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg_p), L.ptr(dbg_b), L.ptr(ws), nb,
                L.stream_of(sc))
+        if full is None:
+            # the per-image views for the usual all-full case are built while the kernels run
+            # (host work overlapped with the device); discarded if some image has fewer
+            full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
         counts = cnt.cpu().tolist()
         if min(counts) >= 0:
             break
@@ -265,8 +270,8 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
                           'top-%d outputs exactly (pathological suppression); unsupported' % top_k)
     if in_place and lc is not locs:
         locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
-    if min(counts) == top_k:     # every image full (the usual eval case): one view op each
-        res = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
+    if min(counts) == top_k:     # every image full (the usual eval case)
+        res = full
     else:
         sizes = []
         for n in counts:

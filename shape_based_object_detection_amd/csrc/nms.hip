@@ -70,6 +70,23 @@ __device__ __forceinline__ bool suppresses(const Box4 &bi, float ai, const Box4 
   }
 }
 
+// Branch-free torchvision test for wave code: sup is decided by the +-2^-18 margin; `amb`
+// marks the rare lanes that need the exact division (then done under a wave-uniform branch).
+__device__ __forceinline__ bool tv_fast(const Box4 &bi, float ai, const Box4 &bj, float aj, float thr,
+                                        bool &amb, float &inter, float &u) {
+  const float xx1 = fmaxf(bj.a, bi.a), yy1 = fmaxf(bj.b, bi.b);
+  const float xx2 = fminf(bj.c, bi.c), yy2 = fminf(bj.d, bi.d);
+  const float w = fmaxf(xx2 - xx1, 0.f), h = fmaxf(yy2 - yy1, 0.f);
+  inter = w * h;
+  u = (ai + aj) - inter;
+  const float t = thr * u;
+  const bool hi = inter > t * (1.f + 3.8147e-6f);
+  const bool lo = inter < t * (1.f - 3.8147e-6f);
+  const bool ok = u > 0.f && u < 3.0e38f;
+  amb = !(ok && (hi || lo));
+  return ok && hi;
+}
+
 __device__ __forceinline__ int next_pow2(int x) {
   int p = 1;
   while (p < x) p <<= 1;
@@ -672,6 +689,7 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
     const int32_t *__restrict__ need) {
   __shared__ uint32_t s_hist[256];
   __shared__ unsigned long long s_sel[64];
+  __shared__ Box4 s_box[64];
   const int lane = threadIdx.x;
   const int c = blockIdx.x + 1, b = blockIdx.y;
   const int64_t seg = static_cast<int64_t>(b) * C + c;
@@ -687,6 +705,10 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
   const unsigned long long *g = cand + seg * P;
   const int q = min(n, window);
   const bool regs = n <= kWaveRegKeys;
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  SEG_PHASE(0);
   unsigned long long kr[kWaveRegKeys / 64];
   if (regs) {
 #pragma unroll
@@ -696,6 +718,7 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
       kr[t] = i < n ? v : 0ull;   // real keys are never 0 (score > 0)
     }
   }
+  SEG_PHASE(1);
   // ---- select: keys with (key >> sh) >= (prefix >> sh) are exactly the top q
   unsigned long long prefix = 0;
   int sh = 64;
@@ -712,7 +735,8 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
       };
       if (regs) {
 #pragma unroll
-        for (int t = 0; t < kWaveRegKeys / 64; ++t) count(kr[t]);
+        for (int t = 0; t < kWaveRegKeys / 64; ++t)
+          if (64 * t < n) count(kr[t]);      // uniform guard: the remaining slots are padding
       } else {
         for (int i = lane; i < n; i += 64) count(g[i]);
       }
@@ -773,39 +797,74 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
     };
     if (regs) {
 #pragma unroll
-      for (int t = 0; t < kWaveRegKeys / 64; ++t) take(kr[t]);
+      for (int t = 0; t < kWaveRegKeys / 64; ++t)
+        if (64 * t < n) take(kr[t]);
     } else {
       for (int i0 = 0; i0 < n; i0 += 64) take(lane + i0 < n ? g[lane + i0] : 0ull);
     }
   }
   wave_lds_sync();
-  // ---- sort descending over lanes
+  SEG_PHASE(2);
+  // ---- sort descending over lanes; the selected boxes are fetched BEFORE the sort (their
+  // latency overlaps it) and each key carries its original lane to find its box afterwards
   unsigned long long v = lane < q ? s_sel[lane] : 0ull;
+  Box4 bu{0.f, 0.f, 0.f, 0.f};
+  if (lane < q) bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(v)));
+  int pos = lane;
 #pragma unroll
   for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
       const unsigned long long w = shfl_xor_u64(v, j);
+      const int wp = __shfl_xor(pos, j, 64);
       const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
-      v = keep_max ? (v > w ? v : w) : (v < w ? v : w);
+      const bool take = keep_max ? (w > v) : (w < v);   // keys are unique (padding 0 never moves past a key)
+      v = take ? w : v;
+      pos = take ? wp : pos;
     }
   }
+  s_box[lane] = bu;
+  wave_lds_sync();
+  SEG_PHASE(3);
   // ---- greedy NMS over the q ranked boxes (torchvision suppression rule)
   Box4 bx{0.f, 0.f, 0.f, 0.f};
   float ar = 0.f;
   if (lane < q) {
-    bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(v)));
+    bx = s_box[pos];
     ar = (bx.c - bx.a) * (bx.d - bx.b);
   }
   unsigned long long alive = q == 64 ? ~0ull : ((1ull << q) - 1ull);
   unsigned long long kept = 0;
-  for (int i = 0; i < q; ++i) {
-    if (!((alive >> i) & 1ull)) continue;
-    kept |= 1ull << i;
-    const Box4 bi{readlane_f(bx.a, i), readlane_f(bx.b, i), readlane_f(bx.c, i), readlane_f(bx.d, i)};
-    const float ai = readlane_f(ar, i);
-    const bool sup = lane > i && lane < q && suppresses<SBOD_NMS_TV>(bi, ai, bx, ar, thr, 1.f);
-    alive &= ~__ballot(sup);
+  // suppression rows do not depend on the greedy state: 8 rows are built as independent
+  // chains (instruction-level parallelism for a lone wave), then applied in rank order
+  constexpr int kRowBatch = 8;
+  for (int i0 = 0; i0 < q; i0 += kRowBatch) {
+    if (!(alive >> i0)) break;                 // nothing left alive at or after i0
+    unsigned long long rows[kRowBatch];
+#pragma unroll
+    for (int u = 0; u < kRowBatch; ++u) {
+      const int i = min(i0 + u, 63);
+      const Box4 bi{readlane_f(bx.a, i), readlane_f(bx.b, i), readlane_f(bx.c, i), readlane_f(bx.d, i)};
+      const float ai = readlane_f(ar, i);
+      const bool act = lane > i && lane < q;
+      bool amb;
+      float inter, un;
+      const bool sup = tv_fast(bi, ai, bx, ar, thr, amb, inter, un);
+      rows[u] = __ballot(act && sup);
+      const unsigned long long am = __ballot(act && amb);
+      if (am != 0ull) {   // rare: exact division for the lanes within the margin
+        const bool ex = act && amb && (inter / un > thr);
+        rows[u] = (rows[u] & ~am) | __ballot(ex);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kRowBatch; ++u) {
+      const int i = i0 + u;
+      if (i < q && ((alive >> i) & 1ull)) {
+        kept |= 1ull << i;
+        alive &= ~rows[u];
+      }
+    }
   }
   unsigned long long *ko = o.kept + seg * stride;
   if ((kept >> lane) & 1ull) ko[__popcll(kept & ((1ull << lane) - 1ull))] = v;
@@ -815,6 +874,12 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
     o.kc[seg] = __popcll(kept);
     o.lastkey[seg] = n > q ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
   }
+  SEG_PHASE(4);
+#ifdef SBOD_PHASE_CLOCKS
+  if (lane == 0 && (c == 1 || c == 8) && (b == 0 || b == 5))
+    printf("segw b%d c%d n=%d: load %lld select+compact %lld sort+boxes %lld nms+store %lld total %lld\n", b, c, n,
+           ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[4] - ph[0]);
+#endif
 }
 
 // ----------------------------------------------------------------------------- K3
@@ -860,6 +925,10 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
   const int b = blockIdx.x, tid = threadIdx.x;
   const int64_t sb0 = static_cast<int64_t>(b) * C;
   if (pass == 2 && need[b] == 0) return;
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  SEG_PHASE(0);
   const int window_stride = window;
   for (int c = tid; c < C; c += blockDim.x) {   // all per-class loads in flight together
     s_kc[c] = c == 0 ? 0u : kc[sb0 + c];
@@ -891,6 +960,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
       out_count[b] = -1;
     }
   };
+  SEG_PHASE(1);
   if (pass == 1 && tid == 0) need[b] = 0;
   const int total = static_cast<int>(s_off[C]);
   const bool any_trunc = s_any_trunc != 0;
@@ -941,7 +1011,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
   const int R = final_nms < 0.f ? top_k : min(total, general ? kMergeStage : kFastStage);
   int *ord = nullptr;          // ord[r] = class << 24 | position, r < R
   unsigned long long *sk = nullptr;
-  bool fast = !general;
+  bool fast = !general && R <= kFastOut;
   if (fast) {
     if (tid == 0) {
       uint32_t acc = 0;
@@ -968,6 +1038,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
               (0xffffffffu - ((static_cast<uint32_t>(c) << 24) | pos));
     }
     __syncthreads();
+    SEG_PHASE(2);
     int m;
     if (nz <= R) {
       const int N = next_pow2(max(nz, 2));
@@ -982,6 +1053,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
       if (tid == 0) out_count[b] = -1;
       return;
     }
+    SEG_PHASE(3);
     for (int r = tid; r < R; r += blockDim.x) ord[r] = static_cast<int>(0xffffffffu - static_cast<uint32_t>(top[r]));
     __syncthreads();
   } else {
@@ -1029,11 +1101,18 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
       undecided();
       return;
     }
+    SEG_PHASE(4);
     for (int r = tid; r < top_k; r += blockDim.x) {
       const unsigned long long ck = entry(r, c);
       emit(r, c, ck);
     }
     if (tid == 0) out_count[b] = top_k;
+    SEG_PHASE(5);
+#ifdef SBOD_PHASE_CLOCKS
+    if (tid == 0 && (b == 0 || b == 5))
+      printf("merge p%d b%d nz=%d: prologue %lld gather %lld select+sort %lld ord+check %lld emit %lld total %lld\n",
+             pass, b, total, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[5] - ph[4], ph[5] - ph[0]);
+#endif
     return;
   }
   // detect_tools: class-agnostic greedy NMS at final_nms over the merged order, first top_k

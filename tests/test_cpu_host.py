@@ -95,3 +95,17 @@ def test_synth_recipe_is_deterministic():
     loc, sc = synth.make_preds(2, prior_table('SSD300').shape[0], 21, seed=1, bg_shift=6.0)
     assert loc.shape == (2, 8732, 4) and sc.shape == (2, 8732, 21)
     assert sc[..., 0].mean() > 5.0
+
+
+def test_no_kernel_spills_to_scratch():
+    """Every HIP kernel keeps its locals in registers/LDS: a scratch (private memory) array is
+    the classic silent slowdown (a conditionally written local array demoted by the compiler).
+    The table is written by build.py from the compiler's kernel-resource-usage remarks."""
+    import json
+    path = os.path.join(REPO, 'shape_based_object_detection_amd', 'lib', 'kernel_resources.json')
+    if not os.path.exists(path):
+        pytest.skip('library not built with resource remarks')
+    usage = json.load(open(path))
+    assert len(usage) >= 20
+    bad = {k: v['ScratchSize'] for k, v in usage.items() if v.get('ScratchSize', 0) > 0}
+    assert bad == {}, bad
