@@ -232,6 +232,23 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
                      float *grad_mask_logits, float *grad_weight, void *workspace,
                      size_t workspace_bytes, void *stream);
 
+/* ---------------------------------------------------------------- f2: VOC 11-point mAP
+ * metrics.calculate_mAP (metrics.py:8-145).  Detections and ground truth are the concatenated
+ * per-image lists: det_offsets / true_offsets [B+1] int32 give each image's row range.
+ *   det_boxes [D,4] f32 xyxy, det_labels [D] int64, det_scores [D] f32;
+ *   true_boxes [T,4] f32, true_labels [T] int64, true_difficulties [T] uint8 (0/1);
+ *   threshold: IoU threshold, compared against the float32 IoU promoted to double (:108);
+ *   recall_thresholds: device float[11] = torch.arange(0, 1.1, 0.1) (float32, :128).
+ * Output: ap [C-1] f32 (class 1..C-1; 0 for classes without detections) and mean_ap [1].
+ * Score ties between detections of one class keep input order (the reference's sort is not
+ * stable: tie order is unspecified there).  Workspace: sbod_map_workspace_bytes(D, T). */
+size_t sbod_map_workspace_bytes(int64_t n_det, int64_t n_true);
+int sbod_map_f32(const float *det_boxes, const int64_t *det_labels, const float *det_scores,
+                 const int32_t *det_offsets, const float *true_boxes, const int64_t *true_labels,
+                 const uint8_t *true_difficulties, const int32_t *true_offsets, int B, int C,
+                 int64_t n_det, int64_t n_true, double threshold, const float *recall_thresholds,
+                 float *ap, float *mean_ap, void *workspace, size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,8 @@ SIGNATURES = {
                               P, P, P, P, SZ, P]),
     'sbod_nms_workspace_bytes': (SZ, [I64]),
     'sbod_nms_f32': (I32, [P, P, I64, F32, I32, I32, F32, P, P, P, SZ, P]),
+    'sbod_map_workspace_bytes': (SZ, [I64, I64]),
+    'sbod_map_f32': (I32, [P, P, P, P, P, P, P, P, I32, I32, I64, I64, ctypes.c_double, P, P, P, P, SZ, P]),
     'sbod_timing_enable': (I32, [ctypes.c_char_p]),
     'sbod_timing_query': (I32, [ctypes.c_char_p, P, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),

@@ -3,12 +3,16 @@
 ``find_jaccard_overlap`` (metrics.py:208-252) is the IoU every criterion and the mAP use:
 inner / (gt_area + anchor_area - inner + 1e-5), GT with |w|,|h| < 1e-5 -> 0, anchors with
 w,h < 1e-5 -> -1 (applied last).  Bit-exact with the reference's CPU path.
-``calculate_mAP`` (VOC 11-point AP bookkeeping) is outside the hot path.
+``calculate_mAP`` (metrics.py:8-145): VOC 11-point mAP on the device —
+sorts, per-(class, image) greedy TP/FP assignment and per-class AP kernels (csrc/map.hip),
+one host sync for the returned Python values, like the reference's ``.item()``/``.tolist()``.
 """
 import torch
 
 from . import _lib as L
 from . import core
+
+_RTHR = {}
 
 
 def _single(gt, anchors, mode, what):
@@ -31,3 +35,45 @@ def find_jaccard_overlap(gt_boxes, anchors):
 def intersect(box_a, box_b):
     """[A, B] intersection areas (metrics.py:192-205)."""
     return _single(box_a, box_b, L.IOU_INTER, 'intersect')
+
+
+def _offsets(lists, device):
+    offs = [0]
+    for t in lists:
+        offs.append(offs[-1] + int(t.shape[0]))
+    return torch.tensor(offs, dtype=torch.int32).to(device, non_blocking=True), offs[-1]
+
+
+def calculate_mAP(det_boxes, det_labels, det_scores, true_boxes, true_labels, true_difficulties, threshold,
+                  label_map, device='cuda:0'):
+    """metrics.py:8-145.  Lists of per-image tensors (ROCm device) -> (dict class name -> AP,
+    mAP).  Score ties within a class keep input order (see include/sbod.h)."""
+    assert len(det_boxes) == len(det_labels) == len(det_scores) == len(true_boxes) == len(
+        true_labels) == len(true_difficulties)
+    n_classes = len(label_map)
+    B = len(det_boxes)
+    dev = torch.device(device)
+    for group in (det_boxes, det_labels, det_scores, true_boxes, true_labels, true_difficulties):
+        L.require_device(*group, what='calculate_mAP')
+    db = torch.cat([b.reshape(-1, 4) for b in det_boxes]).to(dev, torch.float32).contiguous()
+    dl = torch.cat([l.reshape(-1) for l in det_labels]).to(dev, torch.int64).contiguous()
+    ds = torch.cat([s.reshape(-1) for s in det_scores]).to(dev, torch.float32).contiguous()
+    tb = torch.cat([b.reshape(-1, 4) for b in true_boxes]).to(dev, torch.float32).contiguous()
+    tl = torch.cat([l.reshape(-1) for l in true_labels]).to(dev, torch.int64).contiguous()
+    td = torch.cat([d.reshape(-1) for d in true_difficulties]).to(dev, torch.uint8).contiguous()
+    doff, D = _offsets(det_labels, dev)
+    toff, T = _offsets(true_labels, dev)
+    key = str(dev)
+    if key not in _RTHR:   # metrics.py:128, float32 arange exactly as the reference builds it
+        _RTHR[key] = torch.arange(start=0, end=1.1, step=.1).to(dev)
+    ap = torch.empty(n_classes - 1, dtype=torch.float32, device=dev)
+    mean = torch.empty(1, dtype=torch.float32, device=dev)
+    nb = L.lib().sbod_map_workspace_bytes(D, T)
+    ws = core.workspace(nb, dev, 'map')
+    L.call('sbod_map_f32', L.ptr(db), L.ptr(dl), L.ptr(ds), L.ptr(doff), L.ptr(tb), L.ptr(tl), L.ptr(td),
+           L.ptr(toff), B, n_classes, D, T, float(threshold), L.ptr(_RTHR[key]), L.ptr(ap), L.ptr(mean),
+           L.ptr(ws), nb, L.stream_of(db))
+    aps = ap.cpu().tolist()
+    mean_average_precision = float(mean.cpu().item())
+    rev_label_map = {v: k for k, v in label_map.items()}
+    return {rev_label_map[c + 1]: v for c, v in enumerate(aps)}, mean_average_precision

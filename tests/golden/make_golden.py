@@ -558,20 +558,83 @@ def gen_dcn(R):
     save('dcn.npz', d)
 
 
-def main():
+def synth_eval(B, n_classes, seed, n_fp=6, jitter=0.03):
+    """Eval-style lists: GT from synth.make_gt plus difficulties; detections = jittered GT copies
+    (some with a wrong label) and random false positives, tie-free scores in (0, 1)."""
+    g = torch.Generator().manual_seed(seed)
+    boxes, labels = synth.make_gt(B, seed=seed, n_classes=n_classes, max_objects=8)
+    diffs, db, dl, ds = [], [], [], []
+    for i in range(B):
+        G = boxes[i].shape[0]
+        diffs.append((torch.rand(G, generator=g) < 0.2).to(torch.uint8))
+        k = int(torch.randint(0, 2 * G + 1, (1,), generator=g))
+        src = torch.randint(0, G, (k,), generator=g)
+        jb = boxes[i][src] + (torch.rand(k, 4, generator=g) - 0.5) * 2 * jitter
+        jl = labels[i][src].clone()
+        flip = torch.rand(k, generator=g) < 0.15
+        jl[flip] = torch.randint(1, n_classes, (int(flip.sum()),), generator=g)
+        xy = torch.rand(n_fp, 2, generator=g) * 0.7
+        wh = 0.02 + torch.rand(n_fp, 2, generator=g) * 0.3
+        fb = torch.cat([xy, xy + wh], 1)
+        fl = torch.randint(1, n_classes, (n_fp,), generator=g)
+        bb = torch.cat([jb, fb]).clamp(0, 1)
+        ll = torch.cat([jl, fl])
+        sc = torch.rand(bb.shape[0], generator=g) * 0.98 + 0.01
+        db.append(bb.float())
+        dl.append(ll.long())
+        ds.append(sc.float())
+    return db, dl, ds, boxes, labels, diffs
+
+
+def gen_map(R):
+    """metrics.calculate_mAP (metrics.py:8-145) on eval-style synthetic lists, device='cpu'."""
+    d = {}
+    cases = [(6, 6, 0.5, 11), (10, 21, 0.5, 12), (10, 21, 0.7, 13), (8, 5, 0.3, 14), (40, 21, 0.5, 15)]
+    for k, (B, C, thr, seed) in enumerate(cases):
+        db, dl, ds, tb, tl, td = synth_eval(B, C, seed)
+        if k == 1:       # an image with no detections and class 3 without any detection
+            db[0], dl[0], ds[0] = torch.zeros(0, 4), torch.zeros(0, dtype=torch.long), torch.zeros(0)
+            for i in range(B):
+                keep = dl[i] != 3
+                db[i], dl[i], ds[i] = db[i][keep], dl[i][keep], ds[i][keep]
+        if k == 3:       # every object of class 2 difficult (n_easy = 0)
+            for i in range(B):
+                td[i][tl[i] == 2] = 1
+        label_map = {'background': 0}
+        label_map.update({'c%d' % c: c for c in range(1, C)})
+        aps, mean_ap = R.metrics.calculate_mAP(db, dl, ds, tb, tl, td, thr, label_map, device='cpu')
+        pre = 'c%d_' % k
+        d[pre + 'params'] = np.array([B, C, thr, seed], dtype=np.float64)
+        d[pre + 'ap'] = np.array([aps['c%d' % c] for c in range(1, C)], dtype=np.float32)
+        d[pre + 'map'] = np.float64(mean_ap)
+        for i in range(B):
+            d[pre + 'db%d' % i] = f32(db[i])
+            d[pre + 'dl%d' % i] = i64(dl[i])
+            d[pre + 'ds%d' % i] = f32(ds[i])
+            d[pre + 'tb%d' % i] = f32(tb[i])
+            d[pre + 'tl%d' % i] = i64(tl[i])
+            d[pre + 'td%d' % i] = td[i].numpy().astype(np.uint8)
+    d['n_cases'] = np.int64(len(cases))
+    save('map.npz', d)
+
+
+def main(only=None):
+    """Regenerate every fixture, or only the named generators (e.g. ``make_golden.py map``)."""
     torch.set_num_threads(8)
     R = load_reference()
-    priors = gen_priors(R)
-    gen_jaccard(R, priors)
-    gen_match(R, priors)
-    gen_iou_utils_match(R, priors)
-    gen_codecs(R, priors)
-    gen_losses(R)
-    gen_criteria(R, priors)
-    gen_nms(R)
-    gen_detect(R, priors)
-    gen_dcn(R)
+    gens = ['jaccard', 'match', 'iou_utils_match', 'codecs', 'losses', 'criteria', 'nms', 'detect',
+            'dcn', 'map']
+    todo = set(only or gens)
+    priors = gen_priors(R) if (only is None or todo - {'losses', 'nms', 'dcn', 'map'}) else None
+    for name in gens:
+        if name not in todo:
+            continue
+        fn = globals()['gen_' + name]
+        if name in ('losses', 'nms', 'dcn', 'map'):
+            fn(R)
+        else:
+            fn(R, priors)
 
 
 if __name__ == '__main__':
-    main()
+    main(sys.argv[1:] or None)

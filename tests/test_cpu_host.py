@@ -107,5 +107,7 @@ def test_no_kernel_spills_to_scratch():
         pytest.skip('library not built with resource remarks')
     usage = json.load(open(path))
     assert len(usage) >= 20
-    bad = {k: v['ScratchSize'] for k, v in usage.items() if v.get('ScratchSize', 0) > 0}
+    ours = {k: v for k, v in usage.items() if 'sbod' in k}     # library (rocPRIM) kernels excluded
+    assert len(ours) >= 20
+    bad = {k: v['ScratchSize'] for k, v in ours.items() if v.get('ScratchSize', 0) > 0}
     assert bad == {}, bad
