@@ -91,3 +91,32 @@ res['backward'] = round(tb / N * 1e6, 2)
 res['detect_api_incl_sync'] = host_time(lambda: MU.detect(locs.detach(), det, 0.01, 0.45, 200, pri, cfg))
 res['empty_x4'] = host_time(lambda: [torch.empty(32, P, dtype=torch.int32, device=dev) for _ in range(4)])
 print(json.dumps(res))
+
+
+# autograd floor: a Python Function whose backward just hands back a preallocated gradient
+class _Trivial(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.g = torch.empty_like(x)
+        return x.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, g):
+        r = ctx.g
+        ctx.g = None
+        return r
+
+
+xs = locs0.clone().requires_grad_(True)
+tt = 0.0
+for it in range(N + 10):
+    xs.grad = None
+    y = _Trivial.apply(xs)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    y.backward()
+    if it >= 10:
+        tt += time.perf_counter() - t
+    torch.cuda.synchronize()
+res2 = {'trivial_function_backward': round(tt / N * 1e6, 2)}
+print(json.dumps(res2))

@@ -567,24 +567,17 @@ struct SegOut {
 constexpr int kSegSortCap = 2048;  // segments up to this size are selected in LDS
 
 
-__global__ __launch_bounds__(kSegThreads) void k_det_segment(
-    const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
-    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
-    const int32_t *__restrict__ need) {
-  extern __shared__ unsigned char s_raw[];
-  __shared__ uint32_t s_hist[2048];
-  __shared__ unsigned long long s_st[2];
-  __shared__ unsigned long long s_flag[16];
-  __shared__ unsigned long long s_m[kSegThreads];
-  __shared__ int s_nk, s_cnt, s_misc[4];
-  const int c = blockIdx.x + 1, b = blockIdx.y;
+// Block-level segment work for (image b, class c): top-`window` candidates by key, greedy NMS,
+// kept keys in rank order.  Called by every thread of the block (it synchronises); used by
+// k_det_segment (one block per segment) and by k_det_merge's inline second pass.
+__device__ void segment_body(const unsigned long long *cand, const uint32_t *cand_count,
+                             const float *__restrict__ boxes_ws, int P, int C, int b, int c, int window,
+                             int stride, float thr, SegOut o, unsigned char *s_raw, uint32_t *s_hist,
+                             unsigned long long *s_st, unsigned long long *s_flag, unsigned long long *s_m,
+                             int *s_nk_p, int *s_cnt_p, int *s_misc) {
+  int &s_nk = *s_nk_p;
+  int &s_cnt = *s_cnt_p;
   const int64_t seg = static_cast<int64_t>(b) * C + c;
-#ifdef SBOD_PHASE_CLOCKS
-  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-  SEG_PHASE(0);
-  // second pass: only the truncated classes of images whose merge could not decide
-  if (need != nullptr && (need[b] == 0 || o.lastkey[seg] == 0ull)) return;
   const int n = static_cast<int>(cand_count[seg]);
   const unsigned long long *g = cand + seg * P;
   const int q = min(n, window);
@@ -603,9 +596,9 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
       o.kc[seg] = 0;
       o.lastkey[seg] = 0;
     }
+    __syncthreads();
     return;
   }
-  SEG_PHASE(1);
   if (n <= q) {  // whole segment fits the window
     const int N = next_pow2(max(n, 2));
     block_copy_keys(sk, g, n, N);
@@ -636,7 +629,6 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     __syncthreads();
     bitonic_desc(sk, N);
   }
-  SEG_PHASE(2);
   for (int i = threadIdx.x; i < q; i += blockDim.x) {
     const uint32_t p = key_low(sk[i]);
     const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
@@ -647,19 +639,30 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
   const int nk = q <= kMatrixMax
                      ? block_greedy_matrix<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, mat, &s_nk)
                      : block_greedy<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, s_flag, s_m, &s_nk);
-  SEG_PHASE(3);
   unsigned long long *ko = o.kept + seg * stride;
   for (int k = threadIdx.x; k < nk; k += blockDim.x) ko[k] = sk[kl[k]];
   if (threadIdx.x == 0) {
     o.kc[seg] = nk;
     o.lastkey[seg] = n > q ? sk[q - 1] : 0ull;
   }
-  SEG_PHASE(4);
-#ifdef SBOD_PHASE_CLOCKS
-  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 7) && (blockIdx.y == 0 || blockIdx.y == 5))
-    printf("seg w%d b%d c%d n=%d nk=%d: load %lld select %lld nms %lld store %lld total %lld\n", window, b, c, n,
-           nk, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[4] - ph[0]);
-#endif
+  __syncthreads();   // LDS is reused by the caller right after
+}
+
+__global__ __launch_bounds__(kSegThreads) void k_det_segment(
+    const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
+    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
+    const int32_t *__restrict__ need) {
+  extern __shared__ unsigned char s_raw[];
+  __shared__ uint32_t s_hist[2048];
+  __shared__ unsigned long long s_st[2];
+  __shared__ unsigned long long s_flag[16];
+  __shared__ unsigned long long s_m[kSegThreads];
+  __shared__ int s_nk, s_cnt, s_misc[4];
+  const int c = blockIdx.x + 1, b = blockIdx.y;
+  // second pass: only the truncated classes of images whose merge could not decide
+  if (need != nullptr && (need[b] == 0 || o.lastkey[static_cast<int64_t>(b) * C + c] == 0ull)) return;
+  segment_body(cand, cand_count, boxes_ws, P, C, b, c, window, stride, thr, o, s_raw, s_hist, s_st, s_flag,
+               s_m, &s_nk, &s_cnt, s_misc);
 }
 
 // ----------------------------------------------------------------------------- K2 (wave form)
@@ -903,9 +906,9 @@ __device__ __forceinline__ int count_before(const float *a, int n, float s, bool
 
 // pass: 0 = single pass (invalid -> count -1), 1 = first of two (invalid -> need[b] = 1),
 // 2 = second (only images with need[b]; invalid -> count -1).
-__global__ __launch_bounds__(kMergeThreads) void k_det_merge(
-    const unsigned long long *__restrict__ kept, const uint32_t *__restrict__ kc,
-    const unsigned long long *__restrict__ lastkey, const float *__restrict__ boxes_ws, int P,
+__device__ __forceinline__ int merge_body(
+    const unsigned long long *kept, const uint32_t *kc,
+    const unsigned long long *lastkey, const float *__restrict__ boxes_ws, int P,
     int C, int window, int top_k, float final_nms, int general, int pass,
     int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
@@ -924,7 +927,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
   __shared__ float s_lk[256];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int64_t sb0 = static_cast<int64_t>(b) * C;
-  if (pass == 2 && need[b] == 0) return;
+  if (pass == 2 && need[b] == 0) return 0;
 #ifdef SBOD_PHASE_CLOCKS
   long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -987,13 +990,14 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
   if (total == 0) {  // models/utils.py:274-277 placeholder
     if (any_trunc) {
       undecided();
+      return 1;
     } else if (tid == 0) {
       st4(ob, Box4{0.f, 0.f, 1.f, 1.f});
       ol[0] = 0;
       os[0] = 0.f;
       out_count[b] = 1;
     }
-    return;
+    return 0;
   }
   if (final_nms < 0.f && !any_trunc && total <= top_k) {  // all kept, in class order
     for (int r = tid; r < total; r += blockDim.x) {
@@ -1001,11 +1005,11 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
       emit(r, c, ck_of(c, r - s_off[c]));
     }
     if (tid == 0) out_count[b] = total;
-    return;
+    return 0;
   }
   if (final_nms < 0.f && total <= top_k) {  // a truncated window hides how many more exist
     undecided();
-    return;
+    return 1;
   }
   // R = how many leading entries of the merged order are needed
   const int R = final_nms < 0.f ? top_k : min(total, general ? kMergeStage : kFastStage);
@@ -1051,7 +1055,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     }
     if (m > kFastOut) {  // pathological ties: re-run on the general path
       if (tid == 0) out_count[b] = -1;
-      return;
+      return 0;
     }
     SEG_PHASE(3);
     for (int r = tid; r < R; r += blockDim.x) ord[r] = static_cast<int>(0xffffffffu - static_cast<uint32_t>(top[r]));
@@ -1099,7 +1103,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     int c;
     if (any_trunc && !(key_score(entry(top_k - 1, c)) > trunc_score)) {
       undecided();
-      return;
+      return 1;
     }
     SEG_PHASE(4);
     for (int r = tid; r < top_k; r += blockDim.x) {
@@ -1113,7 +1117,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
       printf("merge p%d b%d nz=%d: prologue %lld gather %lld select+sort %lld ord+check %lld emit %lld total %lld\n",
              pass, b, total, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[5] - ph[4], ph[5] - ph[0]);
 #endif
-    return;
+    return 0;
   }
   // detect_tools: class-agnostic greedy NMS at final_nms over the merged order, first top_k
   Box4 *bx = reinterpret_cast<Box4 *>(ord + kMergeStage);
@@ -1140,7 +1144,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
   const bool ok = enough && (!any_trunc || key_score(entry(kl[top_k - 1], c0)) > trunc_score);
   if (!ok) {
     undecided();
-    return;
+    return 1;
   }
   for (int r = tid; r < nout; r += blockDim.x) {
     int c;
@@ -1148,6 +1152,54 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     emit(r, c, ck);
   }
   if (tid == 0) out_count[b] = nout;
+  return 0;
+}
+
+__host__ __device__ inline size_t seg_lds(int window) {
+  size_t wn = 2;
+  while (wn < static_cast<size_t>(window)) wn <<= 1;
+  const size_t mat = window <= kMatrixMax ? static_cast<size_t>(window) * ((window + 63) / 64) * 8 : 0;
+  return static_cast<size_t>(kSegSortCap) * 8 + wn * 8 + static_cast<size_t>(window) * (16 + 4 + 4 + 1) + 16 + mat;
+}
+
+// Inline second pass scratch, after the segment layout in the merge's dynamic LDS:
+// hist [2048] u32 | m [kMergeThreads] u64 | st [2] u64 | flag [16] u64 | nk, cnt, misc[4], tr[256] int
+__host__ __device__ inline size_t inline2_lds(int window) {
+  return ((seg_lds(window) + 15) & ~static_cast<size_t>(15)) + 2048 * 4 + (kMergeThreads + 2 + 16) * 8 + (6 + 256) * 4;
+}
+
+// Per-image merge.  pass 0: single pass; pass 1 (two-pass mode): an undecidable image runs the
+// second pass inline — its truncated classes are re-selected with window w2 by segment_body in
+// this block, then the merge is repeated (pass 2) — so no extra launches when (as usual) no
+// image needs it.
+__global__ __launch_bounds__(kMergeThreads) void k_det_merge(
+    const unsigned long long *kept, const uint32_t *kc, const unsigned long long *lastkey,
+    const float *__restrict__ boxes_ws, int P, int C, int window, int top_k, float final_nms, int general,
+    int pass, int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
+    float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
+    int32_t *__restrict__ out_count, const unsigned long long *cand, const uint32_t *cand_count, float thr,
+    SegOut so) {
+  extern __shared__ unsigned char s_raw[];
+  const int st = merge_body(kept, kc, lastkey, boxes_ws, P, C, window, top_k, final_nms, general, pass, need,
+                            scratch, out_boxes, out_labels, out_scores, out_count);
+  if (st == 0 || pass != 1) return;
+  const int b = blockIdx.x;
+  uint32_t *h2 = reinterpret_cast<uint32_t *>(s_raw + ((seg_lds(window) + 15) & ~static_cast<size_t>(15)));
+  unsigned long long *m2 = reinterpret_cast<unsigned long long *>(h2 + 2048);
+  unsigned long long *st2 = m2 + kMergeThreads, *fl2 = st2 + 2;
+  int *iv = reinterpret_cast<int *>(fl2 + 16);   // nk, cnt, misc[4], tr[256]
+  int *s_tr = iv + 6;
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x)   // classes truncated by the first window
+    s_tr[c] = c > 0 && __builtin_nontemporal_load(lastkey + static_cast<int64_t>(b) * C + c) != 0ull;
+  __syncthreads();
+  for (int c = 1; c < C; ++c)
+    if (s_tr[c])
+      segment_body(cand, cand_count, boxes_ws, P, C, b, c, window, window, thr, so, s_raw, h2, st2, fl2, m2,
+                   iv, iv + 1, iv + 2);
+  __syncthreads();
+  merge_body(kept, kc, lastkey, boxes_ws, P, C, window, top_k, final_nms, general, 2, need, scratch, out_boxes,
+             out_labels, out_scores, out_count);
 }
 
 // ----------------------------------------------------------------------------- single segment
@@ -1198,11 +1250,6 @@ __global__ __launch_bounds__(1024) void k_nms_single(const float *__restrict__ b
   if (threadIdx.x == 0) *count = nk;
 }
 
-size_t seg_lds(int window) {
-  const size_t wn = next_pow2_host(window < 2 ? 2 : window);
-  const size_t mat = window <= kMatrixMax ? static_cast<size_t>(window) * ((window + 63) / 64) * 8 : 0;
-  return static_cast<size_t>(kSegSortCap) * 8 + wn * 8 + static_cast<size_t>(window) * (16 + 4 + 4 + 1) + 16 + mat;
-}
 
 size_t single_lds(int q) {
   return static_cast<size_t>(next_pow2_host(q < 2 ? 2 : q)) * 8 + static_cast<size_t>(q) * (16 + 4 + 4 + 1) + 64;
@@ -1312,27 +1359,16 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   }
   SBOD_LAUNCHED("k_det_segment");
   {
+    // two-pass mode: the second pass runs inline in the merge blocks of undecidable images,
+    // so the merge's dynamic LDS also covers one segment with window w2
+    const size_t seg2 = two ? inline2_lds(w2) : 0;
     KernelTimer kt("k_det_merge", s);
-    hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
-                       ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
-                       ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count);
+    hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, ws.kept,
+                       ws.kc, ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
+                       ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, ws.cand, ws.count,
+                       max_overlap, so);
   }
   SBOD_LAUNCHED("k_det_merge");
-  if (two) {
-    {
-      KernelTimer kt("k_det_segment", s);
-      hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w2), s, ws.cand,
-                         ws.count, ws.boxes, P, C, w2, w2, max_overlap, so, ws.need);
-    }
-    SBOD_LAUNCHED("k_det_segment(pass 2)");
-    {
-      KernelTimer kt("k_det_merge", s);
-      hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds, s, ws.kept, ws.kc,
-                         ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, general, 2, ws.need,
-                         ws.scratch, det_boxes, det_labels, det_scores, det_count);
-    }
-    SBOD_LAUNCHED("k_det_merge(pass 2)");
-  }
   return SBOD_OK;
 }
 
