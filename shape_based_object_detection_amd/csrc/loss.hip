@@ -18,6 +18,8 @@
 
 namespace sbod {
 
+SBOD_STAMP_DECL
+
 constexpr int kLTile = 256;
 constexpr float kHalfBetaDefault = 0.5f / 9.f;
 
@@ -258,6 +260,7 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
                                                      T *__restrict__ glocs, T *__restrict__ gsc) {
   extern __shared__ float s_sc[];
   __shared__ float s_red[16];
+  STAMP_BEGIN();
   const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x;
   const int P = a.P, C = a.C;
   const int np = min(kLTile, P - p0);
@@ -384,6 +387,7 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
     a.partials[2 * blk] = conf_l;
     a.partials[2 * blk + 1] = loc_l;
   }
+  STAMP_END(4, 1);
 }
 
 // ----------------------------------------------------------------------------- hard negatives
@@ -770,3 +774,5 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
 }
 
 }  // extern "C"
+
+SBOD_STAMP_EXPORT(loss)

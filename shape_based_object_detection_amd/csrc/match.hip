@@ -12,6 +12,8 @@
 
 namespace sbod {
 
+SBOD_STAMP_DECL
+
 constexpr int kTile = 256;
 
 struct GtTile {
@@ -85,6 +87,7 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
     int B) {
   extern __shared__ GtTile s_gt[];
   __shared__ unsigned long long s_key[kTile / 64][kMaxGLds];
+  STAMP_BEGIN();
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) npos[B] = 0;  // phase 2 accumulates
   __shared__ int32_t s_lab[kMaxGLds];
   __shared__ int s_red[16];
@@ -141,6 +144,7 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
     }
   }
   if (threadIdx.x == 0) tcount[b * ntile + blockIdx.x] = pos;
+  STAMP_END(5, 1);
 }
 
 // Phase 2 (one wave per image): finish the per-object argmax over the tiles, then the forced
@@ -546,3 +550,5 @@ int sbod_match_ssd_f32(const float *truths, const int64_t *labels, int G,
 }
 
 }  // extern "C"
+
+SBOD_STAMP_EXPORT(match)

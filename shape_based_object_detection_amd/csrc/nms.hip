@@ -21,6 +21,8 @@
 
 namespace sbod {
 
+SBOD_STAMP_DECL
+
 constexpr int kDTile = 256;
 constexpr int kPrepRegC = 32;    // prepare: class rows up to this width are processed in registers
 constexpr int kSegThreads = 256;
@@ -414,11 +416,41 @@ struct DetArgs {
   float *dbg_probs, *dbg_boxes;
 };
 
+// exp(x) and the logistic function on the hardware exp2 / rcp units (~1-2 ulp; the detect path's
+// activations are its own — parity is pinned on the activations it produces).
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + fast_exp(-x)); }
+
+// Candidate slots of one workgroup: the per-(wave, class) ballots in LDS become ONE returning
+// atomic per (workgroup, class) on the segment's counter, all classes' atomics in flight
+// together; s_wb(w, c) = the slot base of wave w's class-c candidates.  Order inside a segment
+// is irrelevant (keys are unique and sorted later).  Synchronises the block.
+__device__ __forceinline__ void prep_slots(const DetArgs &a, int b, int C, int tid,
+                                           const unsigned long long *s_balf, uint32_t *s_wbf) {
+  __syncthreads();
+  for (int c = tid + 1; c < C; c += kDTile) {
+    uint32_t nwv[kDTile / 64], n = 0;
+#pragma unroll
+    for (int w = 0; w < kDTile / 64; ++w) {
+      nwv[w] = __popcll(s_balf[w * C + c]);
+      n += nwv[w];
+    }
+    uint32_t base = n ? atomicAdd(a.cand_count + b * C + c, n) : 0u;
+#pragma unroll
+    for (int w = 0; w < kDTile / 64; ++w) {
+      s_wbf[w * C + c] = base;
+      base += nwv[w];
+    }
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__restrict__ locs,
                                                         const float *__restrict__ scores) {
   // dynamic LDS: score tile [kDTile][C] f32 | ballots [kDTile/64][C] u64 | slot bases [C] u32,
   // sized to C so 6+ workgroups fit per CU (one round for B x ceil(P/256) workgroups at B=32)
   extern __shared__ float s_sc[];
+  STAMP_BEGIN();
   const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
   const int P = a.P, C = a.C;
   unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_sc + kDTile * C);
@@ -452,90 +484,83 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     if (a.box_type == SBOD_BOX_CORNER) st4(locs + 4 * i, d);  // models/utils.py:224 clamp_ in place
     st4(a.boxes_ws + 4 * i, d);
     if (a.dbg_boxes) st4(a.dbg_boxes + 4 * i, d);
-    if (C <= kPrepRegC) {
-      // the row in registers (unconditional, fully unrolled loads): one LDS round trip, not 3C
-      float r[kPrepRegC];
-#pragma unroll
-      for (int k = 0; k < kPrepRegC; ++k) r[k] = row[min(k, C - 1)];
+    if (C > kPrepRegC) {
       if (a.act == SBOD_ACT_SOFTMAX) {
-        float m = r[0];
-#pragma unroll
-        for (int k = 1; k < kPrepRegC; ++k) m = k < C ? fmaxf(m, r[k]) : m;
-        float sum = 0.f;
-#pragma unroll
-        for (int k = 0; k < kPrepRegC; ++k) {
-          r[k] = expf(r[k] - m);
-          sum = k < C ? sum + r[k] : sum;
+        float m = row[0];
+        for (int k = 1; k < C; ++k) m = fmaxf(m, row[k]);
+        float s = 0.f;
+        for (int k = 0; k < C; ++k) {
+          const float e = fast_exp(row[k] - m);
+          row[k] = e;
+          s += e;
         }
-#pragma unroll
-        for (int k = 0; k < kPrepRegC; ++k)
-          if (k < C) row[k] = r[k] / sum;
+        const float rs = __builtin_amdgcn_rcpf(s);
+        for (int k = 0; k < C; ++k) row[k] = row[k] * rs;
       } else {
-#pragma unroll
-        for (int k = 0; k < kPrepRegC; ++k)
-          if (k < C) row[k] = 1.f / (1.f + expf(-r[k]));
+        for (int k = 0; k < C; ++k) row[k] = fast_sigmoid(row[k]);
       }
-    } else if (a.act == SBOD_ACT_SOFTMAX) {
-      float m = row[0];
-      for (int k = 1; k < C; ++k) m = fmaxf(m, row[k]);
-      float s = 0.f;
-      for (int k = 0; k < C; ++k) {
-        const float e = expf(row[k] - m);
-        row[k] = e;
-        s += e;
-      }
-      for (int k = 0; k < C; ++k) row[k] = row[k] / s;
-    } else {
-      for (int k = 0; k < C; ++k) row[k] = 1.f / (1.f + expf(-row[k]));
     }
   }
-  // candidate compaction: ballots per (wave, class) -> ONE atomic per (workgroup, class), all
-  // classes' atomics in flight together -> slots (order inside a segment is irrelevant: keys
-  // are unique and sorted later)
-  SEG_PHASE(2);
   const bool allowed = valid && (a.pos == nullptr || a.pos[i] != 0);
   const int wv = tid >> 6;
-  for (int c = 1; c < C; ++c) {
-    const bool take = allowed && row[c] > a.min_score;
-    const unsigned long long bal = __ballot(take);
-    if (lane == 0) s_bal(wv, c) = bal;
-  }
-  __syncthreads();
-  for (int c = tid + 1; c < C; c += kDTile) {
-    uint32_t nwv[kDTile / 64], n = 0;
-#pragma unroll
-    for (int w = 0; w < kDTile / 64; ++w) {
-      nwv[w] = __popcll(s_bal(w, c));
-      n += nwv[w];
-    }
-    uint32_t base = n ? atomicAdd(a.cand_count + b * C + c, n) : 0u;
-#pragma unroll
-    for (int w = 0; w < kDTile / 64; ++w) {
-      s_wb(w, c) = base;
-      base += nwv[w];
-    }
-  }
-  __syncthreads();
-  SEG_PHASE(3);
   const unsigned long long lt = (1ull << lane) - 1ull;
-  if (C <= 64) {
-    // lane c holds class c's ballot and slot base for this wave; the class loop reads them
-    // with readlane (no LDS round trips inside the loop)
-    const unsigned long long mybal = lane < C ? s_bal(wv, lane) : 0ull;
-    const uint32_t mywb = lane < C ? s_wb(wv, lane) : 0u;
-    const uint32_t blo = static_cast<uint32_t>(mybal), bhi = static_cast<uint32_t>(mybal >> 32);
-    for (int c = 1; c < C; ++c) {
-      // readlane returns int: go through uint32_t so the low word is not sign-extended
-      const uint32_t rl = static_cast<uint32_t>(__builtin_amdgcn_readlane(blo, c));
-      const uint32_t rh = static_cast<uint32_t>(__builtin_amdgcn_readlane(bhi, c));
-      const unsigned long long bal = (static_cast<unsigned long long>(rh) << 32) | rl;
-      if (bal == 0ull) continue;
-      const uint32_t wb = __builtin_amdgcn_readlane(mywb, c);
-      if ((bal >> lane) & 1ull)
-        a.cand[(static_cast<int64_t>(b) * C + c) * P + wb + __popcll(bal & lt)] =
-            make_key(row[c], static_cast<uint32_t>(p));
+  if (C <= kPrepRegC) {
+    // ---- narrow rows (VOC: C = 21): the row, its activation and the candidate tests stay in
+    // registers.  Activation: exp2 / rcp hardware ops (probabilities within ~1e-6 relative of
+    // torch.softmax; every later decision reads these same values, so detect stays exact w.r.t.
+    // them).  Each lane then walks only ITS candidate classes (~1-2 of 20) to emit keys.
+    float r[kPrepRegC];
+#pragma unroll
+    for (int k = 0; k < kPrepRegC; ++k) r[k] = row[min(k, C - 1)];
+    if (a.act == SBOD_ACT_SOFTMAX) {
+      float m = r[0];
+#pragma unroll
+      for (int k = 1; k < kPrepRegC; ++k) m = k < C ? fmaxf(m, r[k]) : m;
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < kPrepRegC; ++k) {
+        r[k] = fast_exp(r[k] - m);
+        sum = k < C ? sum + r[k] : sum;
+      }
+      const float rs = __builtin_amdgcn_rcpf(sum);
+#pragma unroll
+      for (int k = 0; k < kPrepRegC; ++k) r[k] = r[k] * rs;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPrepRegC; ++k) r[k] = fast_sigmoid(r[k]);
+    }
+    uint32_t cmask = 0;
+#pragma unroll
+    for (int k = 0; k < kPrepRegC; ++k) {
+      if (k < C) {
+        row[k] = r[k];                         // for the emission loop and the debug copy
+        if (k >= 1) {
+          const bool take = allowed && r[k] > a.min_score;
+          const unsigned long long bal = __ballot(take);
+          if (lane == 0) s_bal(wv, k) = bal;
+          cmask |= take ? (1u << k) : 0u;
+        }
+      }
+    }
+    SEG_PHASE(2);
+    prep_slots(a, b, C, tid, s_balf, s_wbf);
+    SEG_PHASE(3);
+    while (cmask) {
+      const int c = __builtin_ctz(cmask);
+      cmask &= cmask - 1u;
+      const unsigned long long bal = s_bal(wv, c);
+      a.cand[(static_cast<int64_t>(b) * C + c) * P + s_wb(wv, c) + __popcll(bal & lt)] =
+          make_key(row[c], static_cast<uint32_t>(p));
     }
   } else {
+    SEG_PHASE(2);
+    for (int c = 1; c < C; ++c) {
+      const bool take = allowed && row[c] > a.min_score;
+      const unsigned long long bal = __ballot(take);
+      if (lane == 0) s_bal(wv, c) = bal;
+    }
+    prep_slots(a, b, C, tid, s_balf, s_wbf);
+    SEG_PHASE(3);
     for (int c = 1; c < C; ++c) {
       const unsigned long long bal = s_bal(wv, c);
       if (!((bal >> lane) & 1ull)) continue;
@@ -553,6 +578,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     __syncthreads();
     for (int k = tid; k < np * C; k += kDTile) a.dbg_probs[rbase * C + k] = s_sc[k];
   }
+  STAMP_END(1, 1);
 }
 #undef s_bal
 #undef s_wb
@@ -885,11 +911,292 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
 #endif
 }
 
+// ----------------------------------------------------------------------------- K2 (4-wave form)
+// Pass-1 segments (window <= 64) on one 256-thread workgroup each: the same select / sort /
+// greedy as k_det_segment_wave, with the per-lane work split over four waves —
+//   select: ~n/256 keys per lane (registers), one shared 256-bin LDS histogram per 8-bit digit,
+//           the digit scan by wave 0;
+//   sort:   wave 0 bitonic-sorts the q <= 64 selected keys over its lanes (shuffles);
+//   NMS:    the q x q suppression bit matrix is built with every wave taking q/4 rows (the row
+//           box is an LDS broadcast, a ballot assembles each row), then wave 0 sweeps the rows
+//           in rank order from registers (row i in lane i, readlane).
+// Same keys, same rank order, same suppression test: results identical to k_det_segment_wave.
+constexpr int kSegW = 4;                       // waves per segment
+constexpr int kSegWRegKeys = 2048;             // keys held in registers (8 per lane)
+
+__global__ __launch_bounds__(64 * kSegW) void k_det_segment_w4(
+    const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
+    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
+  constexpr int NT = 64 * kSegW, KR = kSegWRegKeys / NT;
+  STAMP_BEGIN();
+  __shared__ uint32_t s_hist[256];
+  __shared__ unsigned long long s_sel[64];
+  __shared__ Box4 s_bxu[64], s_bx[64];
+  __shared__ float s_ar[64];
+  __shared__ unsigned long long s_rows[64];
+  __shared__ int s_misc[4];
+  __shared__ unsigned long long s_red[2 * kSegW];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int c = blockIdx.x + 1, b = blockIdx.y;
+  const int64_t seg = static_cast<int64_t>(b) * C + c;
+  const int n = static_cast<int>(cand_count[seg]);
+  if (n == 0) {
+    if (tid == 0) {
+      o.kc[seg] = 0;
+      o.lastkey[seg] = 0;
+    }
+    return;
+  }
+  const unsigned long long *g = cand + seg * P;
+  const int q = min(n, window);
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  SEG_PHASE(0);
+  const bool regs = n <= kSegWRegKeys;
+  unsigned long long kr[KR];
+  if (regs) {
+#pragma unroll
+    for (int t = 0; t < KR; ++t) {
+      const int i = tid + NT * t;
+      const unsigned long long v = g[min(i, n - 1)];
+      kr[t] = i < n ? v : 0ull;   // real keys are never 0 (score > 0)
+    }
+  }
+  // ---- common high bits of all keys (OR vs AND): the radix digits start at the highest bit
+  // where keys differ (scores in (0.01, 1] share their top ~6 bits, so a fixed top digit wastes
+  // a level and piles every key onto a few contended histogram bins)
+  unsigned long long vor = 0ull, vand = ~0ull;
+  if (regs) {
+#pragma unroll
+    for (int t = 0; t < KR; ++t)
+      if (kr[t] != 0ull) {
+        vor |= kr[t];
+        vand &= kr[t];
+      }
+  } else {
+    for (int i = tid; i < n; i += NT) {
+      const unsigned long long k = g[i];
+      vor |= k;
+      vand &= k;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    vor |= shfl_xor_u64(vor, m);
+    vand &= shfl_xor_u64(vand, m);
+  }
+  if (lane == 0) {
+    s_red[wv] = vor;
+    s_red[kSegW + wv] = vand;
+  }
+  if (tid == 0) s_misc[3] = 0;
+  __syncthreads();
+  SEG_PHASE(1);
+  // ---- select: keys with (key >> sh) >= (prefix >> sh) are exactly the top q
+  unsigned long long prefix = 0;
+  int sh = 64;
+  if (n > q) {
+    unsigned long long all_or = 0ull, all_and = ~0ull;
+#pragma unroll
+    for (int w = 0; w < kSegW; ++w) {
+      all_or |= s_red[w];
+      all_and &= s_red[kSegW + w];
+    }
+    const int top = 63 - __clzll(static_cast<long long>(all_or ^ all_and));   // keys unique, n > 1
+    prefix = top >= 63 ? 0ull : (all_and & ~((2ull << top) - 1ull));          // the shared bits
+    int kk = q;
+    for (int hb = top; hb >= 0;) {
+      const int lo = hb >= 7 ? hb - 7 : 0, width = hb - lo + 1;
+      const unsigned long long dmask = (1ull << width) - 1ull;
+      s_hist[tid] = 0u;
+      __syncthreads();
+      auto count = [&](unsigned long long k) {
+        if (k != 0ull && (hb >= 63 || ((k ^ prefix) >> (hb + 1)) == 0ull))
+          atomicAdd(&s_hist[(k >> lo) & dmask], 1u);
+      };
+      if (regs) {
+#pragma unroll
+        for (int t = 0; t < KR; ++t)
+          if (NT * t < n) count(kr[t]);
+      } else {
+        for (int i = tid; i < n; i += NT) count(g[i]);
+      }
+      __syncthreads();
+      if (wv == 0) {
+        // lane owns bins 255 - 4 lane - (0..3), top first (bins >= 2^width stay 0)
+        uint32_t hv[4], mine = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hv[j] = s_hist[255 - 4 * lane - j];
+          mine += hv[j];
+        }
+        uint32_t incl = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t v = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += v;
+        }
+        const uint32_t excl = incl - mine;
+        if (excl < static_cast<uint32_t>(kk) && incl >= static_cast<uint32_t>(kk)) {
+          uint32_t acc = excl;
+          bool done = false;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (!done) {
+              if (acc + hv[j] >= static_cast<uint32_t>(kk)) {
+                s_misc[0] = 255 - 4 * lane - j;
+                s_misc[1] = kk - static_cast<int>(acc);
+                s_misc[2] = static_cast<int>(hv[j]);
+                done = true;
+              } else {
+                acc += hv[j];
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+      const int bin = s_misc[0], left = s_misc[1], hbin = s_misc[2];
+      prefix |= static_cast<unsigned long long>(bin) << lo;
+      sh = lo;
+      kk = left;
+      if (hbin == left) break;   // the whole bin is selected: no finer digit needed
+      hb = lo - 1;
+    }
+  }
+  // ---- compact the selected keys (exactly q) into s_sel (any order: sorted next)
+  {
+    auto take = [&](unsigned long long k) {
+      const bool sel = k != 0ull && (sh >= 64 || (k >> sh) >= (prefix >> sh));
+      const unsigned long long bal = __ballot(sel);
+      if (bal == 0ull) return;
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&s_misc[3], __popcll(bal));
+      base = __shfl(base, 0, 64);
+      if (sel) s_sel[base + __popcll(bal & ((1ull << lane) - 1ull))] = k;
+    };
+    if (regs) {
+#pragma unroll
+      for (int t = 0; t < KR; ++t)
+        if (NT * t < n) take(kr[t]);
+    } else {
+      for (int i0 = 0; i0 < n; i0 += NT) take(tid + i0 < n ? g[tid + i0] : 0ull);
+    }
+  }
+  __syncthreads();
+  SEG_PHASE(2);
+  // ---- wave 0: sort descending over lanes; boxes fetched before the sort (latency overlap),
+  // each key carries its original lane to find its box afterwards
+  unsigned long long v = 0ull;
+  if (wv == 0) {
+    v = lane < q ? s_sel[lane] : 0ull;
+    Box4 bu{0.f, 0.f, 0.f, 0.f};
+    if (lane < q) bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(v)));
+    int pos = lane;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const unsigned long long w = shfl_xor_u64(v, j);
+        const int wp = __shfl_xor(pos, j, 64);
+        const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
+        const bool tk = keep_max ? (w > v) : (w < v);
+        v = tk ? w : v;
+        pos = tk ? wp : pos;
+      }
+    }
+    s_bxu[lane] = bu;
+    wave_lds_sync();
+    const Box4 bs = s_bxu[pos];
+    s_bx[lane] = bs;
+    s_ar[lane] = (bs.c - bs.a) * (bs.d - bs.b);
+  }
+  __syncthreads();
+  SEG_PHASE(3);
+  // ---- suppression columns: col_i = the higher-ranked boxes j < i that would suppress box i
+  // (the torchvision test is symmetric in the pair).  Wave w builds columns w, w + 4, ...,
+  // four at a time (independent LDS broadcasts and ballots in flight).
+  {
+    const Box4 bj = lane < q ? s_bx[lane] : Box4{0.f, 0.f, 0.f, 0.f};
+    const float aj = lane < q ? s_ar[lane] : 0.f;
+    constexpr int kU = 4;
+    for (int i0 = wv; i0 < q; i0 += kSegW * kU) {
+      Box4 bi[kU];
+      float ai[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = min(i0 + kSegW * u, 63);
+        bi[u] = s_bx[i];
+        ai[u] = s_ar[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + kSegW * u;
+        const bool act = lane < i && i < q;
+        bool amb;
+        float inter, un;
+        const bool sup = tv_fast(bi[u], ai[u], bj, aj, thr, amb, inter, un);
+        unsigned long long col = __ballot(act && sup);
+        const unsigned long long am = __ballot(act && amb);
+        if (am != 0ull) {   // rare: exact division for the lanes within the margin
+          const bool ex = act && amb && (inter / un > thr);
+          col = (col & ~am) | __ballot(ex);
+        }
+        if (lane == 0 && i < q) s_rows[i] = col;
+      }
+    }
+  }
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph_rows = clock64();
+#endif
+  __syncthreads();
+  if (wv != 0) return;
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph_sync = clock64();
+#endif
+  // ---- wave 0: the greedy result as a parallel fixpoint (column i in lane i).  Box i is kept
+  // once every possible suppressor above it is known suppressed, and suppressed once a kept box
+  // above it suppresses it; each round decides at least the first undecided box, so this is
+  // exactly the sequential greedy order, in as many rounds as the longest suppression chain.
+  const unsigned long long mycol = lane < q ? s_rows[lane] : 0ull;
+  const unsigned long long valid = q == 64 ? ~0ull : ((1ull << q) - 1ull);
+  unsigned long long kept = 0, supp = 0;
+  for (int round = 0; round < 64; ++round) {
+    const unsigned long long und = valid & ~(kept | supp);
+    if (und == 0ull) break;
+    const bool mine = (und >> lane) & 1ull;
+    kept |= __ballot(mine && (mycol & ~supp) == 0ull);
+    supp |= __ballot(mine && (mycol & kept) != 0ull);
+  }
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph_sweep = clock64();
+#endif
+  unsigned long long *ko = o.kept + seg * stride;
+  if ((kept >> lane) & 1ull) ko[__popcll(kept & ((1ull << lane) - 1ull))] = v;
+  const uint32_t llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), q - 1);
+  const uint32_t lhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), q - 1);
+  if (lane == 0) {
+    o.kc[seg] = __popcll(kept);
+    o.lastkey[seg] = n > q ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
+  }
+  STAMP_END(2, 0);
+#ifdef SBOD_PHASE_CLOCKS
+  if (lane == 0) ph[4] = clock64();
+  if (lane == 0 && (c == 1 || c == 8) && (b == 0 || b == 5))
+    printf("seg4 b%d c%d n=%d: load %lld select+compact %lld sort+boxes %lld rows %lld sync %lld sweep %lld store %lld total %lld\n",
+           b, c, n, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph_rows - ph[3], ph_sync - ph_rows, ph_sweep - ph_sync,
+           ph[4] - ph_sweep, ph[4] - ph[0]);
+#endif
+}
+
 // ----------------------------------------------------------------------------- K3
 constexpr int kMergeLdsKeys = 8192;   // general path: merged keys sorted in LDS (radix-select first)
 constexpr int kRankScores = 8192;     // fast path: staged class-prefix merged keys
 constexpr int kFastOut = 1024;        // fast path: selected top-R (+ ties) keys
 constexpr int kFastStage = 512;       // fast path: merged prefix ordered for the final NMS
+constexpr int kRankC = 64;            // rank path: classes (incl. background) handled by wave-0 lanes
+constexpr int kRankLds = (kRankScores + kFastOut) * 8;   // rank path: dynamic LDS it may use
 
 // Count of entries of a non-increasing score list that precede score s in the merged order:
 // scores > s, plus scores == s when the list's class is lower (the concatenation is in class order).
@@ -904,12 +1211,204 @@ __device__ __forceinline__ int count_before(const float *a, int n, float s, bool
   return lo;
 }
 
+// Rank path of the per-image merge (detect without a final NMS, C <= 64): the first top_k of the
+// merged order (score desc, then class, then in-class rank — models/utils.py:274-290: the
+// class-order concatenation, then a descending sort when more than top_k were kept).
+//   1. the kept windows of all classes -> LDS (one coalesced pass; kc / lastkey meanwhile);
+//   2. wave 0 (one lane per class): class offsets, truncation bound, and a lower bound L on the
+//      top_k-th merged key — with k* the smallest k such that the first min(kc_c, k) entries of
+//      all classes number >= top_k, every one of those is >= L = min_c (entry min(kc_c,k*)-1 of
+//      class c), so no entry below L can rank < top_k;
+//   3. the entries >= L (typically ~2 top_k of the ~20 x 64 kept) are compacted, and each one's
+//      merged rank is counted against all of them (broadcast LDS reads, the count split over
+//      the block's threads) — no sort, no radix select, three barriers;
+//   4. entries with rank < top_k are written at their rank.
+// Returns -1 when not applicable (the caller's general merge runs), else the merge status.
+__device__ __forceinline__ int merge_rank(
+    const unsigned long long *kept, const uint32_t *kc, const unsigned long long *lastkey,
+    const float *__restrict__ boxes_ws, int P, int C, int stride, int wmax, int top_k, int pass,
+    int32_t *__restrict__ need, float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
+    float *__restrict__ out_scores, int32_t *__restrict__ out_count) {
+  extern __shared__ unsigned char s_raw[];
+  __shared__ uint32_t r_off[kRankC + 1], r_kc[kRankC];
+  __shared__ unsigned long long r_L;
+  __shared__ uint32_t r_trunc, r_kth;
+  __shared__ int r_m, r_total, r_any;
+  const int nslot = (C - 1) * wmax;   // kc <= wmax entries per class (stored at `stride`)
+  if (C > kRankC || static_cast<size_t>(nslot) * 20 > static_cast<size_t>(kRankLds)) return -1;
+  const int b = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
+  const int64_t sb0 = static_cast<int64_t>(b) * C;
+#ifdef SBOD_PHASE_CLOCKS
+  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  SEG_PHASE(0);
+  unsigned long long *sl = reinterpret_cast<unsigned long long *>(s_raw);   // [nslot] kept windows
+  unsigned long long *sk = sl + nslot;                                      // [<= nslot] entries >= L
+  uint32_t *rk = reinterpret_cast<uint32_t *>(sk + nslot);                 // [<= nslot] ranks
+  {
+    const unsigned long long *kb = kept + (sb0 + 1) * stride;   // classes 1..C-1
+    constexpr int kB = 4;
+    for (int s0 = 0; s0 < nslot; s0 += kB * NT) {
+      unsigned long long r[kB];
+#pragma unroll
+      for (int k = 0; k < kB; ++k) {
+        const int sidx = min(s0 + k * NT + tid, nslot - 1), cc = sidx / wmax;
+        r[k] = kb[static_cast<int64_t>(cc) * stride + (sidx - cc * wmax)];
+      }
+#pragma unroll
+      for (int k = 0; k < kB; ++k) {
+        const int s = s0 + k * NT + tid;
+        if (s < nslot) {
+          sl[s] = r[k];
+          rk[s] = 0u;
+        }
+      }
+    }
+  }
+  uint32_t kcv = 0;
+  if (tid < 64) {
+    const int c = tid;
+    const bool cv = c >= 1 && c < C;
+    kcv = cv ? kc[sb0 + c] : 0u;
+    const unsigned long long lk = cv ? lastkey[sb0 + c] : 0ull;
+    uint32_t incl = kcv;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(incl, off, 64);
+      if (c >= off) incl += v;
+    }
+    if (c <= C) r_off[c] = incl - kcv;
+    r_kc[c] = kcv;
+    uint32_t tr = lk != 0ull ? static_cast<uint32_t>(lk >> 32) : 0u;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) tr = max(tr, static_cast<uint32_t>(__shfl_xor(tr, m, 64)));
+    const int total = static_cast<int>(__shfl(incl, 63, 64));
+    const bool any = __ballot(lk != 0ull) != 0ull;   // whole wave (not inside the lane-0 branch)
+    if (c == 0) {
+      r_trunc = tr;
+      r_any = any;
+      r_total = total;
+      r_m = 0;
+      r_kth = 0u;
+    }
+  }
+  __syncthreads();
+  SEG_PHASE(1);
+  const int total = r_total;
+  const bool any_trunc = r_any != 0;
+  float *ob = out_boxes + static_cast<int64_t>(b) * top_k * 4;
+  int64_t *ol = out_labels + static_cast<int64_t>(b) * top_k;
+  float *os = out_scores + static_cast<int64_t>(b) * top_k;
+  auto emit = [&](int r, int c, unsigned long long key) {
+    st4(ob + 4 * r, ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(key))));
+    ol[r] = c;
+    os[r] = key_score(key);
+  };
+  auto undecided = [&]() {
+    if (tid == 0) {
+      if (pass == 1) need[b] = 1;
+      out_count[b] = -1;
+    }
+    return 1;
+  };
+  if (total <= top_k) {
+    if (any_trunc) return undecided();   // a truncated window hides how many more exist
+    if (total == 0) {                    // models/utils.py:274-277 placeholder
+      if (tid == 0) {
+        st4(ob, Box4{0.f, 0.f, 1.f, 1.f});
+        ol[0] = 0;
+        os[0] = 0.f;
+        out_count[b] = 1;
+      }
+      return 0;
+    }
+    for (int r = tid; r < total; r += NT) {   // all kept, in class order
+      int lo = 1, hi = C - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (r_off[mid] <= static_cast<uint32_t>(r)) lo = mid;
+        else hi = mid - 1;
+      }
+      emit(r, lo, sl[(lo - 1) * wmax + (r - static_cast<int>(r_off[lo]))]);
+    }
+    if (tid == 0) out_count[b] = total;
+    return 0;
+  }
+  auto mkey = [&](int c, int pos) {
+    return (sl[(c - 1) * wmax + pos] & 0xffffffff00000000ull) |
+           (0xffffffffu - ((static_cast<uint32_t>(c) << 24) | static_cast<uint32_t>(pos)));
+  };
+  if (tid < 64) {
+    const int c = tid;
+    const bool cv = c >= 1 && c < C && kcv > 0u;
+    int lo = 1, hi = top_k;   // k*: smallest k with sum_c min(kc_c, k) >= top_k (exists: total > top_k)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (wave_sum_i32(static_cast<int>(min(kcv, static_cast<uint32_t>(mid)))) >= top_k) hi = mid;
+      else lo = mid + 1;
+    }
+    unsigned long long lc = cv ? mkey(c, static_cast<int>(min(kcv, static_cast<uint32_t>(lo))) - 1) : ~0ull;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const unsigned long long o = shfl_xor_u64(lc, m);
+      lc = o < lc ? o : lc;
+    }
+    if (c == 0) r_L = lc;
+  }
+  __syncthreads();
+  SEG_PHASE(2);
+  const unsigned long long L = r_L;
+  for (int s = tid; s < nslot; s += NT) {
+    const int c = s / wmax + 1, pos = s - (c - 1) * wmax;
+    if (pos < static_cast<int>(min(r_kc[c], static_cast<uint32_t>(top_k)))) {
+      const unsigned long long k = mkey(c, pos);
+      if (k >= L) sk[atomicAdd(&r_m, 1)] = k;
+    }
+  }
+  __syncthreads();
+  SEG_PHASE(3);
+  const int m = r_m;
+  const int nsplit = max(1, min(16, NT / m)), per = (m + nsplit - 1) / nsplit;
+  for (int t = tid; t < m * nsplit; t += NT) {
+    const int e = t % m, part = t / m;
+    const int j0 = part * per, j1 = min(m, j0 + per);
+    const unsigned long long ke = sk[e];
+    uint32_t cnt = 0;
+    for (int j = j0; j < j1; ++j) cnt += sk[j] > ke ? 1u : 0u;
+    if (cnt) atomicAdd(&rk[e], cnt);
+  }
+  __syncthreads();
+  SEG_PHASE(4);
+  for (int e = tid; e < m; e += NT) {
+    const uint32_t rank = rk[e];
+    if (rank < static_cast<uint32_t>(top_k)) {
+      const unsigned long long k = sk[e];
+      const uint32_t low = 0xffffffffu - static_cast<uint32_t>(k);
+      const int c = static_cast<int>(low >> 24), pos = static_cast<int>(low & 0xffffffu);
+      emit(static_cast<int>(rank), c, sl[(c - 1) * wmax + pos]);
+      if (rank == static_cast<uint32_t>(top_k - 1)) r_kth = static_cast<uint32_t>(k >> 32);
+    }
+  }
+  __syncthreads();
+  SEG_PHASE(5);
+#ifdef SBOD_PHASE_CLOCKS
+  if (tid == 0 && (b == 0 || b == 5))
+    printf("mrank p%d b%d total=%d m=%d: load+scan %lld L %lld compact %lld rank %lld emit %lld total %lld\n", pass, b,
+           total, m, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[5] - ph[4], ph[5] - ph[0]);
+#endif
+  // a truncated class may hide candidates scoring up to its window's last key: the top_k-th
+  // output must beat them all (else the wider second-pass window decides)
+  if (any_trunc && !(r_kth > r_trunc)) return undecided();
+  if (tid == 0) out_count[b] = top_k;
+  return 0;
+}
+
 // pass: 0 = single pass (invalid -> count -1), 1 = first of two (invalid -> need[b] = 1),
 // 2 = second (only images with need[b]; invalid -> count -1).
 __device__ __forceinline__ int merge_body(
     const unsigned long long *kept, const uint32_t *kc,
     const unsigned long long *lastkey, const float *__restrict__ boxes_ws, int P,
-    int C, int window, int top_k, float final_nms, int general, int pass,
+    int C, int window, int wmax, int top_k, float final_nms, int general, int pass,
     int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
     float *__restrict__ out_scores, int32_t *__restrict__ out_count) {
@@ -928,6 +1427,11 @@ __device__ __forceinline__ int merge_body(
   const int b = blockIdx.x, tid = threadIdx.x;
   const int64_t sb0 = static_cast<int64_t>(b) * C;
   if (pass == 2 && need[b] == 0) return 0;
+  if (final_nms < 0.f && !general) {
+    const int st = merge_rank(kept, kc, lastkey, boxes_ws, P, C, window, wmax, top_k, pass, need, out_boxes,
+                              out_labels, out_scores, out_count);
+    if (st >= 0) return st;
+  }
 #ifdef SBOD_PHASE_CLOCKS
   long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1174,14 +1678,16 @@ __host__ __device__ inline size_t inline2_lds(int window) {
 // image needs it.
 __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     const unsigned long long *kept, const uint32_t *kc, const unsigned long long *lastkey,
-    const float *__restrict__ boxes_ws, int P, int C, int window, int top_k, float final_nms, int general,
-    int pass, int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
+    const float *__restrict__ boxes_ws, int P, int C, int window, int wfirst, int top_k, float final_nms,
+    int general, int pass, int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
     int32_t *__restrict__ out_count, const unsigned long long *cand, const uint32_t *cand_count, float thr,
     SegOut so) {
   extern __shared__ unsigned char s_raw[];
-  const int st = merge_body(kept, kc, lastkey, boxes_ws, P, C, window, top_k, final_nms, general, pass, need,
+  STAMP_BEGIN();
+  const int st = merge_body(kept, kc, lastkey, boxes_ws, P, C, window, wfirst, top_k, final_nms, general, pass, need,
                             scratch, out_boxes, out_labels, out_scores, out_count);
+  STAMP_END(3, 1);
   if (st == 0 || pass != 1) return;
   const int b = blockIdx.x;
   uint32_t *h2 = reinterpret_cast<uint32_t *>(s_raw + ((seg_lds(window) + 15) & ~static_cast<size_t>(15)));
@@ -1198,7 +1704,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
       segment_body(cand, cand_count, boxes_ws, P, C, b, c, window, window, thr, so, s_raw, h2, st2, fl2, m2,
                    iv, iv + 1, iv + 2);
   __syncthreads();
-  merge_body(kept, kc, lastkey, boxes_ws, P, C, window, top_k, final_nms, general, 2, need, scratch, out_boxes,
+  merge_body(kept, kc, lastkey, boxes_ws, P, C, window, window, top_k, final_nms, general, 2, need, scratch, out_boxes,
              out_labels, out_scores, out_count);
 }
 
@@ -1351,8 +1857,13 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   {
     KernelTimer kt("k_det_segment", s);
     if (w1 <= 64)
+#ifdef SBOD_SEG_WAVE
       hipLaunchKernelGGL(k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, ws.boxes,
                          P, C, w1, w2, max_overlap, so, nullptr);
+#else
+      hipLaunchKernelGGL(k_det_segment_w4, dim3(C - 1, B), dim3(64 * kSegW), 0, s, ws.cand, ws.count, ws.boxes,
+                         P, C, w1, w2, max_overlap, so);
+#endif
     else
       hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
                          ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
@@ -1364,7 +1875,7 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     const size_t seg2 = two ? inline2_lds(w2) : 0;
     KernelTimer kt("k_det_merge", s);
     hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, ws.kept,
-                       ws.kc, ws.lastkey, ws.boxes, P, C, w2, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
+                       ws.kc, ws.lastkey, ws.boxes, P, C, w2, w1, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
                        ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, ws.cand, ws.count,
                        max_overlap, so);
   }
@@ -1412,3 +1923,5 @@ int sbod_nms_f32(const float *boxes, const float *scores, int64_t n, float overl
 }
 
 }  // extern "C"
+
+SBOD_STAMP_EXPORT(nms)

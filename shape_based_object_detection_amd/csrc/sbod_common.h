@@ -183,3 +183,47 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
 }
 
 }  // namespace sbod
+
+// ----------------------------------------------------------------------------- debug timeline
+// -DSBOD_BLOCK_STAMPS (diagnostic builds only; scripts/build_stamps_lib.sh): the kernel armed
+// by sbod_debug_stamps_<tu>(arm) records, per workgroup, its wall-clock start and end
+// (s_memrealtime, 100 MHz) and the CU it ran on, so launch ramp, per-block duration and tail
+// can be read off one dispatch.  Compiles to nothing otherwise.
+#ifdef SBOD_BLOCK_STAMPS
+#define SBOD_STAMP_CAP 65536u
+#define SBOD_STAMP_DECL                                                  \
+  static __device__ unsigned long long g_stamps[2 * SBOD_STAMP_CAP]; \
+  static __device__ int g_stamp_armed = -1;
+#define STAMP_BEGIN() const unsigned long long _st0 = __builtin_amdgcn_s_memrealtime()
+// SYNC: 1 = the whole workgroup is still running (barrier first), 0 = the caller is the last wave
+#define STAMP_END(ID, SYNC)                                                                      \
+  do {                                                                                           \
+    if (g_stamp_armed == (ID)) {                                                                 \
+      if (SYNC) __syncthreads();                                                                 \
+      if ((threadIdx.x & 63) == 0 && ((SYNC) == 0 || threadIdx.x == 0)) {                        \
+        const unsigned _blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);    \
+        if (_blk < SBOD_STAMP_CAP) {                                                          \
+          g_stamps[2 * _blk] = _st0;                                                             \
+          g_stamps[2 * _blk + 1] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) |     \
+                                   (static_cast<unsigned long long>(__smid() & 0xffff) << 48);  \
+        }                                                                                        \
+      }                                                                                          \
+    }                                                                                            \
+  } while (0)
+#define SBOD_STAMP_EXPORT(TU)                                                                    \
+  extern "C" int sbod_debug_stamps_##TU(int arm, unsigned long long *host, int n) {              \
+    if (host && n > 0)                                                                           \
+      hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 2 *           \
+                          (n < static_cast<int>(SBOD_STAMP_CAP) ? n : SBOD_STAMP_CAP));     \
+    void *_sym = nullptr;                                                                        \
+    if (hipGetSymbolAddress(&_sym, HIP_SYMBOL(g_stamps)) == hipSuccess)                          \
+      hipMemset(_sym, 0, sizeof(unsigned long long) * 2 * SBOD_STAMP_CAP);                       \
+    hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_armed), &arm, sizeof(int));                             \
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;                                        \
+  }
+#else
+#define SBOD_STAMP_DECL
+#define STAMP_BEGIN() do { } while (0)
+#define STAMP_END(ID, SYNC) do { } while (0)
+#define SBOD_STAMP_EXPORT(TU)
+#endif
