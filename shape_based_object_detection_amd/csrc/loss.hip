@@ -254,13 +254,21 @@ struct LossArgs {
   float *partials, *pool;
 };
 
-template <typename T>
-__global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__restrict__ locs,
+// exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'
+// budget is 1e-4 relative; the all-classes underflow test (p == 0 -> NaN) stays exact (below).
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+// CM > 0: class rows of C <= CM in registers (padding slots -inf: no per-slot guards in the
+// max / exp / sum); CM == 0: any C, rows in LDS.
+template <typename T, int CM, int CLS>
+__global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__restrict__ locs,
                                                      const T *__restrict__ scores,
                                                      T *__restrict__ glocs, T *__restrict__ gsc) {
   extern __shared__ float s_sc[];
   __shared__ float s_red[16];
   STAMP_BEGIN();
+  PHASE_DECL;
+  SEG_PHASE(0);
   const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x;
   const int P = a.P, C = a.C;
   const int np = min(kLTile, P - p0);
@@ -270,6 +278,7 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
   const bool grad = gsc != nullptr;
   __syncthreads();
+  SEG_PHASE(1);
   float conf_l = 0.f, loc_l = 0.f;
   if (tid < np) {
     const int p = p0 + tid;
@@ -287,6 +296,124 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
       easy = e1 / (e0 + e1) < a.theta;
     }
     const bool pos = c > 0 && !easy;
+    // ---------------- classification
+    float *row = s_sc + tid * C;
+    if constexpr (CM > 0) {
+      float r[CM];
+      float m = -__builtin_inff(), zmin = __builtin_inff();
+#pragma unroll
+      for (int k = 0; k < CM; ++k) {
+        r[k] = k < C ? row[k] : -__builtin_inff();
+        m = r[k] > m ? r[k] : m;
+        zmin = (k < C && r[k] < zmin) ? r[k] : zmin;
+      }
+      const float zt = row[c];
+      // the exponentials are summed here and recomputed (bit-identically) from the LDS row in
+      // the gradient loops, so r[] is dead before the loss math (no spills around powf)
+      float s = 0.f;
+      if constexpr (CLS == SBOD_CLS_FOCAL) {
+#pragma unroll
+        for (int k = 0; k < CM; ++k) s += fast_exp(r[k] - m);   // padding: exp(-inf) = 0
+      } else {
+        // CE feeds the hard-negative selection (a ranking): the accurate exp keeps its values
+        // within an ulp of the reference's so near-ties at the top-k boundary do not move
+#pragma unroll
+        for (int k = 0; k < CM; ++k) s += expf(r[k] - m);
+      }
+      const float inv = 1.f / s;
+      if constexpr (CLS == SBOD_CLS_FOCAL) {
+        if (pos || negrow) {  // SSD512.py:588-593: rows = positives ++ negatives(IoU < thr - 0.1)
+          const float scale = (a.flags & SBOD_LOSS_FOCAL_NORM) ? 1.f / n : 1.f;
+          // Loss.py:9-38: q = p_t; background rows weighted by p_bg (sic)
+          const float q = fast_exp(zt - m) * inv;
+          const float lq = logf(q);
+          float loss, dq;
+          if (c == 0) {  // alpha_bg * p0^gamma * (-log p0)
+            loss = a.abg * powg(q, a.gamma) * -lq;
+            dq = a.abg * (a.gamma * powg1(q, a.gamma) * -lq - powg1(q, a.gamma));
+          } else {       // alpha_fg * (1 - p_t)^gamma * (-log p_t)
+            const float om = 1.f - q;
+            loss = a.afg * powg(om, a.gamma) * -lq;
+            dq = a.afg * (-a.gamma * powg1(om, a.gamma) * -lq - powg(om, a.gamma) / q);
+          }
+          // 0 * log 0 in the reference when any class probability is exactly 0: decided on the
+          // smallest logit with the accurate exp (underflow is monotone in the logit)
+          if (!(expf(zmin - m) * inv > 0.f)) loss = __builtin_nanf("");
+          conf_l += loss;
+          if (grad) {
+            const float kq = dq * q * scale;
+#pragma unroll
+            for (int k = 0; k < CM; ++k)
+              if (k < C) row[k] = loss != loss ? loss : kq * ((k == c ? 1.f : 0.f) - fast_exp(row[k] - m) * inv);
+          }
+        } else if (grad) {
+#pragma unroll
+          for (int k = 0; k < CM; ++k)
+            if (k < C) row[k] = 0.f;
+        }
+      } else {
+        const float ce = -((zt - m) - logf(s));  // cross_entropy = -log_softmax[t]
+        if (pos) {
+          conf_l += ce;
+          a.pool[i] = -1.f;
+          if (grad) {
+            const float sc = 1.f / n;
+#pragma unroll
+            for (int k = 0; k < CM; ++k)
+              if (k < C) row[k] = (expf(row[k] - m) * inv - (k == c ? 1.f : 0.f)) * sc;
+          }
+        } else {
+          bool member;
+          const int pool = a.flags & (SBOD_POOL_NEG | SBOD_POOL_GLOBAL_NEG | SBOD_POOL_NONPOS_NOT_EASY);
+          if (pool == SBOD_POOL_NEG || pool == SBOD_POOL_GLOBAL_NEG) member = negrow;
+          else if (pool == SBOD_POOL_NONPOS_NOT_EASY) member = !easy;
+          else member = true;
+          a.pool[i] = member ? ce : -1.f;
+          if (grad) {
+#pragma unroll
+            for (int k = 0; k < CM; ++k)
+              if (k < C) row[k] = 0.f;
+          }
+        }
+      }
+    } else {
+      float m = row[0];
+      for (int k = 1; k < C; ++k) m = fmaxf(m, row[k]);
+      const float zt = row[c];
+      float s = 0.f;
+      for (int k = 0; k < C; ++k) {
+        const float e = expf(row[k] - m);
+        row[k] = e;
+        s += e;
+      }
+      if (a.cls == SBOD_CLS_FOCAL) {
+        if (pos || negrow) {  // SSD512.py:588-593: rows = positives ++ negatives(IoU < thr - 0.1)
+          const float scale = (a.flags & SBOD_LOSS_FOCAL_NORM) ? 1.f / n : 1.f;
+          conf_l += focal_row(row, C, c, s, a.afg, a.abg, a.gamma, scale, grad);
+        } else if (grad) {
+          for (int k = 0; k < C; ++k) row[k] = 0.f;
+        }
+      } else {
+        const float ce = -((zt - m) - logf(s));  // cross_entropy = -log_softmax[t]
+        if (pos) {
+          conf_l += ce;
+          a.pool[i] = -1.f;
+          if (grad) {
+            const float inv = 1.f / s, sc = 1.f / n;
+            for (int k = 0; k < C; ++k) row[k] = (row[k] * inv - (k == c ? 1.f : 0.f)) * sc;
+          }
+        } else {
+          bool member;
+          const int pool = a.flags & (SBOD_POOL_NEG | SBOD_POOL_GLOBAL_NEG | SBOD_POOL_NONPOS_NOT_EASY);
+          if (pool == SBOD_POOL_NEG || pool == SBOD_POOL_GLOBAL_NEG) member = negrow;
+          else if (pool == SBOD_POOL_NONPOS_NOT_EASY) member = !easy;
+          else member = true;
+          a.pool[i] = member ? ce : -1.f;
+          if (grad)
+            for (int k = 0; k < C; ++k) row[k] = 0.f;
+        }
+      }
+    }
     // ---------------- box regression
     float gl[4] = {0.f, 0.f, 0.f, 0.f};
     if (pos) {
@@ -339,49 +466,18 @@ __global__ __launch_bounds__(kLTile) void k_multibox(LossArgs a, const T *__rest
         for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
       }
     }
-    // ---------------- classification
-    float *row = s_sc + tid * C;
-    float m = row[0];
-    for (int k = 1; k < C; ++k) m = fmaxf(m, row[k]);
-    const float zt = row[c];
-    float s = 0.f;
-    for (int k = 0; k < C; ++k) {
-      const float e = expf(row[k] - m);
-      row[k] = e;
-      s += e;
-    }
-    if (a.cls == SBOD_CLS_FOCAL) {
-      if (pos || negrow) {  // SSD512.py:588-593: rows = positives ++ negatives(IoU < thr - 0.1)
-        const float scale = (a.flags & SBOD_LOSS_FOCAL_NORM) ? 1.f / n : 1.f;
-        conf_l += focal_row(row, C, c, s, a.afg, a.abg, a.gamma, scale, grad);
-      } else if (grad) {
-        for (int k = 0; k < C; ++k) row[k] = 0.f;
-      }
-    } else {
-      const float ce = -((zt - m) - logf(s));  // cross_entropy = -log_softmax[t]
-      if (pos) {
-        conf_l += ce;
-        a.pool[i] = -1.f;
-        if (grad) {
-          const float inv = 1.f / s, sc = 1.f / n;
-          for (int k = 0; k < C; ++k) row[k] = (row[k] * inv - (k == c ? 1.f : 0.f)) * sc;
-        }
-      } else {
-        bool member;
-        const int pool = a.flags & (SBOD_POOL_NEG | SBOD_POOL_GLOBAL_NEG | SBOD_POOL_NONPOS_NOT_EASY);
-        if (pool == SBOD_POOL_NEG || pool == SBOD_POOL_GLOBAL_NEG) member = negrow;
-        else if (pool == SBOD_POOL_NONPOS_NOT_EASY) member = !easy;
-        else member = true;
-        a.pool[i] = member ? ce : -1.f;
-        if (grad)
-          for (int k = 0; k < C; ++k) row[k] = 0.f;
-      }
-    }
   }
   __syncthreads();
+  SEG_PHASE(2);
   if (grad) tile_store(gsc + rbase * C, s_sc, np * C);
   conf_l = block_sum(conf_l, s_red);
   loc_l = block_sum(loc_l, s_red + 8);
+  SEG_PHASE(3);
+#ifdef SBOD_PHASE_CLOCKS
+  if (PHASE_PRINT_SEL)
+    printf("multibox x%d b%d: load %lld compute %lld store+sum %lld total %lld\n", blockIdx.x, b,
+           ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
+#endif
   if (tid == 0) {
     const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
     a.partials[2 * blk] = conf_l;
@@ -700,14 +796,30 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   const size_t lds = static_cast<size_t>(kLTile) * C * sizeof(float);
   {
     KernelTimer kt("k_multibox", s);
-    if (dtype == SBOD_DT_F32)
-      hipLaunchKernelGGL(k_multibox<float>, grid, dim3(kLTile), lds, s, a,
-                         static_cast<const float *>(locs), static_cast<const float *>(scores),
-                         static_cast<float *>(grad_locs), static_cast<float *>(grad_scores));
-    else
-      hipLaunchKernelGGL(k_multibox<uint16_t>, grid, dim3(kLTile), lds, s, a,
-                         static_cast<const uint16_t *>(locs), static_cast<const uint16_t *>(scores),
-                         static_cast<uint16_t *>(grad_locs), static_cast<uint16_t *>(grad_scores));
+#define SBOD_MB(T, CM, CLS)                                                                       \
+  hipLaunchKernelGGL((k_multibox<T, CM, CLS>), grid, dim3(kLTile), lds, s, a, static_cast<const T *>(locs), \
+                     static_cast<const T *>(scores), static_cast<T *>(grad_locs), static_cast<T *>(grad_scores))
+    // rows of C <= CM classes in registers; wider rows take the LDS path
+#define SBOD_MB_C(T)                                                  \
+  do {                                                                \
+    if (cls == SBOD_CLS_FOCAL) {                                      \
+      if (C <= 8) SBOD_MB(T, 8, SBOD_CLS_FOCAL);                      \
+      else if (C <= 16) SBOD_MB(T, 16, SBOD_CLS_FOCAL);               \
+      else if (C <= 24) SBOD_MB(T, 24, SBOD_CLS_FOCAL);               \
+      else if (C <= 32) SBOD_MB(T, 32, SBOD_CLS_FOCAL);               \
+      else SBOD_MB(T, 0, SBOD_CLS_FOCAL);                             \
+    } else {                                                          \
+      if (C <= 8) SBOD_MB(T, 8, SBOD_CLS_CE);                         \
+      else if (C <= 16) SBOD_MB(T, 16, SBOD_CLS_CE);                  \
+      else if (C <= 24) SBOD_MB(T, 24, SBOD_CLS_CE);                  \
+      else if (C <= 32) SBOD_MB(T, 32, SBOD_CLS_CE);                  \
+      else SBOD_MB(T, 0, SBOD_CLS_CE);                                \
+    }                                                                 \
+  } while (0)
+    if (dtype == SBOD_DT_F32) SBOD_MB_C(float);
+    else SBOD_MB_C(uint16_t);
+#undef SBOD_MB_C
+#undef SBOD_MB
   }
   SBOD_LAUNCHED("k_multibox");
   int nseg = 0;

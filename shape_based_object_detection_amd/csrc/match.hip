@@ -91,20 +91,24 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) npos[B] = 0;  // phase 2 accumulates
   __shared__ int32_t s_lab[kMaxGLds];
   __shared__ int s_red[16];
+  PHASE_DECL;
+  SEG_PHASE(0);
   const int b = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ntile = gridDim.x;
+  // the prior's own load goes out first: it does not wait on the ground-truth chain
+  const int p = blockIdx.x * kTile + threadIdx.x;
+  const bool valid = p < P;
+  Anchor a{0.f, 0.f, 0.f, 0.f, 0.f, false};
+  if (valid) a = load_anchor<kOdm>(anchors, priors, b, P, p);
   const int g0 = off[b], G = off[b + 1] - g0;
   load_gt_tile(s_gt, gt, g0, G);
   for (int i = threadIdx.x; i < G && i < kMaxGLds; i += blockDim.x)
     s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
   __syncthreads();
-  const int p = blockIdx.x * kTile + threadIdx.x;
-  const bool valid = p < P;
-  Anchor a{0.f, 0.f, 0.f, 0.f, 0.f, false};
-  if (valid) a = load_anchor<kOdm>(anchors, priors, b, P, p);
+  SEG_PHASE(1);
   float best = 0.f;
   int bi = 0;
-  const unsigned long long low = 0xffffffffull - static_cast<uint32_t>(p);
+  const int pw = blockIdx.x * kTile + wv * 64;   // prior of lane 0 of this wave
   unsigned long long *prow = part + (static_cast<int64_t>(b) * ntile + blockIdx.x) * Gmax;
   for (int g = 0; g < G; ++g) {
     const float ov = iou_metrics(s_gt[g], a.x1, a.y1, a.x2, a.y2, a.area, a.zero);
@@ -112,13 +116,21 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
       best = ov;
       bi = g;
     }
-    unsigned long long key = valid ? ((static_cast<unsigned long long>(f2ord(ov)) << 32) | low) : 0ull;
-    key = wave_max_u64(key);
+    // the wave's best (ord(overlap), lowest prior) — torch's first-index argmax over priors:
+    // max of the 32-bit ord over the wave (DPP), then the lowest lane holding it (ballot)
+    const uint32_t ko = valid ? f2ord(ov) : 0u;   // f2ord of any real overlap is > 0
+    const uint32_t mx = wave_max_u32(ko);
+    const unsigned long long hit = __ballot(valid && ko == mx);
     if (lane == 0) {
+      const unsigned long long key =
+          hit ? ((static_cast<unsigned long long>(mx) << 32) |
+                 (0xffffffffull - static_cast<uint32_t>(pw + __builtin_ctzll(hit))))
+              : 0ull;
       if (G <= kMaxGLds) s_key[wv][g] = key;
       else if (key) atomicMax(prow + g, key);   // very large G: partial row via atomics
     }
   }
+  SEG_PHASE(2);
   int pos = 0;
   if (valid) {
     obj[static_cast<int64_t>(b) * P + p] = bi;
@@ -144,6 +156,12 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
     }
   }
   if (threadIdx.x == 0) tcount[b * ntile + blockIdx.x] = pos;
+  SEG_PHASE(3);
+#ifdef SBOD_PHASE_CLOCKS
+  if (PHASE_PRINT_SEL)
+    printf("match x%d b%d G=%d: gt %lld iou+argmax %lld store+sum %lld total %lld\n", blockIdx.x, b, G,
+           ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
+#endif
   STAMP_END(5, 1);
 }
 

@@ -24,7 +24,6 @@ namespace sbod {
 SBOD_STAMP_DECL
 
 constexpr int kDTile = 256;
-constexpr int kPrepRegC = 32;    // prepare: class rows up to this width are processed in registers
 constexpr int kSegThreads = 256;
 constexpr int kMaxWindow = 4096;   // LDS-resident window (keys + boxes + areas + flags)
 constexpr int kMergeThreads = 1024;
@@ -397,12 +396,6 @@ __device__ int block_greedy_matrix(const Box4 *sb, const float *sa, int n, float
   return *s_nk;
 }
 
-// Debug aid (off by default): -DSBOD_PHASE_CLOCKS prints per-phase cycle stamps of two blocks.
-#ifdef SBOD_PHASE_CLOCKS
-#define SEG_PHASE(i) do { __syncthreads(); if (threadIdx.x == 0) ph[i] = clock64(); } while (0)
-#else
-#define SEG_PHASE(i) do { } while (0)
-#endif
 
 // ----------------------------------------------------------------------------- K1
 struct DetArgs {
@@ -445,6 +438,9 @@ __device__ __forceinline__ void prep_slots(const DetArgs &a, int b, int C, int t
   __syncthreads();
 }
 
+// CM > 0: rows of C <= CM classes live in CM registers (padding slots hold -inf, so the max, the
+// exponentials and the sum need no per-slot guards); CM == 0: any C, rows in LDS.
+template <int CM>
 __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__restrict__ locs,
                                                         const float *__restrict__ scores) {
   // dynamic LDS: score tile [kDTile][C] f32 | ballots [kDTile/64][C] u64 | slot bases [C] u32,
@@ -484,7 +480,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     if (a.box_type == SBOD_BOX_CORNER) st4(locs + 4 * i, d);  // models/utils.py:224 clamp_ in place
     st4(a.boxes_ws + 4 * i, d);
     if (a.dbg_boxes) st4(a.dbg_boxes + 4 * i, d);
-    if (C > kPrepRegC) {
+    if constexpr (CM == 0) {
       if (a.act == SBOD_ACT_SOFTMAX) {
         float m = row[0];
         for (int k = 1; k < C; ++k) m = fmaxf(m, row[k]);
@@ -504,34 +500,34 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   const bool allowed = valid && (a.pos == nullptr || a.pos[i] != 0);
   const int wv = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  if (C <= kPrepRegC) {
+  if constexpr (CM > 0) {
     // ---- narrow rows (VOC: C = 21): the row, its activation and the candidate tests stay in
     // registers.  Activation: exp2 / rcp hardware ops (probabilities within ~1e-6 relative of
     // torch.softmax; every later decision reads these same values, so detect stays exact w.r.t.
     // them).  Each lane then walks only ITS candidate classes (~1-2 of 20) to emit keys.
-    float r[kPrepRegC];
+    float r[CM];
 #pragma unroll
-    for (int k = 0; k < kPrepRegC; ++k) r[k] = row[min(k, C - 1)];
+    for (int k = 0; k < CM; ++k) r[k] = k < C ? row[k] : -__builtin_inff();
     if (a.act == SBOD_ACT_SOFTMAX) {
       float m = r[0];
 #pragma unroll
-      for (int k = 1; k < kPrepRegC; ++k) m = k < C ? fmaxf(m, r[k]) : m;
+      for (int k = 1; k < CM; ++k) m = r[k] > m ? r[k] : m;
       float sum = 0.f;
 #pragma unroll
-      for (int k = 0; k < kPrepRegC; ++k) {
-        r[k] = fast_exp(r[k] - m);
-        sum = k < C ? sum + r[k] : sum;
+      for (int k = 0; k < CM; ++k) {
+        r[k] = fast_exp(r[k] - m);   // padding: exp(-inf) = 0
+        sum += r[k];
       }
       const float rs = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
-      for (int k = 0; k < kPrepRegC; ++k) r[k] = r[k] * rs;
+      for (int k = 0; k < CM; ++k) r[k] = r[k] * rs;
     } else {
 #pragma unroll
-      for (int k = 0; k < kPrepRegC; ++k) r[k] = fast_sigmoid(r[k]);
+      for (int k = 0; k < CM; ++k) r[k] = fast_sigmoid(r[k]);
     }
     uint32_t cmask = 0;
 #pragma unroll
-    for (int k = 0; k < kPrepRegC; ++k) {
+    for (int k = 0; k < CM; ++k) {
       if (k < C) {
         row[k] = r[k];                         // for the emission loop and the debug copy
         if (k >= 1) {
@@ -1341,13 +1337,20 @@ __device__ __forceinline__ int merge_rank(
   if (tid < 64) {
     const int c = tid;
     const bool cv = c >= 1 && c < C && kcv > 0u;
-    int lo = 1, hi = top_k;   // k*: smallest k with sum_c min(kc_c, k) >= top_k (exists: total > top_k)
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (wave_sum_i32(static_cast<int>(min(kcv, static_cast<uint32_t>(mid)))) >= top_k) hi = mid;
-      else lo = mid + 1;
+    // k*: the smallest k with sum_c min(kc_c, k) >= top_k (exists: total > top_k); lane l tests
+    // k = base + l + 1, the class counts read from the lanes that hold them
+    int kstar = 1;
+    for (int base = 0;; base += 64) {
+      const uint32_t k = static_cast<uint32_t>(base + c + 1);
+      uint32_t f = 0;
+      for (int c2 = 1; c2 < C; ++c2) f += min(static_cast<uint32_t>(__builtin_amdgcn_readlane(kcv, c2)), k);
+      const unsigned long long hit = __ballot(f >= static_cast<uint32_t>(top_k));
+      if (hit) {
+        kstar = base + __builtin_ctzll(hit) + 1;
+        break;
+      }
     }
-    unsigned long long lc = cv ? mkey(c, static_cast<int>(min(kcv, static_cast<uint32_t>(lo))) - 1) : ~0ull;
+    unsigned long long lc = cv ? mkey(c, static_cast<int>(min(kcv, static_cast<uint32_t>(kstar))) - 1) : ~0ull;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
       const unsigned long long o = shfl_xor_u64(lc, m);
@@ -1374,7 +1377,15 @@ __device__ __forceinline__ int merge_rank(
     const int j0 = part * per, j1 = min(m, j0 + per);
     const unsigned long long ke = sk[e];
     uint32_t cnt = 0;
-    for (int j = j0; j < j1; ++j) cnt += sk[j] > ke ? 1u : 0u;
+    int j = j0;
+    for (; j + 8 <= j1; j += 8) {   // eight independent (broadcast) LDS reads in flight
+      unsigned long long v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = sk[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cnt += v[u] > ke ? 1u : 0u;
+    }
+    for (; j < j1; ++j) cnt += sk[j] > ke ? 1u : 0u;
     if (cnt) atomicAdd(&rk[e], cnt);
   }
   __syncthreads();
@@ -1849,7 +1860,13 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
             debug_probs, debug_boxes};
   {
     KernelTimer kt("k_det_prepare", s);
-    hipLaunchKernelGGL(k_det_prepare, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
+    const dim3 pg((P + kDTile - 1) / kDTile, B);
+    const size_t pl = static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12;
+    if (C <= 8) hipLaunchKernelGGL(k_det_prepare<8>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 16) hipLaunchKernelGGL(k_det_prepare<16>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 24) hipLaunchKernelGGL(k_det_prepare<24>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 32) hipLaunchKernelGGL(k_det_prepare<32>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else hipLaunchKernelGGL(k_det_prepare<0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
                        static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, locs, scores);
   }
   SBOD_LAUNCHED("k_det_prepare");

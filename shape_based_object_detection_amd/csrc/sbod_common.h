@@ -84,6 +84,23 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
   return v;
 }
 
+// Wave-wide max of a u32, valid in every lane: DPP quad swaps and mirrors inside each row of 16,
+// then row broadcasts (gfx9 DPP) — no LDS traffic, a few cycles per step.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(static_cast<int>(x), static_cast<int>(x), kCtrl, kRowMask, 0xf, false));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, dpp_u32<0xB1, 0xf>(v));    // quad_perm [1,0,3,2]
+  v = max(v, dpp_u32<0x4E, 0xf>(v));    // quad_perm [2,3,0,1]
+  v = max(v, dpp_u32<0x141, 0xf>(v));   // row_half_mirror
+  v = max(v, dpp_u32<0x140, 0xf>(v));   // row_mirror: every lane of a row holds the row max
+  v = max(v, dpp_u32<0x142, 0xa>(v));   // row_bcast:15 -> rows 1, 3
+  v = max(v, dpp_u32<0x143, 0xc>(v));   // row_bcast:31 -> rows 2, 3: lane 63 holds the wave max
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
 __device__ __forceinline__ float wave_sum_f32(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
@@ -189,6 +206,16 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
 // by sbod_debug_stamps_<tu>(arm) records, per workgroup, its wall-clock start and end
 // (s_memrealtime, 100 MHz) and the CU it ran on, so launch ramp, per-block duration and tail
 // can be read off one dispatch.  Compiles to nothing otherwise.
+// Debug aid (off by default): -DSBOD_PHASE_CLOCKS prints per-phase cycle stamps of a few blocks.
+#ifdef SBOD_PHASE_CLOCKS
+#define SEG_PHASE(i) do { __syncthreads(); if (threadIdx.x == 0) ph[i] = clock64(); } while (0)
+#define PHASE_DECL long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PHASE_PRINT_SEL (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 20) && (blockIdx.y == 0 || blockIdx.y == 5))
+#else
+#define SEG_PHASE(i) do { } while (0)
+#define PHASE_DECL do { } while (0)
+#endif
+
 #ifdef SBOD_BLOCK_STAMPS
 #define SBOD_STAMP_CAP 65536u
 #define SBOD_STAMP_DECL                                                  \
