@@ -140,6 +140,26 @@ enum { SBOD_DT_F32 = 0, SBOD_DT_BF16 = 1 };
 enum { SBOD_LOSS_FOCAL_NORM = 4, SBOD_POOL_NONPOS = 0, SBOD_POOL_NEG = 8,
        SBOD_POOL_GLOBAL_NEG = 16, SBOD_POOL_NONPOS_NOT_EASY = 32 };
 size_t sbod_loss_workspace_bytes(int B, int P);
+
+/* Data-parallel global mining — the one exchange step of the data-parallel path (SURVEY
+ * §8(e)): MultiBoxLoss300's CE mines its hard negatives over the WHOLE batch
+ * (models/SSD300.py:580-588), so with the batch sharded over ranks the top-k must see every
+ * rank's pool.  Call sbod_multibox_loss with flags | SBOD_LOSS_DEFER_MINING (CE +
+ * SBOD_POOL_GLOBAL_NEG only): it runs the fused pass and leaves this rank's pool [B*P] f32
+ * (CE of pool members, -1 otherwise) at workspace + sbod_loss_pool_offset(B, P).  The caller
+ * all-gathers the pools rank-major (equal B on every rank) and calls
+ * sbod_multibox_mine_global with the gathered pool and this rank's offset in it: threshold,
+ * tie order (lowest global index first) and k = ratio * npos_total are those of one device
+ * holding the whole batch; the hard-negative gradients and the loss cover this rank's rows
+ * (the sum over ranks is the single-device loss).  Same workspace as the deferred call. */
+enum { SBOD_LOSS_DEFER_MINING = 64 };
+size_t sbod_loss_pool_offset(int B, int P);
+int sbod_multibox_mine_global(const void *scores, int dtype, int B, int P, int C,
+                              const int32_t *npos_total, int reg, int cls, int flags,
+                              int neg_pos_ratio, float reg_weight, const float *pool_all,
+                              int64_t n_all, int64_t local_off, void *grad_scores,
+                              float *loss_out, void *workspace, size_t workspace_bytes,
+                              void *stream);
 int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, int P, int C,
                        const float *priors_cxcy, const float *odm_arm_locs,
                        const float *arm_scores, const float *gt_boxes, const int64_t *gt_labels,

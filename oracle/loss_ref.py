@@ -162,12 +162,25 @@ def local_npos(priors_cxcy, boxes, labels, threshold=0.5):
     return int((cls > 0).sum())
 
 
+def ssd300_pool(priors_cxcy, scores, boxes, labels, threshold=0.5):
+    """MultiBoxLoss300's mining pool of this (shard of the) batch, flattened [B*P]: the CE of
+    negative priors (SSD300.py:571-580), -1 elsewhere — what data-parallel ranks exchange."""
+    B, P, C = scores.shape
+    _, cls, neg = _assign(priors_cxcy, boxes, labels, threshold)
+    ce = F.cross_entropy(scores.detach().reshape(-1, C), cls.reshape(-1), reduction='none')
+    return torch.where(torch.as_tensor(neg == -1).reshape(-1), ce, torch.full_like(ce, -1.0))
+
+
 def criterion(kind, priors_cxcy, locs, scores, boxes, labels, reg_loss, cls_loss,
-              threshold=0.5, neg_pos_ratio=3, reg_weights=1.0, npos_total=None):
+              threshold=0.5, neg_pos_ratio=3, reg_weights=1.0, npos_total=None, pool_all=None,
+              local_off=0):
     """kind: 'ssd512' (``models/SSD512.py:508-626``), 'ssd300' (``SSD300.py:477-594``),
     'retina' (``RetinaNet.py:385-506``).  ``locs``/``scores`` are autograd leaves.
     ``npos_total`` overrides the batch positive count in every normaliser (a data-parallel shard
-    normalised by the global count; summing shard losses gives the full-batch loss)."""
+    normalised by the global count; summing shard losses gives the full-batch loss).
+    ``pool_all``/``local_off`` (ssd300 CE, data-parallel): every rank's ``ssd300_pool``
+    concatenated rank-major and this shard's offset in it — the hard negatives are the global
+    top ratio*npos_total (ties: lowest global index first), summed over this shard's rows."""
     B, P, C = scores.shape
     obj, cls, neg = _assign(priors_cxcy, boxes, labels, threshold)
     pos = cls > 0
@@ -193,7 +206,14 @@ def criterion(kind, priors_cxcy, locs, scores, boxes, labels, reg_loss, cls_loss
     else:
         ce = F.cross_entropy(scores.view(-1, C), cls.view(-1), reduction='none').view(B, P)
         n_hard = neg_pos_ratio * n_pos
-        if kind == 'ssd300':
+        if kind == 'ssd300' and pool_all is not None:
+            k = neg_pos_ratio * int(n_tot)
+            vals = pool_all.detach().cpu().numpy()
+            order = np.argsort(-vals, kind='stable')              # value desc, index asc on ties
+            sel = order[vals[order] >= 0][:k]
+            mine = sel[(sel >= local_off) & (sel < local_off + B * P)] - local_off
+            hard = ce.reshape(-1)[torch.from_numpy(mine)].sum()
+        elif kind == 'ssd300':
             negs = ce[negm]
             k = int(n_hard.sum())
             hard = torch.topk(negs, min(k, negs.numel())).values.sum() if k > 0 else ce.new_zeros(())

@@ -33,6 +33,9 @@ SIGNATURES = {
     'sbod_loss_workspace_bytes': (SZ, [I32, I32]),
     'sbod_multibox_loss': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, P, F32, F32,
                                  F32, I32, I32, I32, I32, F32, F32, F32, P, P, P, P, SZ, P]),
+    'sbod_loss_pool_offset': (SZ, [I32, I32]),
+    'sbod_multibox_mine_global': (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, F32, P, I64, I64, P,
+                                        P, P, SZ, P]),
     'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),
     'sbod_scale2_inplace': (I32, [P, I64, P, I64, I32, P, P]),
     'sbod_aligned_overlap_f32': (I32, [I32, P, P, I64, P, P, P]),
@@ -62,6 +65,7 @@ REG = dict(smoothl1=0, l1=1, diou=2)
 CLS = dict(focal=0, ce=1)
 DT_F32, DT_BF16 = 0, 1
 LOSS_FOCAL_NORM = 4
+LOSS_DEFER_MINING = 64
 POOL = dict(nonpos=0, neg=8, global_neg=16, nonpos_not_easy=32)
 OV = dict(iou=0, giou=1, diou=2, ciou=3)
 FOCAL = dict(softmax=0, sigmoid=1, bce=2)

@@ -180,9 +180,13 @@ class _FusedLoss(torch.autograd.Function):
 
 
 def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, spec, threshold,
-                    neg_threshold, theta=0.01, arm_locs=None, arm_scores=None):
+                    neg_threshold, theta=0.01, arm_locs=None, arm_scores=None, exchange=None):
     """Scalar loss (autograd-enabled) of one criterion pass; also returns the device vector
-    {total, conf, loc, n_pos_total} (no sync)."""
+    {total, conf, loc, n_pos_total} (no sync).
+
+    ``exchange`` (CE with the global pool only): ``f(pool [B*P] f32) -> (pool_all, local_off)``,
+    the data-parallel exchange step — every rank's pool gathered rank-major (``allgather_pool``).
+    Mining then selects over the whole gathered batch (sbod_multibox_mine_global)."""
     locs = locs.contiguous()
     scores = scores.contiguous()
     if locs.dtype not in (torch.float32, torch.bfloat16) or scores.dtype != locs.dtype:
@@ -204,17 +208,46 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
         gs = torch.empty_like(scores) if want_grad else None
         nb = L.lib().sbod_loss_workspace_bytes(B, P)
         ws = workspace(nb, dev, 'loss')
+        flags = spec.flags | (L.LOSS_DEFER_MINING if exchange is not None else 0)
         L.call('sbod_multibox_loss', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy),
                L.ptr(arm_locs), L.ptr(arm_scores), L.ptr(gt.boxes), L.ptr(gt.labels),
                L.ptr(gt.offsets), L.ptr(obj), L.ptr(ovl), L.ptr(n_pos), L.ptr(npos_total),
-               float(threshold), float(neg_threshold), float(theta), spec.reg, spec.cls, spec.flags,
+               float(threshold), float(neg_threshold), float(theta), spec.reg, spec.cls, flags,
                int(spec.neg_pos_ratio), float(spec.reg_weight), float(spec.alpha), float(spec.gamma),
                L.ptr(gl), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
+        if exchange is not None:
+            off = L.lib().sbod_loss_pool_offset(B, P)
+            pool = ws.narrow(0, off, 4 * B * P).view(torch.float32)
+            pool_all, local_off = exchange(pool)
+            pool_all = pool_all.contiguous()
+            L.call('sbod_multibox_mine_global', L.ptr(scores), dt, B, P, C, L.ptr(npos_total), spec.reg,
+                   spec.cls, flags, int(spec.neg_pos_ratio), float(spec.reg_weight), L.ptr(pool_all),
+                   pool_all.numel(), int(local_off), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
         return out, gl, gs
 
     want = torch.is_grad_enabled() and (locs.requires_grad or scores.requires_grad)
     loss = _FusedLoss.apply(locs, scores, run, want)
     return loss, holder[0]
+
+
+def allgather_pool(group=None):
+    """The data-parallel exchange of MultiBoxLoss300's global mining pool (SSD300.py:580-588):
+    every rank's [B*P] pool gathered rank-major over RCCL (B*P*4 bytes per rank; equal B on every
+    rank, as a DistributedSampler with drop_last gives).  Returns ``f(pool) -> (pool_all,
+    local_off)`` for ``fused_criterion(exchange=...)``."""
+    import torch.distributed as dist
+
+    def exchange(pool):
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        out = torch.empty(world * pool.numel(), dtype=pool.dtype, device=pool.device)
+        try:
+            dist.all_gather_into_tensor(out, pool, group=group)
+        except (RuntimeError, NotImplementedError, AttributeError):   # backends without it (gloo)
+            parts = [torch.empty_like(pool) for _ in range(world)]
+            dist.all_gather(parts, pool, group=group)
+            out = torch.cat(parts)
+        return out, rank * pool.numel()
+    return exchange
 
 
 def allreduce_npos(n_pos, group=None):

@@ -501,13 +501,20 @@ __device__ __forceinline__ bool pool_key(float v, uint32_t &u) {
   return true;
 }
 
+// Global pool (SSD300, SSD300.py:580-588): the selection runs over n_all values of which this
+// caller owns [local_off, local_off + B*P) — the whole batch on one device (n_all = B*P,
+// local_off = 0) or, data-parallel, the rank-major concatenation of every rank's pool
+// (all-gathered by the caller), so the threshold, its tie order and k = ratio * (global
+// positives) are those of one device holding the whole batch; gradients and the returned sum
+// cover the local rows only.
 template <typename T, bool kStaged>
 __global__ __launch_bounds__(kHBlock) void k_hnm(const float *__restrict__ pool, int P, int B,
                                                  int global, const int32_t *__restrict__ npos,
                                                  int ratio, const T *__restrict__ scores,
                                                  T *__restrict__ gsc, int C,
                                                  const int32_t *__restrict__ npos_total,
-                                                 float *__restrict__ hnm_sum) {
+                                                 float *__restrict__ hnm_sum, int64_t n_all,
+                                                 int64_t local_off) {
   extern __shared__ float s_val[];
   __shared__ uint32_t s_hist[kHWaves][256];
   __shared__ uint32_t s_tot[256];
@@ -515,9 +522,10 @@ __global__ __launch_bounds__(kHBlock) void k_hnm(const float *__restrict__ pool,
   __shared__ float s_red[16];
   __shared__ int s_wcnt[kHWaves];
   const int seg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t n = global ? static_cast<int64_t>(B) * P : P;
+  const int64_t n = global ? n_all : P;
   const int64_t base = global ? 0 : static_cast<int64_t>(seg) * P;
-  const int64_t k = static_cast<int64_t>(ratio) * (global ? npos[B] : npos[seg]);
+  const int64_t n_local = static_cast<int64_t>(B) * P;
+  const int64_t k = static_cast<int64_t>(ratio) * (global ? *npos_total : npos[seg]);
   const float *src = pool + base;
   if (kStaged) {
     for (int64_t i = tid; i < n; i += kHBlock) s_val[i] = src[i];
@@ -599,10 +607,10 @@ __global__ __launch_bounds__(kHBlock) void k_hnm(const float *__restrict__ pool,
       running += tot;
       __syncthreads();
     }
-    if (sel) {
+    const int64_t r = global ? i - local_off : base + i;   // row in this caller's batch
+    if (sel && r >= 0 && r < n_local) {
       sum += val(i);
       if (gsc) {
-        const int64_t r = base + i;
         const T *z = scores + r * C;
         float m = ldf(z);
         for (int q = 1; q < C; ++q) m = fmaxf(m, ldf(z + q));
@@ -760,6 +768,40 @@ LossWs carve(void *w, int B, int P) {
   r.bytes = o;
   return r;
 }
+// Hard-negative mining (CE) and the loss finaliser, after the fused pass: per-image pools, or
+// the global pool over `n_all` gathered values of which this caller owns [local_off, +B*P).
+int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const int32_t *n_pos,
+                    const int32_t *npos_total, int reg, int cls, int flags, int neg_pos_ratio,
+                    float reg_weight, const float *pool, int64_t n_all, int64_t local_off,
+                    void *grad_scores, float *loss_out, const LossWs &ws, hipStream_t s) {
+  const int nblk = B * ((P + kLTile - 1) / kLTile);
+  int nseg = 0;
+  if (cls == SBOD_CLS_CE) {
+    const int global = (flags & SBOD_POOL_GLOBAL_NEG) ? 1 : 0;
+    nseg = global ? 1 : B;
+    const int64_t segn = global ? n_all : P;
+    const bool staged = segn <= kHStage;
+    const size_t hl = staged ? segn * sizeof(float) : 0;
+#define SBOD_HNM(T, ST)                                                                         \
+  do {                                                                                          \
+    KernelTimer kt("k_hnm", s);                                                                 \
+    hipLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, pool, P, B, global,    \
+                       n_pos, neg_pos_ratio, static_cast<const T *>(scores), static_cast<T *>(grad_scores), C, \
+                       npos_total, ws.hnm, n_all, local_off);                                   \
+  } while (0)
+    if (dtype == SBOD_DT_F32) {
+      if (staged) SBOD_HNM(float, true); else SBOD_HNM(float, false);
+    } else {
+      if (staged) SBOD_HNM(uint16_t, true); else SBOD_HNM(uint16_t, false);
+    }
+#undef SBOD_HNM
+    SBOD_LAUNCHED("k_hnm");
+  }
+  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(256), 0, s, ws.partials, nblk, ws.hnm, nseg, npos_total, reg,
+                     cls, flags, reg_weight, loss_out);
+  SBOD_LAUNCHED("k_loss_final");
+  return SBOD_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -783,6 +825,8 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   SBOD_REQUIRE(C * kLTile * 4 <= 160 * 1024, "sbod_multibox_loss: C=%d too large for one LDS tile", C);
   const bool odm = (flags & SBOD_MATCH_ODM) != 0;
   SBOD_REQUIRE(!odm || (odm_arm_locs && arm_scores), "sbod_multibox_loss: ODM needs ARM locs/scores");
+  SBOD_REQUIRE(!(flags & SBOD_LOSS_DEFER_MINING) || (cls == SBOD_CLS_CE && (flags & SBOD_POOL_GLOBAL_NEG)),
+               "sbod_multibox_loss: DEFER_MINING applies to the CE global pool only");
   LossWs ws = carve(workspace, B, P);
   if (workspace_bytes < ws.bytes) {
     set_error("sbod_multibox_loss: workspace %zu < %zu", workspace_bytes, ws.bytes);
@@ -822,33 +866,38 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
 #undef SBOD_MB
   }
   SBOD_LAUNCHED("k_multibox");
-  int nseg = 0;
-  if (cls == SBOD_CLS_CE) {
-    const int global = (flags & SBOD_POOL_GLOBAL_NEG) ? 1 : 0;
-    nseg = global ? 1 : B;
-    const int64_t segn = global ? static_cast<int64_t>(B) * P : P;
-    const bool staged = segn <= kHStage;
-    const size_t hl = staged ? segn * sizeof(float) : 0;
-#define SBOD_HNM(T, ST)                                                                         \
-  do {                                                                                          \
-    KernelTimer kt("k_hnm", s);                                                                 \
-    hipLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, ws.pool, P, B, global,  \
-                       n_pos, neg_pos_ratio, static_cast<const T *>(scores), static_cast<T *>(grad_scores), C, \
-                       npos_total, ws.hnm);                                                     \
-  } while (0)
-    if (dtype == SBOD_DT_F32) {
-      if (staged) SBOD_HNM(float, true); else SBOD_HNM(float, false);
-    } else {
-      if (staged) SBOD_HNM(uint16_t, true); else SBOD_HNM(uint16_t, false);
-    }
-#undef SBOD_HNM
-    SBOD_LAUNCHED("k_hnm");
+  if (flags & SBOD_LOSS_DEFER_MINING) return SBOD_OK;   // the caller exchanges the pool first
+  return mine_and_finish(scores, dtype, B, P, C, n_pos, npos_total, reg, cls, flags, neg_pos_ratio,
+                         reg_weight, ws.pool, static_cast<int64_t>(B) * P, 0, grad_scores, loss_out, ws, s);
+}
+
+size_t sbod_loss_pool_offset(int B, int P) {
+  LossWs ws = carve(nullptr, B, P);
+  return static_cast<size_t>(reinterpret_cast<uintptr_t>(ws.pool));
+}
+
+int sbod_multibox_mine_global(const void *scores, int dtype, int B, int P, int C,
+                              const int32_t *npos_total, int reg, int cls, int flags,
+                              int neg_pos_ratio, float reg_weight, const float *pool_all,
+                              int64_t n_all, int64_t local_off, void *grad_scores,
+                              float *loss_out, void *workspace, size_t workspace_bytes,
+                              void *stream) {
+  SBOD_REQUIRE(B > 0 && P > 0 && C >= 2 && scores && npos_total && pool_all && loss_out,
+               "sbod_multibox_mine_global: bad arguments (B=%d P=%d C=%d)", B, P, C);
+  SBOD_REQUIRE(cls == SBOD_CLS_CE && (flags & SBOD_POOL_GLOBAL_NEG),
+               "sbod_multibox_mine_global: only the CE global pool (SSD300) is mined across ranks");
+  SBOD_REQUIRE(local_off >= 0 && local_off + static_cast<int64_t>(B) * P <= n_all,
+               "sbod_multibox_mine_global: rows [%lld, %lld) outside the gathered pool of %lld",
+               static_cast<long long>(local_off), static_cast<long long>(local_off + static_cast<int64_t>(B) * P),
+               static_cast<long long>(n_all));
+  SBOD_REQUIRE(dtype == SBOD_DT_F32 || dtype == SBOD_DT_BF16, "sbod_multibox_mine_global: dtype %d", dtype);
+  LossWs ws = carve(workspace, B, P);
+  if (workspace_bytes < ws.bytes) {
+    set_error("sbod_multibox_mine_global: workspace %zu < %zu", workspace_bytes, ws.bytes);
+    return SBOD_E_WORKSPACE;
   }
-  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(256), 0, s, ws.partials,
-                     static_cast<int>(grid.x * grid.y), ws.hnm, nseg, npos_total, reg, cls, flags,
-                     reg_weight, loss_out);
-  SBOD_LAUNCHED("k_loss_final");
-  return SBOD_OK;
+  return mine_and_finish(scores, dtype, B, P, C, nullptr, npos_total, reg, cls, flags, neg_pos_ratio,
+                         reg_weight, pool_all, n_all, local_off, grad_scores, loss_out, ws, as_stream(stream));
 }
 
 int sbod_aligned_overlap_f32(int kind, const float *b1, const float *b2, int64_t n,

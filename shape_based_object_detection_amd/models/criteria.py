@@ -74,10 +74,6 @@ class _AnchorCriterion(nn.Module):
             cls = L.CLS['ce']
             flags = {'ssd512': L.POOL['nonpos'], 'ssd300': L.POOL['global_neg'],
                      'retina': L.POOL['neg']}[self.KIND]
-            if self.KIND == 'ssd300' and self.distributed:
-                raise NotImplementedError('MultiBoxLoss300 CE mining pools negatives across the whole '
-                                          'batch (SSD300.py:580-588); a cross-rank top-k is not '
-                                          'implemented — use focal loss or one rank')
         return core.CriterionSpec(reg, cls, flags, self.neg_pos_ratio, float(self.alpha))
 
     def forward(self, predicted_locs, predicted_scores, boxes, labels):
@@ -89,9 +85,13 @@ class _AnchorCriterion(nn.Module):
         gt = core.pack_gt(boxes, labels)
         obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold)
         tot = core.allreduce_npos(npos, self.process_group) if self.distributed else npos[B:]
+        spec = self._spec()
+        # SSD300's CE mines over the whole batch: data-parallel, the pools are exchanged
+        exchange = (core.allgather_pool(self.process_group)
+                    if self.distributed and (spec.flags & L.POOL['global_neg']) else None)
         loss, comps = core.fused_criterion(predicted_locs, predicted_scores, gt, obj, ovl, npos, tot,
-                                           self.priors_cxcy, self._spec(), self.threshold,
-                                           self.threshold - 0.1)
+                                           self.priors_cxcy, spec, self.threshold,
+                                           self.threshold - 0.1, exchange=exchange)
         self.last_components = comps
         return loss
 

@@ -72,9 +72,8 @@ def test_criterion_specs_follow_reference(cls, reg, clsl, exp_reg, exp_cls, exp_
     c.increase_threshold()
     assert abs(c.threshold - 0.6) < 1e-12
     if cls is CR.MultiBoxLoss300 and clsl == 'ce':
-        c.distributed = True
-        with pytest.raises(NotImplementedError):
-            c._spec()
+        c.distributed = True   # global mining across ranks: same spec, pools exchanged per call
+        assert c._spec().flags == exp_flags
 
 
 def test_criterion_entry_names():

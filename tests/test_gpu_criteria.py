@@ -134,3 +134,54 @@ def test_bf16_inputs_close_to_fp32():
     assert lo16.grad.dtype == torch.bfloat16
     l32 = crit(lo16.detach().float(), sc16.detach().float(), bx, lb)
     np.testing.assert_allclose(l16.item(), l32.item(), rtol=1e-4)
+
+
+def test_ssd300_global_mining_sharded_equals_full_batch():
+    """Data-parallel MultiBoxLoss300 CE through the HIP ABI, two 'ranks' emulated in one process:
+    each shard runs the fused pass with deferred mining, the pools are concatenated rank-major
+    (what core.allgather_pool does over RCCL) and each shard mines its rows of the global top-k
+    (sbod_multibox_mine_global).  Sum of shard losses and concatenated gradients must equal the
+    single-call full batch."""
+    from shape_based_object_detection_amd import core
+    P = torch.from_numpy(prior_table('SSD300')).to(DEV)
+    B, C = 8, 21
+    boxes, labels = synth.make_gt(B, seed=12)
+    locs, scores = synth.make_preds(B, P.shape[0], C, seed=12)
+    bx, lb = [b.to(DEV) for b in boxes], [l.to(DEV) for l in labels]
+    cfg = Cfg(reg_weights=1.0, device=DEV, n_classes=C, reg_loss='l1', cls_loss='ce')
+    crit = CR.MultiBoxLoss300(priors_cxcy=P, config=cfg)
+    lo = locs.to(DEV).requires_grad_(True)
+    sc = scores.to(DEV).requires_grad_(True)
+    full = crit(lo, sc, bx, lb)
+    full.backward()
+    spec = crit._spec()
+    halves = [slice(0, B // 2), slice(B // 2, B)]
+    gts = [core.pack_gt(bx[h], lb[h]) for h in halves]
+    m = [core.match(g, crit.priors_xy, P.shape[0], crit.threshold) for g in gts]
+    tot = (m[0][2][-1:] + m[1][2][-1:]).contiguous()          # all-reduced positives
+    pools = {}
+
+    def capture(i):
+        def ex(pool):
+            pools[i] = pool.clone()
+            return pool, 0
+        return ex
+    for i, h in enumerate(halves):                            # each rank's pool (exchange step)
+        with torch.no_grad():
+            core.fused_criterion(locs[h].to(DEV), scores[h].to(DEV), gts[i], *m[i], tot, P, spec,
+                                 crit.threshold, crit.threshold - 0.1, exchange=capture(i))
+    pool_all = torch.cat([pools[0], pools[1]])
+    total, gls, gss = 0.0, [], []
+    for i, h in enumerate(halves):
+        l_i = locs[h].to(DEV).requires_grad_(True)
+        s_i = scores[h].to(DEV).requires_grad_(True)
+        loss, _ = core.fused_criterion(l_i, s_i, gts[i], *m[i], tot, P, spec, crit.threshold,
+                                       crit.threshold - 0.1,
+                                       exchange=lambda p, i=i: (pool_all, i * pools[0].numel()))
+        loss.backward()
+        total += loss.item()
+        gls.append(l_i.grad.cpu().numpy())
+        gss.append(s_i.grad.cpu().numpy())
+    np.testing.assert_allclose(total, full.item(), rtol=1e-5)
+    np.testing.assert_allclose(np.concatenate(gls), lo.grad.cpu().numpy(), rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(np.concatenate(gss), sc.grad.cpu().numpy(), rtol=1e-5, atol=1e-9)
