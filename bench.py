@@ -6,8 +6,11 @@ One step = one pass of the hot path over one batch of SSD512 synthetic input res
   1. MultiBoxLoss512 (DIoU box loss + softmax focal, the configs[1] losses) forward AND
      backward through the drop-in criterion: ground-truth packing, the HIP matcher, the fused
      loss+gradient pass, and the upstream-gradient application;
-  2. models.utils.detect on the same batch (softmax, offset decode + clamp, per-class NMS at
-     IoU 0.45, min_score 0.01, top_k 200), whose per-image lists need one device->host sync.
+  2. detect on the same batch (softmax, offset decode + clamp, per-class NMS at IoU 0.45,
+     min_score 0.01, top_k 200 — models.utils.detect's work), whose per-image lists need one
+     device->host sync.  Its kernels are queued between the criterion's forward and backward
+     (core.detect(async_=True)) so they run under the backward's host work; the lists are
+     collected at the end of the step.  --sync-detect: models.utils.detect after the backward.
 Per-GPU batch is fixed (weak scaling); with N > 1 every rank owns its images and the loss
 normaliser (batch positives) is SUM-all-reduced over RCCL each step, as data-parallel training
 needs for exact single-device parity.
@@ -26,7 +29,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 from shape_based_object_detection_amd import _lib as L  # noqa: E402
-from shape_based_object_detection_amd import synth  # noqa: E402
+from shape_based_object_detection_amd import core, synth  # noqa: E402
 from shape_based_object_detection_amd.models import criteria as CR  # noqa: E402
 from shape_based_object_detection_amd.models import utils as MU  # noqa: E402
 from shape_based_object_detection_amd.models.priors import prior_table  # noqa: E402
@@ -48,6 +51,9 @@ def parse():
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample-images', type=int, default=2)
+    ap.add_argument('--sync-detect', action='store_true',
+                    help='run detect after the backward, synchronously (no overlap of its kernels '
+                         'with the backward host work)')
     return ap.parse_args()
 
 
@@ -149,20 +155,35 @@ def main():
     boxes, labels, locs0, scores0, det_scores = make_batch(B, 1000 * rank, dev)
     locs = locs0.clone().requires_grad_(True)
     scores = scores0.clone().requires_grad_(True)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     loss_ms = []
 
     def step(record=False):
+        # criterion forward; detect's kernels queued (core.detect async: the same work as
+        # models.utils.detect, whose lists are collected at the end of the step); backward —
+        # its host work overlaps the detect kernels; then the per-image detection lists
         locs.grad = None
         scores.grad = None
         if record:
             ev[0].record()
         loss = crit(locs, scores, boxes, labels)
-        loss.backward()
         if record:
             ev[1].record()
-        det = MU.detect(locs.detach(), det_scores, 0.01, 0.45, 200, priors, cfg)
-        return loss, det
+        if a.sync_detect:
+            if record:
+                ev[2].record()
+            loss.backward()
+            if record:
+                ev[3].record()
+            return loss, MU.detect(locs.detach(), det_scores, 0.01, 0.45, 200, priors, cfg)
+        h = core.detect(locs.detach(), det_scores, 0.01, 0.45, 200, priors, box_type='offset',
+                        act='softmax', async_=True)
+        if record:
+            ev[2].record()
+        loss.backward()
+        if record:
+            ev[3].record()
+        return loss, h.wait()
 
     # workload constants for the algorithmic byte counts (computed before any timing)
     with torch.no_grad():
@@ -191,8 +212,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(record=True)
-        loss_ms.append((ev[0], ev[1]))
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        loss_ms.append(tuple(ev))
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -204,7 +225,7 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    crit_ms = sorted(s.elapsed_time(e) for s, e in loss_ms)
+    crit_ms = sorted(e0.elapsed_time(e1) + e2.elapsed_time(e3) for e0, e1, e2, e3 in loss_ms)
     crit_ms_med = crit_ms[len(crit_ms) // 2]
     if rank != 0:
         if dist:
@@ -220,7 +241,8 @@ def main():
         'warmup': a.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
         'config': {'workload': 'SSD512 per-GPU batch %d: MultiBoxLoss512(DIoU+focal) fwd+bwd + '
-                               'detect(min_score 0.01, iou 0.45, top_k 200)' % B,
+                               'detect(min_score 0.01, iou 0.45, top_k 200)%s'
+                               % (B, '' if a.sync_detect else ', detect kernels overlapped with the backward'),
                    'global_batch': world * B, 'n_priors': P, 'n_classes': N_CLASSES,
                    'parallelism': 'dp%d' % world},
         'manchors_per_sec': round(world * B * P * a.steps / elapsed / 1e6, 3),

@@ -262,10 +262,77 @@ def allreduce_npos(n_pos, group=None):
 
 
 # ----------------------------------------------------------------------------- detection
+class DetectHandle:
+    """An in-flight ``detect``: the kernels are queued on the stream and the per-image counts are
+    copied to pinned host memory behind an event.  ``wait()`` blocks on that event only (work
+    queued after the detect — e.g. a training backward — keeps running) and returns the lists
+    ``detect`` returns.  The inputs must stay alive and unmodified until ``wait()``."""
+
+    __slots__ = ('_args', '_out', '_cnt_host', '_event', '_full', '_res', '_window', '_launch', '_slot_key')
+
+    def __init__(self, args, out, cnt_host, event, full, window):
+        self._args, self._out, self._cnt_host, self._event = args, out, cnt_host, event
+        self._full, self._res, self._window = full, None, window
+
+    def wait(self):
+        if self._res is not None:
+            return self._res
+        lc, locs, sc, B, top_k, in_place, debug = self._args
+        out_b, out_l, out_s, cnt, dbg_p, dbg_b = self._out
+        self._event.synchronize()
+        counts = self._cnt_host.tolist()
+        _COUNT_SLOTS.setdefault(self._slot_key, []).append((self._cnt_host, self._event))
+        if min(counts) < 0:   # rare: some image needs the full candidate window (exactness)
+            _detect_launch(*self._launch_args(4096))
+            counts = cnt.cpu().tolist()
+            if min(counts) < 0:
+                raise L.SbodError('detect: a per-class candidate window of 4096 is not enough to decide '
+                                  'the top-%d outputs exactly (pathological suppression); unsupported'
+                                  % top_k)
+        if in_place and lc is not locs:
+            locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
+        if min(counts) == top_k:     # every image full (the usual eval case)
+            res = self._full
+        else:
+            sizes = []
+            for n in counts:
+                sizes += [n, top_k - n]
+            res = (list(out_b.view(B * top_k, 4).split(sizes)[0::2]),
+                   list(out_l.view(-1).split(sizes)[0::2]), list(out_s.view(-1).split(sizes)[0::2]))
+        self._res = (res, dbg_p, dbg_b) if debug else res
+        return self._res
+
+    def _launch_args(self, window):
+        return self._launch + (window,)
+
+
+_COUNT_SLOTS = {}
+
+
+def _count_slot(dev, B):
+    """A free (pinned count buffer, event) pair for a detect of batch B on ``dev``; returned to
+    the pool by DetectHandle.wait().  Several handles in flight get separate pairs."""
+    free = _COUNT_SLOTS.get((dev, B))
+    if free:
+        return free.pop()
+    return torch.empty(B, dtype=torch.int32, pin_memory=True), torch.cuda.Event()
+
+
+def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn, out,
+                   dbg, ws, nb, window):
+    out_b, out_l, out_s, cnt = out
+    L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
+           L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(window), L.ptr(out_b),
+           L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg[0]), L.ptr(dbg[1]), L.ptr(ws), nb,
+           L.stream_of(sc))
+
+
 def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='offset',
-           act='softmax', pos_mask=None, final_nms=None, debug=False, window=0):
+           act='softmax', pos_mask=None, final_nms=None, debug=False, window=0, async_=False):
     """Batched decode + per-class NMS + top-k.  Returns (boxes, labels, scores) lists of per-image
-    tensors (views of batched device outputs).  ONE host sync: the per-image counts."""
+    tensors (views of batched device outputs).  ONE host sync: the per-image counts (waited on
+    through an event).  ``async_=True`` returns a ``DetectHandle`` instead (``.wait()`` gives the
+    lists), so a caller can overlap the detect kernels with later host work."""
     L.require_device(locs, scores, what='detect')
     B, P, C = scores.shape
     if top_k <= 0:
@@ -274,8 +341,6 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     sc = scores.contiguous().float()
     in_place = box_type not in ('offset', 'center')
     lc = locs if (locs.is_contiguous() and locs.dtype == torch.float32) else locs.contiguous().float()
-    if not in_place and lc is locs:
-        pass  # offset/center decode never writes the caller's tensor
     pri = priors_cxcy.contiguous().float() if priors_cxcy is not None else None
     pm = pos_mask.contiguous().to(torch.uint8) if pos_mask is not None else None
     out_b = torch.empty(B, top_k, 4, dtype=torch.float32, device=dev)
@@ -287,35 +352,22 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     nb = L.lib().sbod_detect_workspace_bytes(B, P, C)
     ws = workspace(nb, dev, 'detect')
     fn = -1.0 if final_nms is None else float(final_nms)
-    full = None
-    for w in (window, 4096):
-        L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
-               L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(w), L.ptr(out_b),
-               L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg_p), L.ptr(dbg_b), L.ptr(ws), nb,
-               L.stream_of(sc))
-        if full is None:
-            # the per-image views for the usual all-full case are built while the kernels run
-            # (host work overlapped with the device); discarded if some image has fewer
-            full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
-        counts = cnt.cpu().tolist()
-        if min(counts) >= 0:
-            break
-    else:
-        raise L.SbodError('detect: a per-class candidate window of 4096 is not enough to decide the '
-                          'top-%d outputs exactly (pathological suppression); unsupported' % top_k)
-    if in_place and lc is not locs:
-        locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
-    if min(counts) == top_k:     # every image full (the usual eval case)
-        res = full
-    else:
-        sizes = []
-        for n in counts:
-            sizes += [n, top_k - n]
-        res = (list(out_b.view(B * top_k, 4).split(sizes)[0::2]),
-               list(out_l.view(-1).split(sizes)[0::2]), list(out_s.view(-1).split(sizes)[0::2]))
-    if debug:
-        return res, dbg_p, dbg_b
-    return res
+    launch = (lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn,
+              (out_b, out_l, out_s, cnt), (dbg_p, dbg_b), ws, nb)
+    _detect_launch(*launch, window)
+    # counts -> pinned host memory behind an event, both cached per (device, B): a pinned
+    # allocation per call goes through hipHostMalloc / the host allocator's event bookkeeping and
+    # stalls the launching thread for the whole queue
+    cnt_host, ev = _count_slot(dev, B)
+    cnt_host.copy_(cnt, non_blocking=True)
+    ev.record(torch.cuda.current_stream(dev))
+    # the per-image views for the usual all-full case are built while the kernels run
+    full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
+    h = DetectHandle((lc, locs, sc, B, top_k, in_place, debug), (out_b, out_l, out_s, cnt, dbg_p, dbg_b),
+                     cnt_host, ev, full, window)
+    h._launch = launch
+    h._slot_key = (dev, B)
+    return h if async_ else h.wait()
 
 
 def nms(boxes, scores, overlap, top_k=0, variant='tv', beta1=1.0):

@@ -51,14 +51,11 @@ __device__ __forceinline__ void tile_load(float *__restrict__ dst, const uint16_
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) r[k] = s4[min(base + k * nt + static_cast<int>(threadIdx.x), n4 - 1)];
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        const int i = base + k * nt + threadIdx.x;
-        if (i < n4) {
-          dst[4 * i] = __uint_as_float(r[k].x << 16);
-          dst[4 * i + 1] = __uint_as_float(r[k].x & 0xffff0000u);
-          dst[4 * i + 2] = __uint_as_float(r[k].y << 16);
-          dst[4 * i + 3] = __uint_as_float(r[k].y & 0xffff0000u);
-        }
+      for (int k = 0; k < kBatch; ++k) {   // unguarded clamped stores: see tile_load_f32
+        const int i = min(base + k * nt + static_cast<int>(threadIdx.x), n4 - 1);
+        *reinterpret_cast<float4 *>(dst + 4 * i) =
+            make_float4(__uint_as_float(r[k].x << 16), __uint_as_float(r[k].x & 0xffff0000u),
+                        __uint_as_float(r[k].y << 16), __uint_as_float(r[k].y & 0xffff0000u));
       }
     }
     for (int i = (n4 << 2) + threadIdx.x; i < n; i += nt) dst[i] = ldf(src + i);
@@ -71,7 +68,7 @@ __device__ __forceinline__ void tile_store(float *dst, const float *src, int n) 
     const int n4 = n >> 2;
     float4 *d4 = reinterpret_cast<float4 *>(dst);
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) st4_nt(reinterpret_cast<float *>(d4 + i), s4[i]);
     for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
   } else {
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
@@ -79,6 +76,40 @@ __device__ __forceinline__ void tile_store(float *dst, const float *src, int n) 
 }
 __device__ __forceinline__ void tile_store(uint16_t *dst, const float *src, int n) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) stf(dst + i, src[i]);
+}
+
+// Score tile split into issue (loads into registers) and commit (LDS stores), so a kernel can
+// issue its per-row loads, then the tile's, then the loads that depend on the per-row values,
+// with every request in flight together.  NB vector loads per thread cover the tile when
+// n <= 4 * NB * blockDim; `fast_tile` says whether this tile qualifies (else tile_load).
+template <typename T> struct TileVec;
+template <> struct TileVec<float> { using V = float4; static constexpr int kAlign = 16; };
+template <> struct TileVec<uint16_t> { using V = uint2; static constexpr int kAlign = 8; };
+
+template <typename T, int NB>
+__device__ __forceinline__ bool fast_tile(const T *src, int n) {
+  return NB > 0 && (reinterpret_cast<uintptr_t>(src) & (TileVec<T>::kAlign - 1)) == 0 && (n & 3) == 0 &&
+         n <= 4 * NB * static_cast<int>(blockDim.x);
+}
+template <typename T, int NB>
+__device__ __forceinline__ void tile_issue(typename TileVec<T>::V (&r)[NB], const T *src, int n) {
+  const auto *s4 = reinterpret_cast<const typename TileVec<T>::V *>(src);
+  const int n4 = n >> 2;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) r[k] = s4[min(k * static_cast<int>(blockDim.x) + static_cast<int>(threadIdx.x), n4 - 1)];
+}
+__device__ __forceinline__ float4 widen4(float4 v) { return v; }
+__device__ __forceinline__ float4 widen4(uint2 v) {
+  return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                     __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+}
+template <typename V, int NB>
+__device__ __forceinline__ void tile_commit(float *dst, const V (&r)[NB], int n) {
+  const int n4 = n >> 2;
+#pragma unroll
+  for (int k = 0; k < NB; ++k)   // unguarded clamped stores (see tile_load_f32)
+    reinterpret_cast<float4 *>(dst)[min(k * static_cast<int>(blockDim.x) + static_cast<int>(threadIdx.x), n4 - 1)] =
+        widen4(r[k]);
 }
 
 struct OvOut {
@@ -273,19 +304,47 @@ __global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__r
   const int P = a.P, C = a.C;
   const int np = min(kLTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
-  tile_load(s_sc, scores + rbase * C, np * C);
+  // memory schedule: the row's matcher outputs first, then the score tile, then the loads
+  // that depend on the matcher outputs (label, GT box, and the loc / prior of rows that can
+  // be positive) — all in flight together; the tile is committed to LDS last
+  // (a tile that does not qualify for the register path is staged first, with nothing live)
+  const bool valid = tid < np;
+  const int64_t ic = rbase + (valid ? tid : 0);
+  constexpr int NB = CM / 4;
+  const T *tsrc = scores + rbase * C;
+  const bool fast = fast_tile<T, NB>(tsrc, np * C);
+  if (!fast) tile_load(s_sc, tsrc, np * C);
+  const int objv = a.obj[ic];
+  const float v = a.ovl[ic];
+  const int offb = a.off[b];
+  // every load below is unconditional (a tile that is not staged through registers loads an
+  // aligned dummy vector instead): a conditional load makes the wait-count insertion at
+  // the join assume the short path and wait for the whole batch
+  typename TileVec<T>::V tr[NB > 0 ? NB : 1];
+  if constexpr (NB > 0)   // (the workspace's partials: 256-byte aligned, whatever `scores` is)
+    tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
+  __builtin_amdgcn_sched_barrier(0);   // keep the tile's loads ahead of the dependent chain
+  const int g = offb + objv;
+  const int64_t labg = a.labels[g];
+  Box4 lc;
+  if constexpr (sizeof(T) == 4)
+    lc = ld4(reinterpret_cast<const float *>(locs) + 4 * ic);
+  else
+    lc = Box4{ldf(locs + 4 * ic), ldf(locs + 4 * ic + 1), ldf(locs + 4 * ic + 2), ldf(locs + 4 * ic + 3)};
+  const Box4 pri_cxcy = ld4(a.priors + 4 * static_cast<int64_t>(p0 + (valid ? tid : 0)));
+  const Box4 tb = ld4(a.gt + 4 * static_cast<int64_t>(g));
+  if constexpr (NB > 0)
+    if (fast) tile_commit(s_sc, tr, np * C);
   const float n = static_cast<float>(*a.npos_total);
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
   const bool grad = gsc != nullptr;
   __syncthreads();
   SEG_PHASE(1);
   float conf_l = 0.f, loc_l = 0.f;
-  if (tid < np) {
+  if (valid) {
     const int p = p0 + tid;
-    const int64_t i = rbase + tid;
-    const int g = a.off[b] + a.obj[i];
-    const float v = a.ovl[i];
-    int c = v < a.thr ? 0 : static_cast<int>(a.labels[g]);
+    const int64_t i = ic;
+    int c = v < a.thr ? 0 : static_cast<int>(labg);
     if (a.flags & SBOD_MATCH_BINARY) c = c > 0 ? 1 : 0;
     const bool negrow = v < a.nthr;
     bool easy = false;
@@ -296,6 +355,51 @@ __global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__r
       easy = e1 / (e0 + e1) < a.theta;
     }
     const bool pos = c > 0 && !easy;
+    // ---------------- box regression (first: its prologue loads die before the class row is live)
+    float gl[4] = {0.f, 0.f, 0.f, 0.f};
+    if (pos) {   // lc, pri_cxcy, tb were loaded in the prologue
+      if (a.reg == SBOD_REG_DIOU) {  // SSD512.py:579-581: IouLoss(Diou) on decoded boxes
+        const Box4 d = decode_tenfive_xy(lc, pri_cxcy);
+        const OvOut r = aligned_overlap(SBOD_OV_DIOU, d, tb, grad);
+        loc_l += 1.f - r.v;
+        if (grad) {
+          const float s = -a.reg_weight / n;
+          const float gb[4] = {r.g[0] * s, r.g[1] * s, r.g[2] * s, r.g[3] * s};
+          decode_backward(gb, lc, pri_cxcy, gl);
+        }
+      } else {  // smooth-L1 (Loss.py:213-217) or L1 on encoded targets
+        const Box4 pr = odm ? xy_to_cxcy(decode_tenfive_xy(ld4(a.arm_locs + 4 * i), pri_cxcy)) : pri_cxcy;
+        const Box4 e = encode_tenfive(xy_to_cxcy(tb), pr);
+        const float lv[4] = {lc.a, lc.b, lc.c, lc.d}, ev[4] = {e.a, e.b, e.c, e.d};
+        const bool l1 = a.reg == SBOD_REG_L1;
+        const float beta = 1.f / 9.f;
+        const float s = l1 ? a.reg_weight / (4.f * n) : a.reg_weight / n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d = lv[k] - ev[k];
+          const float x = fabsf(d);
+          const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+          if (l1) {
+            loc_l += x;
+            gl[k] = sg * s;
+          } else if (x >= beta) {
+            loc_l += x - kHalfBetaDefault;
+            gl[k] = sg * s;
+          } else {
+            loc_l += 0.5f * (x * x) / beta;
+            gl[k] = (x / beta) * sg * s;
+          }
+        }
+      }
+    }
+    if (glocs) {
+      if constexpr (sizeof(T) == 4) {
+        st4_nt(reinterpret_cast<float *>(glocs) + 4 * i, Box4{gl[0], gl[1], gl[2], gl[3]});
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
+      }
+    }
     // ---------------- classification
     float *row = s_sc + tid * C;
     if constexpr (CM > 0) {
@@ -303,8 +407,9 @@ __global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__r
       float m = -__builtin_inff(), zmin = __builtin_inff();
 #pragma unroll
       for (int k = 0; k < CM; ++k) {
-        r[k] = k < C ? row[k] : -__builtin_inff();
-        m = r[k] > m ? r[k] : m;
+        const float x = row[k < C ? k : C - 1];   // unconditional reads (no per-slot branches)
+        r[k] = k < C ? x : -__builtin_inff();
+        m = fmaxf(m, r[k]);                       // a NaN logit gives a NaN loss either way
         zmin = (k < C && r[k] < zmin) ? r[k] : zmin;
       }
       const float zt = row[c];
@@ -412,58 +517,6 @@ __global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__r
           if (grad)
             for (int k = 0; k < C; ++k) row[k] = 0.f;
         }
-      }
-    }
-    // ---------------- box regression
-    float gl[4] = {0.f, 0.f, 0.f, 0.f};
-    if (pos) {
-      Box4 lc;
-      if constexpr (sizeof(T) == 4)
-        lc = ld4(reinterpret_cast<const float *>(locs) + 4 * i);
-      else
-        lc = Box4{ldf(locs + 4 * i), ldf(locs + 4 * i + 1), ldf(locs + 4 * i + 2), ldf(locs + 4 * i + 3)};
-      const Box4 pri_cxcy = ld4(a.priors + 4 * static_cast<int64_t>(p));
-      const Box4 tb = ld4(a.gt + 4 * static_cast<int64_t>(g));
-      if (a.reg == SBOD_REG_DIOU) {  // SSD512.py:579-581: IouLoss(Diou) on decoded boxes
-        const Box4 d = decode_tenfive_xy(lc, pri_cxcy);
-        const OvOut r = aligned_overlap(SBOD_OV_DIOU, d, tb, grad);
-        loc_l += 1.f - r.v;
-        if (grad) {
-          const float s = -a.reg_weight / n;
-          const float gb[4] = {r.g[0] * s, r.g[1] * s, r.g[2] * s, r.g[3] * s};
-          decode_backward(gb, lc, pri_cxcy, gl);
-        }
-      } else {  // smooth-L1 (Loss.py:213-217) or L1 on encoded targets
-        const Box4 pr = odm ? xy_to_cxcy(decode_tenfive_xy(ld4(a.arm_locs + 4 * i), pri_cxcy)) : pri_cxcy;
-        const Box4 e = encode_tenfive(xy_to_cxcy(tb), pr);
-        const float lv[4] = {lc.a, lc.b, lc.c, lc.d}, ev[4] = {e.a, e.b, e.c, e.d};
-        const bool l1 = a.reg == SBOD_REG_L1;
-        const float beta = 1.f / 9.f;
-        const float s = l1 ? a.reg_weight / (4.f * n) : a.reg_weight / n;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float d = lv[k] - ev[k];
-          const float x = fabsf(d);
-          const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-          if (l1) {
-            loc_l += x;
-            gl[k] = sg * s;
-          } else if (x >= beta) {
-            loc_l += x - kHalfBetaDefault;
-            gl[k] = sg * s;
-          } else {
-            loc_l += 0.5f * (x * x) / beta;
-            gl[k] = (x / beta) * sg * s;
-          }
-        }
-      }
-    }
-    if (glocs) {
-      if constexpr (sizeof(T) == 4) {
-        st4(reinterpret_cast<float *>(glocs) + 4 * i, Box4{gl[0], gl[1], gl[2], gl[3]});
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
       }
     }
   }

@@ -24,6 +24,7 @@ namespace sbod {
 SBOD_STAMP_DECL
 
 constexpr int kDTile = 256;
+__device__ const uint8_t kOneByte = 1;
 constexpr int kSegThreads = 256;
 constexpr int kMaxWindow = 4096;   // LDS-resident window (keys + boxes + areas + flags)
 constexpr int kMergeThreads = 1024;
@@ -459,17 +460,23 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   long long ph[6] = {0, 0, 0, 0, 0, 0};
 #endif
   SEG_PHASE(0);
-  tile_load_f32(s_sc, scores + rbase * C, np * C);
-  __syncthreads();
-  SEG_PHASE(1);
   const bool valid = tid < np;
   const int p = p0 + tid;
   const int64_t i = rbase + tid;
+  // this prior's loc / prior / mask loads go out with the score tile's (one memory round trip)
+  const int64_t ic = valid ? i : rbase;
+  const Box4 l = ld4(locs + 4 * ic);
+  const Box4 pr = a.box_type == SBOD_BOX_OFFSET ? ld4(a.priors + 4 * static_cast<int64_t>(valid ? p : p0))
+                                                : Box4{0.f, 0.f, 0.f, 0.f};
+  const uint8_t posv = *(a.pos != nullptr ? a.pos + ic : &kOneByte);   // branch-free: no early wait
+  tile_load_f32(s_sc, scores + rbase * C, np * C);
+  __syncthreads();
+  SEG_PHASE(1);
   float *row = s_sc + tid * C;
   if (valid) {
-    Box4 l = ld4(locs + 4 * i), d;
+    Box4 d;
     if (a.box_type == SBOD_BOX_OFFSET) {
-      d = decode_tenfive_xy(l, ld4(a.priors + 4 * static_cast<int64_t>(p)));
+      d = decode_tenfive_xy(l, pr);
     } else if (a.box_type == SBOD_BOX_CENTER) {
       d = Box4{l.a - l.c / 2.f, l.b - l.d / 2.f, l.a + l.c / 2.f, l.b + l.d / 2.f};
     } else {
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     d = Box4{fminf(fmaxf(d.a, 0.f), 1.f), fminf(fmaxf(d.b, 0.f), 1.f), fminf(fmaxf(d.c, 0.f), 1.f),
              fminf(fmaxf(d.d, 0.f), 1.f)};
     if (a.box_type == SBOD_BOX_CORNER) st4(locs + 4 * i, d);  // models/utils.py:224 clamp_ in place
-    st4(a.boxes_ws + 4 * i, d);
+    st4_nt(a.boxes_ws + 4 * i, d);
     if (a.dbg_boxes) st4(a.dbg_boxes + 4 * i, d);
     if constexpr (CM == 0) {
       if (a.act == SBOD_ACT_SOFTMAX) {
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
       }
     }
   }
-  const bool allowed = valid && (a.pos == nullptr || a.pos[i] != 0);
+  const bool allowed = valid && posv != 0;
   const int wv = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
   if constexpr (CM > 0) {
@@ -505,37 +512,46 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     // registers.  Activation: exp2 / rcp hardware ops (probabilities within ~1e-6 relative of
     // torch.softmax; every later decision reads these same values, so detect stays exact w.r.t.
     // them).  Each lane then walks only ITS candidate classes (~1-2 of 20) to emit keys.
+    // the raw row stays in LDS: an emitted candidate's probability is recomputed from it with
+    // the same operations (bit-identical), so the 20 probabilities are never written back
     float r[CM];
 #pragma unroll
-    for (int k = 0; k < CM; ++k) r[k] = k < C ? row[k] : -__builtin_inff();
-    if (a.act == SBOD_ACT_SOFTMAX) {
-      float m = r[0];
+    for (int k = 0; k < CM; ++k) {
+      const float v = row[k < C ? k : C - 1];   // unconditional reads (no per-slot branches)
+      r[k] = k < C ? v : -__builtin_inff();
+    }
+    const bool softmax = a.act == SBOD_ACT_SOFTMAX;
+    float m = 0.f, rs = 1.f;
+    if (softmax) {
+      m = r[0];
 #pragma unroll
-      for (int k = 1; k < CM; ++k) m = r[k] > m ? r[k] : m;
+      for (int k = 1; k < CM; ++k) m = fmaxf(m, r[k]);   // NaN rows give NaN probabilities either way
       float sum = 0.f;
 #pragma unroll
       for (int k = 0; k < CM; ++k) {
         r[k] = fast_exp(r[k] - m);   // padding: exp(-inf) = 0
         sum += r[k];
       }
-      const float rs = __builtin_amdgcn_rcpf(sum);
+      rs = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
       for (int k = 0; k < CM; ++k) r[k] = r[k] * rs;
     } else {
 #pragma unroll
       for (int k = 0; k < CM; ++k) r[k] = fast_sigmoid(r[k]);
     }
+    if (a.dbg_probs && valid) {
+#pragma unroll
+      for (int k = 0; k < CM; ++k)
+        if (k < C) a.dbg_probs[i * C + k] = r[k];
+    }
     uint32_t cmask = 0;
 #pragma unroll
-    for (int k = 0; k < CM; ++k) {
+    for (int k = 1; k < CM; ++k) {
       if (k < C) {
-        row[k] = r[k];                         // for the emission loop and the debug copy
-        if (k >= 1) {
-          const bool take = allowed && r[k] > a.min_score;
-          const unsigned long long bal = __ballot(take);
-          if (lane == 0) s_bal(wv, k) = bal;
-          cmask |= take ? (1u << k) : 0u;
-        }
+        const bool take = allowed && r[k] > a.min_score;
+        const unsigned long long bal = __ballot(take);
+        if (lane == 0) s_bal(wv, k) = bal;
+        cmask |= take ? (1u << k) : 0u;
       }
     }
     SEG_PHASE(2);
@@ -545,8 +561,11 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
       const int c = __builtin_ctz(cmask);
       cmask &= cmask - 1u;
       const unsigned long long bal = s_bal(wv, c);
+      const float pc = softmax ? fast_exp(row[c] - m) * rs : fast_sigmoid(row[c]);
+      // (plain store: these 8-byte scattered writes must merge into full lines in L2 first —
+      // streamed through they cost 1.7x the kernel time)
       a.cand[(static_cast<int64_t>(b) * C + c) * P + s_wb(wv, c) + __popcll(bal & lt)] =
-          make_key(row[c], static_cast<uint32_t>(p));
+          make_key(pc, static_cast<uint32_t>(p));
     }
   } else {
     SEG_PHASE(2);
@@ -570,9 +589,11 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     printf("prep x%d b%d: tile %lld compute %lld ballot+atomic %lld keys %lld total %lld\n", blockIdx.x, b,
            ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3], ph[4] - ph[0]);
 #endif
-  if (a.dbg_probs) {
-    __syncthreads();
-    for (int k = tid; k < np * C; k += kDTile) a.dbg_probs[rbase * C + k] = s_sc[k];
+  if constexpr (CM == 0) {
+    if (a.dbg_probs) {
+      __syncthreads();
+      for (int k = tid; k < np * C; k += kDTile) a.dbg_probs[rbase * C + k] = s_sc[k];
+    }
   }
   STAMP_END(1, 1);
 }

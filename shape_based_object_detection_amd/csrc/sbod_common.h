@@ -160,6 +160,15 @@ __device__ __forceinline__ Box4 ld4(const float *p) {
 __device__ __forceinline__ void st4(float *p, Box4 b) {
   *reinterpret_cast<float4 *>(p) = make_float4(b.a, b.b, b.c, b.d);
 }
+// Streaming (non-temporal) stores for large one-shot outputs: written through instead of left
+// dirty in the XCD's L2, so the write-back overlaps the kernel instead of following it.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st4_nt(float *p, Box4 b) {
+  f32x4_t v = {b.a, b.b, b.c, b.d};
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4_t *>(p));
+}
+__device__ __forceinline__ void st4_nt(float *p, float4 b) { st4_nt(p, Box4{b.x, b.y, b.z, b.w}); }
+__device__ __forceinline__ void st_nt(unsigned long long *p, unsigned long long v) { __builtin_nontemporal_store(v, p); }
 
 // [n] floats global -> LDS, 16 bytes per lane when the source is 16-byte aligned.
 // Global -> LDS copy of n floats by the whole block.  Loads are issued in batches of 8 per
@@ -172,17 +181,15 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
     const int n4 = n >> 2;
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
     float4 *d4 = reinterpret_cast<float4 *>(dst);
-    // loads are unconditional (index clamped) so the batch stays in registers — a
-    // conditionally written array is demoted to scratch memory by the compiler
+    // loads AND stores are unconditional (index clamped; an out-of-range lane rewrites the last
+    // element with the value it holds): a guarded store lets the compiler sink each load into
+    // its store's branch, which serialises the batch into one memory round trip per element
     for (int base = 0; base < n4; base += kBatch * nt) {
       float4 r[kBatch];
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) r[k] = s4[min(base + k * nt + static_cast<int>(threadIdx.x), n4 - 1)];
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        const int i = base + k * nt + threadIdx.x;
-        if (i < n4) d4[i] = r[k];
-      }
+      for (int k = 0; k < kBatch; ++k) d4[min(base + k * nt + static_cast<int>(threadIdx.x), n4 - 1)] = r[k];
     }
     for (int i = (n4 << 2) + threadIdx.x; i < n; i += nt) dst[i] = src[i];
   } else {
@@ -191,10 +198,7 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
 #pragma unroll
       for (int k = 0; k < kBatch; ++k) r[k] = src[min(base + k * nt + static_cast<int>(threadIdx.x), n - 1)];
 #pragma unroll
-      for (int k = 0; k < kBatch; ++k) {
-        const int i = base + k * nt + threadIdx.x;
-        if (i < n) dst[i] = r[k];
-      }
+      for (int k = 0; k < kBatch; ++k) dst[min(base + k * nt + static_cast<int>(threadIdx.x), n - 1)] = r[k];
     }
   }
 }
