@@ -11,6 +11,7 @@ import torch  # noqa: F401  (must precede the dlopen; see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SBOD_LIB', os.path.join(_HERE, 'lib', 'libsbod_hip.so'))
+FAST_PATH = os.path.join(os.path.dirname(LIB_PATH), '_sbodcall.so')
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int
@@ -79,6 +80,7 @@ class SbodError(RuntimeError):
 
 
 _lib = None
+_fast = {}     # name -> _sbodcall wrapper (same C entry point, no ctypes argument conversion)
 MISSING = []   # declared in include/sbod.h but not exported (tests assert this is empty)
 
 
@@ -99,12 +101,35 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = L
+        _load_fast()
     return _lib
+
+
+def _load_fast():
+    """The _sbodcall extension built next to the library (build.py), if present: a CPython
+    METH_FASTCALL wrapper per entry point, calling the very same C functions.  Without it the
+    ctypes binding is used (same kernels, more host time per call)."""
+    if not os.path.exists(FAST_PATH) or os.environ.get('SBOD_NO_FASTCALL'):
+        return
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('_sbodcall', FAST_PATH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    for name in SIGNATURES:
+        f = getattr(mod, name, None)
+        if f is not None:
+            _fast[name] = f
+
+
+def fastcall_names():
+    lib()
+    return sorted(_fast)
 
 
 def call(name, *args):
     """Invoke an sbod_* entry point; raise SbodError with sbod_last_error() on failure."""
-    st = getattr(lib(), name)(*args)
+    f = _fast.get(name)
+    st = f(*args) if f is not None else getattr(lib(), name)(*args)
     if st != 0:
         msg = lib().sbod_last_error().decode(errors='replace')
         raise SbodError('%s failed (%d): %s' % (name, st, msg))

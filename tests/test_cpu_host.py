@@ -1,5 +1,6 @@
 """CPU-only checks: the C-ABI library loads and exports every declared symbol (no compute calls),
 host-side logic (criterion specs, config handling, loud rejection of CPU tensors)."""
+import ctypes
 import os
 import re
 
@@ -29,6 +30,20 @@ def test_library_exports_every_declared_symbol():
     assert L.MISSING == []
     assert lib.sbod_abi_version() == 1
     assert b'gfx950' in lib.sbod_version()
+
+
+def test_fastcall_wraps_every_launch_entry_point():
+    # _sbodcall (generated from SIGNATURES) covers every int / size_t entry point and returns
+    # what the ctypes binding returns for the same arguments
+    lib = L.lib()
+    want = sorted(n for n, (res, args) in L.SIGNATURES.items()
+                  if res in (L.I32, L.SZ) and ctypes.c_char_p not in args)
+    assert L.fastcall_names() == want
+    for n in ('sbod_loss_workspace_bytes', 'sbod_detect_workspace_bytes', 'sbod_match_workspace_bytes_p'):
+        args = (32, 10248, 21)[:len(L.SIGNATURES[n][1])]
+        assert L._fast[n](*args) == getattr(lib, n)(*args)
+    with pytest.raises(TypeError):
+        L._fast['sbod_multibox_loss'](1, 2)
 
 
 def test_invalid_arguments_return_status_not_crash():
