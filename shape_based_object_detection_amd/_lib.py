@@ -109,7 +109,10 @@ def _load_fast():
     """The _sbodcall extension built next to the library (build.py), if present: a CPython
     METH_FASTCALL wrapper per entry point, calling the very same C functions.  Without it the
     ctypes binding is used (same kernels, more host time per call)."""
-    if not os.path.exists(FAST_PATH) or os.environ.get('SBOD_NO_FASTCALL'):
+    # the extension links libsbod_hip.so by name: a variant library (SBOD_LIB=..._phase.so etc.)
+    # keeps the ctypes path so every call reaches the library that was asked for
+    if (not os.path.exists(FAST_PATH) or os.environ.get('SBOD_NO_FASTCALL')
+            or os.path.basename(LIB_PATH) != 'libsbod_hip.so'):
         return
     import importlib.util
     spec = importlib.util.spec_from_file_location('_sbodcall', FAST_PATH)

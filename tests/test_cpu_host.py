@@ -125,3 +125,8 @@ def test_no_kernel_spills_to_scratch():
     assert len(ours) >= 20
     bad = {k: v['ScratchSize'] for k, v in ours.items() if v.get('ScratchSize', 0) > 0}
     assert bad == {}, bad
+
+
+def test_stress_anchor_generator_size():
+    # SURVEY §8 C3 stress size: RetinaNet's generator on 896x896 maps
+    assert prior_table('RETINA896').shape == (100254, 4)
