@@ -51,6 +51,12 @@ const char *sbod_last_error(void);
 int sbod_timing_enable(const char *kernel_filter);
 int sbod_timing_query(const char *kernel, int *launches, double *total_ms);
 
+/* Asynchronous device -> host copy on `stream` (hipMemcpyAsync; dst_host should be pinned, e.g.
+ * torch's pin_memory buffers).  Used for detect's per-image counts (the one value the host needs
+ * from a detect call, models/utils.py:274-290); the caller orders its host read after an event
+ * recorded behind it.  Cheaper on the host than a framework-level non_blocking copy. */
+int sbod_memcpy_d2h_async(void *dst_host, const void *src_dev, size_t bytes, void *stream);
+
 /* ---------------------------------------------------------------- a1 / a4: pairwise IoU
  * Replaces metrics.find_jaccard_overlap (metrics.py:208-252; mode SBOD_IOU_METRICS: +1e-5
  * denominator, zero-GT -> 0, zero-anchor -> -1) and iou_utils.jaccard (iou_utils.py:215-233;

@@ -359,7 +359,8 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     # allocation per call goes through hipHostMalloc / the host allocator's event bookkeeping and
     # stalls the launching thread for the whole queue
     cnt_host, ev = _count_slot(dev, B)
-    cnt_host.copy_(cnt, non_blocking=True)
+    stream = L.stream_of(cnt)
+    L.call('sbod_memcpy_d2h_async', cnt_host.data_ptr(), L.ptr(cnt), 4 * B, stream)
     ev.record(torch.cuda.current_stream(dev))
     # the per-image views for the usual all-full case are built while the kernels run
     full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))

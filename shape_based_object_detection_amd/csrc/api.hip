@@ -142,6 +142,14 @@ const char *sbod_version(void) { return "sbod-hip 0.1.0 (gfx950)"; }
 int sbod_abi_version(void) { return SBOD_ABI_VERSION; }
 const char *sbod_last_error(void) { return sbod::g_err; }
 
+int sbod_memcpy_d2h_async(void *dst_host, const void *src_dev, size_t bytes, void *stream) {
+  SBOD_REQUIRE(bytes == 0 || (dst_host != nullptr && src_dev != nullptr), "sbod_memcpy_d2h_async: bad arguments");
+  if (bytes == 0) return SBOD_OK;
+  if (hipMemcpyAsync(dst_host, src_dev, bytes, hipMemcpyDeviceToHost, sbod::as_stream(stream)) != hipSuccess)
+    return sbod::launch_status("sbod_memcpy_d2h_async");
+  return SBOD_OK;
+}
+
 int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, void *stream) {
   SBOD_REQUIRE(n >= 0 && scale != nullptr, "sbod_scale_inplace: bad arguments");
   if (n == 0) return SBOD_OK;
