@@ -38,7 +38,7 @@ __device__ __forceinline__ float dmax_a(float a, float b) { return a > b ? 1.f :
 __device__ __forceinline__ float dmin_a(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }
 
 // [n] floats global <-> LDS, 16 bytes per lane when the global side is 16-byte aligned.
-__device__ __forceinline__ void tile_load(float *dst, const float *src, int n) { tile_load_f32(dst, src, n); }
+__device__ __forceinline__ void tile_load(float *dst, const float *src, int n) { tile_load_f32<>(dst, src, n); }
 // bf16 -> f32 staging, 8 requests in flight per thread before the LDS stores (see tile_load_f32)
 __device__ __forceinline__ void tile_load(float *__restrict__ dst, const uint16_t *__restrict__ src, int n) {
   constexpr int kBatch = 8;

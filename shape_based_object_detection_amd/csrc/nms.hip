@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   const Box4 pr = a.box_type == SBOD_BOX_OFFSET ? ld4(a.priors + 4 * static_cast<int64_t>(valid ? p : p0))
                                                 : Box4{0.f, 0.f, 0.f, 0.f};
   const uint8_t posv = *(a.pos != nullptr ? a.pos + ic : &kOneByte);   // branch-free: no early wait
-  tile_load_f32(s_sc, scores + rbase * C, np * C);
+  tile_load_f32<(CM > 0 ? (CM + 3) / 4 : 8)>(s_sc, scores + rbase * C, np * C);
   __syncthreads();
   SEG_PHASE(1);
   float *row = s_sc + tid * C;

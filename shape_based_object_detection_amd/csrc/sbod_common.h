@@ -174,8 +174,10 @@ __device__ __forceinline__ void st_nt(unsigned long long *p, unsigned long long 
 // Global -> LDS copy of n floats by the whole block.  Loads are issued in batches of 8 per
 // thread into registers before any LDS store, so a thread has 8 HBM requests in flight instead
 // of one round trip per element (the compiler cannot reorder loads past stores to `dst`).
+// kBatch = loads per thread per batch: a caller that knows its tile (256 rows x C <= 4 kBatch
+// floats per thread) passes the exact count, so no lane issues clamped duplicate requests.
+template <int kBatch = 8>
 __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const float *__restrict__ src, int n) {
-  constexpr int kBatch = 8;
   const int nt = blockDim.x;
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
     const int n4 = n >> 2;
