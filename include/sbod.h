@@ -50,6 +50,11 @@ const char *sbod_last_error(void);
  * and returns the number of timed launches and their summed duration in milliseconds. */
 int sbod_timing_enable(const char *kernel_filter);
 int sbod_timing_query(const char *kernel, int *launches, double *total_ms);
+/* Time only one launch in n of each selected kernel (n >= 1, default 1; resets the per-kernel
+ * launch counts).  Timed launches carry their events on the dispatch itself
+ * (hipExtLaunchKernelGGL), which costs host time per timed launch; sampling keeps that out of
+ * most steps of a benchmark. */
+int sbod_timing_every(int n);
 
 /* Asynchronous device -> host copy on `stream` (hipMemcpyAsync; dst_host should be pinned, e.g.
  * torch's pin_memory buffers).  Used for detect's per-image counts (the one value the host needs

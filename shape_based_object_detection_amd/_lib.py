@@ -51,6 +51,7 @@ SIGNATURES = {
     'sbod_map_f32': (I32, [P, P, P, P, P, P, P, P, I32, I32, I64, I64, ctypes.c_double, P, P, P, P, SZ, P]),
     'sbod_timing_enable': (I32, [ctypes.c_char_p]),
     'sbod_timing_query': (I32, [ctypes.c_char_p, P, P]),
+    'sbod_timing_every': (I32, [I32]),
     'sbod_memcpy_d2h_async': (I32, [P, P, SZ, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
     'sbod_dcn_fwd_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),

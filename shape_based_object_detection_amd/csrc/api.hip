@@ -2,6 +2,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -77,6 +78,8 @@ struct TimingRec {
   hipEvent_t a, b;
 };
 std::vector<TimingRec> g_recs;
+int g_every = 1;                                  // time one launch in g_every (per kernel name)
+std::unordered_map<std::string, long long> g_seen;
 std::vector<hipEvent_t> g_pool;
 
 hipEvent_t pooled_event() {
@@ -91,16 +94,27 @@ hipEvent_t pooled_event() {
 }
 }  // namespace
 
-KernelTimer::KernelTimer(const char *name, hipStream_t s) : name_(name), stream_(s) {
+KernelTimer::KernelTimer(const char *name, hipStream_t s, bool attached)
+    : name_(name), stream_(s), attached_(attached) {
   std::lock_guard<std::mutex> g(g_tmu);
   if (g_filter.empty() || (g_filter != "*" && g_filter != name)) return;
+  if (g_every > 1 && (g_seen[name]++ % g_every) != 0) return;
   start_ = pooled_event();
+  if (attached_) {
+    stop_ = pooled_event();
+    if (!start_ || !stop_) start_ = stop_ = nullptr;
+    return;
+  }
   if (start_ && hipEventRecord(start_, s) != hipSuccess) start_ = nullptr;
 }
 
 KernelTimer::~KernelTimer() {
   if (!start_) return;
   std::lock_guard<std::mutex> g(g_tmu);
+  if (attached_) {
+    g_recs.push_back({name_, start_, stop_});
+    return;
+  }
   hipEvent_t e = pooled_event();
   if (e && hipEventRecord(e, stream_) == hipSuccess) g_recs.push_back({name_, start_, e});
 }
@@ -116,7 +130,16 @@ int sbod_timing_enable(const char *kernel_filter) {
     sbod::g_pool.push_back(r.b);
   }
   sbod::g_recs.clear();
+  sbod::g_seen.clear();
   sbod::g_filter = kernel_filter ? kernel_filter : "";
+  return SBOD_OK;
+}
+
+int sbod_timing_every(int n) {
+  SBOD_REQUIRE(n >= 1, "sbod_timing_every: n must be >= 1");
+  std::lock_guard<std::mutex> g(sbod::g_tmu);
+  sbod::g_every = n;
+  sbod::g_seen.clear();
   return SBOD_OK;
 }
 

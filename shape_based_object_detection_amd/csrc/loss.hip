@@ -837,8 +837,8 @@ int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const in
     const size_t hl = staged ? segn * sizeof(float) : 0;
 #define SBOD_HNM(T, ST)                                                                         \
   do {                                                                                          \
-    KernelTimer kt("k_hnm", s);                                                                 \
-    hipLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, pool, P, B, global,    \
+    KernelTimer kt("k_hnm", s, true);                                                                 \
+    hipExtLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, kt.start(), kt.stop(), 0, pool, P, B, global,    \
                        n_pos, neg_pos_ratio, static_cast<const T *>(scores), static_cast<T *>(grad_scores), C, \
                        npos_total, ws.hnm, n_all, local_off);                                   \
   } while (0)
@@ -892,9 +892,9 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   dim3 grid((P + kLTile - 1) / kLTile, B);
   const size_t lds = static_cast<size_t>(kLTile) * C * sizeof(float);
   {
-    KernelTimer kt("k_multibox", s);
+    KernelTimer kt("k_multibox", s, true);
 #define SBOD_MB(T, CM, CLS)                                                                       \
-  hipLaunchKernelGGL((k_multibox<T, CM, CLS>), grid, dim3(kLTile), lds, s, a, static_cast<const T *>(locs), \
+  hipExtLaunchKernelGGL((k_multibox<T, CM, CLS>), grid, dim3(kLTile), lds, s, kt.start(), kt.stop(), 0, a, static_cast<const T *>(locs), \
                      static_cast<const T *>(scores), static_cast<T *>(grad_locs), static_cast<T *>(grad_scores))
     // rows of C <= CM classes in registers; wider rows take the LDS path
 #define SBOD_MB_C(T)                                                  \

@@ -486,15 +486,15 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
   const size_t lds = Gmax * sizeof(GtTile);
 #define SBOD_TILE(ODM, FL)                                                                      \
   do {                                                                                          \
-    KernelTimer kt("k_match_tile", s);                                                          \
-    hipLaunchKernelGGL((k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, gt_boxes, gt_labels,   \
+    KernelTimer kt("k_match_tile", s, true);                                                          \
+    hipExtLaunchKernelGGL((k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, kt.start(), kt.stop(), 0, gt_boxes, gt_labels,   \
                        gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, \
                        ovl, w.part, w.tcount, n_pos, B);                                        \
   } while (0)
 #define SBOD_FINAL(FL)                                                                          \
   do {                                                                                          \
-    KernelTimer kt("k_match_final", s);                                                         \
-    hipLaunchKernelGGL((k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, gt_labels, gt_offsets, \
+    KernelTimer kt("k_match_final", s, true);                                                         \
+    hipExtLaunchKernelGGL((k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, kt.start(), kt.stop(), 0, gt_labels, gt_offsets, \
                        w.part, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B); \
   } while (0)
   if (odm) {

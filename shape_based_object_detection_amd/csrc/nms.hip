@@ -1880,30 +1880,30 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.boxes, ws.cand, ws.count,
             debug_probs, debug_boxes};
   {
-    KernelTimer kt("k_det_prepare", s);
+    KernelTimer kt("k_det_prepare", s, true);
     const dim3 pg((P + kDTile - 1) / kDTile, B);
     const size_t pl = static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12;
-    if (C <= 8) hipLaunchKernelGGL(k_det_prepare<8>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 16) hipLaunchKernelGGL(k_det_prepare<16>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 24) hipLaunchKernelGGL(k_det_prepare<24>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 32) hipLaunchKernelGGL(k_det_prepare<32>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else hipLaunchKernelGGL(k_det_prepare<0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
-                       static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, locs, scores);
+    if (C <= 8) hipExtLaunchKernelGGL(k_det_prepare<8>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
+    else if (C <= 16) hipExtLaunchKernelGGL(k_det_prepare<16>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
+    else if (C <= 24) hipExtLaunchKernelGGL(k_det_prepare<24>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
+    else if (C <= 32) hipExtLaunchKernelGGL(k_det_prepare<32>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
+    else hipExtLaunchKernelGGL(k_det_prepare<0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
+                       static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, kt.start(), kt.stop(), 0, a, locs, scores);
   }
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
   {
-    KernelTimer kt("k_det_segment", s);
+    KernelTimer kt("k_det_segment", s, true);
     if (w1 <= 64)
 #ifdef SBOD_SEG_WAVE
-      hipLaunchKernelGGL(k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, ws.boxes,
+      hipExtLaunchKernelGGL(k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, kt.start(), kt.stop(), 0, ws.cand, ws.count, ws.boxes,
                          P, C, w1, w2, max_overlap, so, nullptr);
 #else
-      hipLaunchKernelGGL(k_det_segment_w4, dim3(C - 1, B), dim3(64 * kSegW), 0, s, ws.cand, ws.count, ws.boxes,
+      hipExtLaunchKernelGGL(k_det_segment_w4, dim3(C - 1, B), dim3(64 * kSegW), 0, s, kt.start(), kt.stop(), 0, ws.cand, ws.count, ws.boxes,
                          P, C, w1, w2, max_overlap, so);
 #endif
     else
-      hipLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
+      hipExtLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, kt.start(), kt.stop(), 0, ws.cand,
                          ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
   }
   SBOD_LAUNCHED("k_det_segment");
@@ -1911,8 +1911,8 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     // two-pass mode: the second pass runs inline in the merge blocks of undecidable images,
     // so the merge's dynamic LDS also covers one segment with window w2
     const size_t seg2 = two ? inline2_lds(w2) : 0;
-    KernelTimer kt("k_det_merge", s);
-    hipLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, ws.kept,
+    KernelTimer kt("k_det_merge", s, true);
+    hipExtLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, kt.start(), kt.stop(), 0, ws.kept,
                        ws.kc, ws.lastkey, ws.boxes, P, C, w2, w1, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
                        ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, ws.cand, ws.count,
                        max_overlap, so);

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -38,17 +39,24 @@ constexpr float kIouEps = 1e-5f;  // metrics.py:233 EPS (compared as float32, li
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 // Brackets a launch with HIP events on its stream when sbod_timing_enable() selected it.
+// With `attached` the scope's launch carries the two events itself (hipExtLaunchKernelGGL(...,
+// kt.start(), kt.stop(), 0, ...)): the runtime stamps them at the dispatch's own start and end, so
+// the measured time is the kernel's, without the gap between a separately recorded event and
+// the dispatch.  Without it the events are recorded around the scope's launches.
 class KernelTimer {
  public:
-  KernelTimer(const char *name, hipStream_t s);
+  KernelTimer(const char *name, hipStream_t s, bool attached = false);
   ~KernelTimer();
   KernelTimer(const KernelTimer &) = delete;
   KernelTimer &operator=(const KernelTimer &) = delete;
+  hipEvent_t start() const { return attached_ ? start_ : nullptr; }
+  hipEvent_t stop() const { return attached_ ? stop_ : nullptr; }
 
  private:
   const char *name_;
   hipStream_t stream_;
-  hipEvent_t start_ = nullptr;
+  bool attached_;
+  hipEvent_t start_ = nullptr, stop_ = nullptr;
 };
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
