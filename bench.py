@@ -3,19 +3,29 @@
 
 One step = one pass of the hot path over one batch of SSD512 synthetic input resident in HBM
 (SURVEY §8(d) recipe; BASELINE.json metric "images/sec train step SSD512 batch=32"):
-  1. MultiBoxLoss512 (DIoU box loss + softmax focal, the configs[1] losses) forward AND
-     backward through the drop-in criterion: ground-truth packing, the HIP matcher, the fused
-     loss+gradient pass, and the upstream-gradient application;
-  2. detect on the same batch (softmax, offset decode + clamp, per-class NMS at IoU 0.45,
-     min_score 0.01, top_k 200 — models.utils.detect's work), whose per-image lists need one
-     device->host sync.  Its kernels are queued between the criterion's forward and backward
-     (core.detect(async_=True)) so they run under the backward's host work; the lists are
-     collected at the end of the step.  --sync-detect: models.utils.detect after the backward.
-Per-GPU batch is fixed (weak scaling); with N > 1 every rank owns its images and the loss
-normaliser (batch positives) is SUM-all-reduced over RCCL each step, as data-parallel training
-needs for exact single-device parity.
+  1. ground-truth packing of the per-image lists into fixed-capacity device buffers (one
+     sbod_gt_pack launch; SURVEY §8(f) row 1);
+  2. MultiBoxLoss512 (DIoU box loss + softmax focal, the configs[1] losses) forward AND
+     backward through the drop-in criterion: the HIP matcher, the fused loss+gradient pass and
+     the upstream-gradient application;
+  3. detect on the same batch (softmax, offset decode + clamp, per-class NMS at IoU 0.45,
+     min_score 0.01, top_k 200 — models.utils.detect's work) up to its per-image lists, which
+     need one device->host sync.
+Steps 2-3 are captured once into a hipGraph (torch.cuda.graph over the same eager calls, one
+stream) and replayed every step.  Every kernel still runs every step; the graph removes the
+per-launch host work.  ``--eager`` runs the same calls without the graph; the line also carries
+the eager step time (measured before the capture).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--no-cpu-baseline]
+Data parallel (``--gpus N``): one process per GPU.  Without WORLD_SIZE in the environment this
+script starts the N rank processes itself (subprocesses, before any GPU call); under
+torch.distributed.run it is one of them.  Per-GPU batch is fixed (weak scaling).  The hot path's
+exchange is the SUM all-reduce of the batch positive count (the loss normaliser), inside the
+graph.  Reported beside the hot-path value: the same step with the SSD512-sized gradient
+all-reduce of data-parallel training (26,450,959 fp32 values), bucketed on its own
+RCCL communicator and overlapped with the step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--eager]
+                    [--no-cpu-baseline] [--no-dcn]
 """
 import argparse
 import json
@@ -31,30 +41,32 @@ sys.path.insert(0, HERE)
 from shape_based_object_detection_amd import _lib as L  # noqa: E402
 from shape_based_object_detection_amd import core, synth  # noqa: E402
 from shape_based_object_detection_amd.models import criteria as CR  # noqa: E402
-from shape_based_object_detection_amd.models import utils as MU  # noqa: E402
 from shape_based_object_detection_amd.models.priors import prior_table  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+F32_MFMA_PEAK_TFS = 157.3  # dense fp32 MFMA (MI355X_MICROARCH.md)
 N_CLASSES = 21
 ARCH = 'SSD512'
+SSD512_PARAMS = 26450959   # SSD512 parameter count -> fp32 gradient elements
+BUCKET_MB = 25             # DDP's default bucket size
+TIMING_EVERY = 10          # one step in 10 carries the dominant kernel's timing
 
 
 class Cfg(dict):
     __getattr__ = dict.__getitem__
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--eager', action='store_true', help='no hipGraph: launch every call each step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-sample-images', type=int, default=2)
-    ap.add_argument('--sync-detect', action='store_true',
-                    help='run detect after the backward, synchronously (no overlap of its kernels '
-                         'with the backward host work)')
-    return ap.parse_args()
+    ap.add_argument('--no-dcn', action='store_true')
+    ap.add_argument('--cpu-detect-images', type=int, default=2)
+    return ap.parse_args(argv)
 
 
 def make_batch(B, seed, dev):
@@ -67,28 +79,31 @@ def make_batch(B, seed, dev):
             det_scores.to(dev))
 
 
-def bytes_per_step(B, P, C):
+def criterion_bytes(B, P, C):
     """Algorithmic HBM bytes of the fused loss pass: read locs+scores once,
     write their gradients once, priors once per batch."""
     return B * P * 2 * (4 + C) * 4 + 16 * P
 
 
+def detect_bytes(w):
+    """scores [B,P,C] + locs [B,P,4] + priors read; decoded boxes [B,P,4], candidate keys (8 B
+    each) and per-(image, class) counts written (k_det_prepare; the NMS kernels after it are
+    latency-bound and read only the candidates)."""
+    return w['B'] * w['P'] * (4 * w['C'] + 16 + 16) + 16 * w['P'] + 8 * w['n_cand'] + 4 * w['B'] * w['C']
+
+
 # Algorithmic HBM bytes per launch of the streaming (HBM-bound) kernels of one step (DESIGN.md
 # "Kernels"): every input read once, every output written once.  w = workload constants.
 ALGO_BYTES = {
-    # scores [B,P,C] + locs [B,P,4] + priors [P,4] read; decoded boxes [B,P,4] and the
-    # candidate keys (8 B each) + per-(image, class) counts written
-    'k_det_prepare': lambda w: w['B'] * w['P'] * (4 * w['C'] + 16 + 16) + 16 * w['P']
-                               + 8 * w['n_cand'] + 4 * w['B'] * w['C'],
+    'k_det_prepare': detect_bytes,
     # locs + scores read, their gradients written, matcher obj (i32) + overlap (f32) read,
-    # the hard-negative pool (f32) written, priors read once
-    'k_multibox': lambda w: w['B'] * w['P'] * (2 * (16 + 4 * w['C']) + 12) + 16 * w['P'],
-    # priors read per image tile, obj + overlap written, per-tile per-object partial keys (u64)
-    'k_match_tile': lambda w: w['B'] * w['P'] * (16 + 8) + w['B'] * ((w['P'] + 255) // 256) * w['Gmax'] * 8,
+    # priors read once
+    'k_multibox': lambda w: w['B'] * w['P'] * (2 * (16 + 4 * w['C']) + 8) + 16 * w['P'],
+    # priors read per image tile, obj + overlap written
+    'k_match_tile': lambda w: w['B'] * w['P'] * (16 + 8),
 }
 HBM_KERNELS = tuple(ALGO_BYTES)
 ALL_KERNELS = HBM_KERNELS + ('k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm')
-TIMING_EVERY = 10
 PMC_FILE = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
 
 
@@ -103,40 +118,222 @@ def pmc_traffic(kernel):
         return None
 
 
-def cpu_baseline(B_sample, threads):
-    """The oracle (CPU restatement of the reference, pinned by tests/golden) on host cores:
-    criterion fwd+bwd on B_sample images + detect on B_sample images.  kind = 'port'."""
-    import numpy as np
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(B, det_images, threads_all):
+    """The oracle (CPU restatement of the reference, pinned by tests/golden) on host cores: warm
+    median of MultiBoxLoss512 (DIoU+focal) fwd+bwd over the SAME B-image workload, plus detect on
+    a sample of `det_images` images (numpy greedy NMS, torchvision semantics), at all host threads
+    (capped at 16, the box's CPU share) and at 1 thread.  kind = 'port'."""
     from oracle import loss_ref as LR
     from oracle import match_ref as M
-    torch.set_num_threads(threads)
     Pn = prior_table(ARCH)
     P = torch.from_numpy(Pn)
-    boxes, labels = synth.make_gt(B_sample, seed=0, n_classes=N_CLASSES)
-    locs, scores = synth.make_preds(B_sample, Pn.shape[0], N_CLASSES, seed=0)
-    det = scores.clone()
+    boxes, labels = synth.make_gt(B, seed=0, n_classes=N_CLASSES)
+    locs, scores = synth.make_preds(B, Pn.shape[0], N_CLASSES, seed=0)
+    det = scores[:det_images].clone()
     det[:, :, 0] += 6.0
+    out = {}
+    for threads in (threads_all, 1):
+        torch.set_num_threads(threads)
+        crit = []
+        for _ in range(3):      # first run warms the allocator / thread pool; median of the rest
+            lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
+            t0 = time.perf_counter()
+            LR.criterion('ssd512', P, lo, sc, boxes, labels, 'diou', 'focal').backward()
+            crit.append(time.perf_counter() - t0)
+        t_crit = sorted(crit[1:])[len(crit[1:]) // 2]
+        t0 = time.perf_counter()
+        probs = torch.softmax(det, 2).numpy()
+        bx = M.decode_boxes(locs[:det_images].numpy(), Pn, 'offset')
+        M.detect(probs, bx, 0.01, 0.45, 200)
+        t_det = time.perf_counter() - t0
+        per_img = t_crit / B + t_det / det_images
+        out[threads] = (1.0 / per_img, t_crit, t_det)
+    torch.set_num_threads(threads_all)
+    v_all, c_all, d_all = out[threads_all]
+    v_one, c_one, d_one = out[1]
+    return {'value': round(v_all, 3), 'unit': 'images/s', 'cores': threads_all, 'kind': 'port',
+            'sample': ('oracle MultiBoxLoss512 (DIoU+focal) fwd+bwd on the %d-image batch, warm median '
+                       'of 2: %.3f s; oracle detect on %d images: %.2f s; images/s = 1 / (criterion '
+                       's/img + detect s/img), %d host threads' % (B, c_all, det_images, d_all, threads_all)),
+            'one_thread': {'value': round(v_one, 3), 'cores': 1, 'criterion_s': round(c_one, 4),
+                           'detect_s': round(d_one, 3)}}
+
+
+# ----------------------------------------------------------------------------- DCN (config C4)
+def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
+    """DeformConv2d (a14) forward+backward at config C4's largest map: TF/s of the three
+    contractions (fwd, d-cols, d-weight: 3 x 2*M*O*C*9) against the fp32 MFMA peak."""
+    g = torch.Generator(device=dev).manual_seed(H)
+    x = torch.randn(B, C, H, H, device=dev, generator=g).requires_grad_(True)
+    off = torch.randn(B, 18, H, H, device=dev, generator=g).requires_grad_(True)
+    ml = torch.randn(B, 9, H, H, device=dev, generator=g).requires_grad_(True)
+    w = (torch.randn(O, C, 3, 3, device=dev, generator=g) / 48).requires_grad_(True)
+    gout = torch.randn(B, O, H, H, device=dev, generator=g)
+    for _ in range(2):
+        core.deform_conv2d(x, off, ml, w).backward(gout)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        core.deform_conv2d(x, off, ml, w).backward(gout)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    tf = 3 * 2.0 * B * H * H * O * C * 9 / ms / 1e9
+    return {'config': 'C4 DeformConv2d B=%d %d->%d 3x3 %dx%d fwd+bwd fp32' % (B, C, O, H, H),
+            'ms': round(ms, 3), 'tflops': round(tf, 2), 'peak_tflops': F32_MFMA_PEAK_TFS,
+            'mfma_frac': round(tf / F32_MFMA_PEAK_TFS, 4)}
+
+
+# ----------------------------------------------------------------------------- the step
+class Step:
+    """Criterion forward+backward and detect on one batch; eager or captured in a hipGraph."""
+
+    def __init__(self, dev, B, rank, world, graph):
+        self.dev, self.B = dev, B
+        Pn = prior_table(ARCH)
+        self.P = Pn.shape[0]
+        self.priors = torch.from_numpy(Pn).to(dev)
+        self.cfg = Cfg(reg_weights=1.0, device=dev, n_classes=N_CLASSES, reg_loss='diou',
+                       cls_loss='focal', focal_type='softmax', model={'box_type': 'offset'})
+        self.crit = CR.MultiBoxLoss512(priors_cxcy=self.priors, config=self.cfg)
+        self.crit.distributed = world > 1
+        self.boxes, self.labels, locs0, scores0, self.det_scores = make_batch(B, 1000 * rank, dev)
+        self.locs = locs0.clone().requires_grad_(True)
+        self.scores = scores0.clone().requires_grad_(True)
+        cap = max(int(b.shape[0]) for b in self.boxes)
+        self.capacity = max(16, (cap + 15) // 16 * 16)
+        self.stage = core.GtStaging(B, self.capacity, dev)
+        # the warm-up runs on the capture stream, so every workspace the captured calls use
+        # (cached per stream in core.workspace) already exists: nothing large is allocated
+        # under capture
+        self.cap_stream = torch.cuda.Stream(dev)
+        self.graph = None
+        self.use_graph = graph
+
+    def body(self, gt, capture=False):
+        """The step's device work, in stream order on the current stream: criterion forward,
+        detect (kernels queued ahead of the backward, lists collected later), backward.  One
+        stream on purpose: a fork/join inside a graph costs ~30 us per edge on this runtime
+        (scripts/probe_graph_launch.py), more than the parallel branch would save."""
+        loss = self.crit(self.locs, self.scores, gt, None)
+        h = core.detect(self.locs.detach(), self.det_scores, 0.01, 0.45, 200, self.priors,
+                        box_type='offset', act='softmax', async_=True, capture=capture)
+        loss.backward()
+        return loss, h
+
+    def launch_eager(self):
+        self.locs.grad = None
+        self.scores.grad = None
+        gt = self.stage.stage(self.boxes, self.labels)
+        return self.body(gt)
+
+    def eager(self):
+        loss, h = self.launch_eager()
+        return loss, h.wait()
+
+    def capture(self):
+        """Capture body() into a hipGraph (the usual torch pattern: warm-up already done on a
+        side stream; gradients set to None so the captured backward owns them)."""
+        gt = self.stage.stage(self.boxes, self.labels)
+        torch.cuda.synchronize()
+        self.locs.grad = None
+        self.scores.grad = None
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.cap_stream):
+            self.g_loss, self.g_det = self.body(gt, capture=True)
+        torch.cuda.synchronize()
+
+    def launch_replay(self):
+        self.stage.stage(self.boxes, self.labels)
+        self.graph.replay()
+        return self.g_loss, self.g_det.replayed()
+
+    def replay(self):
+        loss, h = self.launch_replay()
+        return loss, h.wait()
+
+    def launch(self):
+        return self.launch_replay() if self.graph is not None else self.launch_eager()
+
+    def __call__(self):
+        return self.replay() if self.graph is not None else self.eager()
+
+
+def timed(fn, steps, dist, dev, per_step=None):
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
-    loss = LR.criterion('ssd512', P, lo, sc, boxes, labels, 'diou', 'focal')
-    loss.backward()
-    t1 = time.perf_counter()
-    probs = torch.softmax(det, 2).numpy()
-    bx = M.decode_boxes(locs.numpy(), Pn, 'offset')
-    M.detect(probs, bx, 0.01, 0.45, 200)
-    t2 = time.perf_counter()
-    per_img = (t2 - t0) / B_sample
-    return {'value': round(1.0 / per_img, 4), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
-            'sample': '%d SSD512 images: oracle MultiBoxLoss512 (DIoU+focal) fwd+bwd %.2f s + oracle '
-                      'detect (numpy greedy NMS, torchvision semantics) %.2f s, torch/numpy on %d host '
-                      'threads' % (B_sample, t1 - t0, t2 - t1, threads)}
+    for i in range(steps):
+        fn()
+        if per_step is not None:
+            per_step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def grad_allreduce_figure(step, a, dist, dev, world):
+    """The data-parallel train step's gradient exchange: an SSD512-sized fp32
+    gradient buffer SUM-all-reduced in DDP-sized buckets on its own RCCL communicator and stream,
+    overlapped with the hot-path step (as DDP overlaps it with the backward).  Returns the
+    all-reduce alone and the overlapped step."""
+    grad = torch.ones(SSD512_PARAMS, dtype=torch.float32, device=dev)
+    per = BUCKET_MB * (1 << 20) // 4
+    buckets = list(grad.split(per))
+    group = dist.new_group(backend='nccl')
+    comm = torch.cuda.Stream(dev)
+
+    def allreduce():
+        for b in buckets:
+            dist.all_reduce(b, group=group)
+
+    for _ in range(3):
+        allreduce()
+    torch.cuda.synchronize()
+    n_ar = max(5, a.steps // 5)
+    t_ar = timed(allreduce, n_ar, dist, dev) / n_ar
+    cur = torch.cuda.current_stream(dev)
+
+    def overlapped():
+        comm.wait_stream(cur)
+        with torch.cuda.stream(comm):
+            allreduce()
+        step()
+        cur.wait_stream(comm)
+
+    for _ in range(3):
+        overlapped()
+    t_step = timed(overlapped, a.steps, dist, dev) / a.steps
+    nbytes = SSD512_PARAMS * 4
+    return {'grad_elems': SSD512_PARAMS, 'grad_bytes': nbytes, 'bucket_mb': BUCKET_MB,
+            'n_buckets': len(buckets), 'allreduce_ms': round(t_ar * 1e3, 4),
+            'allreduce_busbw_GBps': round(2 * (world - 1) / world * nbytes / t_ar / 1e9, 1),
+            'step_ms': round(t_step * 1e3, 4),
+            'images_per_s': round(world * a.batch / t_step, 1)}
 
 
 def main():
     a = parse()
+    if 'WORLD_SIZE' not in os.environ and a.gpus > 1:
+        # one process per GPU: start the ranks now, before anything touches the GPU
+        from shape_based_object_detection_amd.launch import spawn_ranks
+        sys.exit(spawn_ranks(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != a.gpus:
+        raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' % (a.gpus, world))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -146,58 +343,26 @@ def main():
     torch.cuda.set_device(dev)
     L.lib()
     B = a.batch
-    Pn = prior_table(ARCH)
-    P = Pn.shape[0]
-    priors = torch.from_numpy(Pn).to(dev)
-    cfg = Cfg(reg_weights=1.0, device=dev, n_classes=N_CLASSES, reg_loss='diou', cls_loss='focal',
-              focal_type='softmax', model={'box_type': 'offset'})
-    crit = CR.MultiBoxLoss512(priors_cxcy=priors, config=cfg)
-    crit.distributed = world > 1
-    boxes, labels, locs0, scores0, det_scores = make_batch(B, 1000 * rank, dev)
-    locs = locs0.clone().requires_grad_(True)
-    scores = scores0.clone().requires_grad_(True)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    loss_ms = []
-
-    def step(record=False):
-        # criterion forward; detect's kernels queued (core.detect async: the same work as
-        # models.utils.detect, whose lists are collected at the end of the step); backward —
-        # its host work overlaps the detect kernels; then the per-image detection lists
-        locs.grad = None
-        scores.grad = None
-        if record:
-            ev[0].record()
-        loss = crit(locs, scores, boxes, labels)
-        if record:
-            ev[1].record()
-        if a.sync_detect:
-            if record:
-                ev[2].record()
-            loss.backward()
-            if record:
-                ev[3].record()
-            return loss, MU.detect(locs.detach(), det_scores, 0.01, 0.45, 200, priors, cfg)
-        h = core.detect(locs.detach(), det_scores, 0.01, 0.45, 200, priors, box_type='offset',
-                        act='softmax', async_=True)
-        if record:
-            ev[2].record()
-        loss.backward()
-        if record:
-            ev[3].record()
-        return loss, h.wait()
-
+    st = Step(dev, B, rank, world, graph=not a.eager)
+    P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing)
     with torch.no_grad():
-        n_cand = int((torch.softmax(det_scores, 2)[:, :, 1:] > 0.01).sum().item())
-    wl = {'B': B, 'P': P, 'C': N_CLASSES, 'n_cand': n_cand, 'Gmax': max(int(b.shape[0]) for b in boxes)}
+        n_cand = int((torch.softmax(st.det_scores, 2)[:, :, 1:] > 0.01).sum().item())
+    wl = {'B': B, 'P': P, 'C': N_CLASSES, 'n_cand': n_cand}
 
-    for _ in range(max(a.warmup - 1, 0)):
-        step()
-    # one more untimed step with every instrumented kernel bracketed by HIP events: the
-    # per-kernel table, and the dominant HBM-bound kernel that is timed live below
+    # warm-up on the capture stream (lazy init of autograd / allocator state, and the per-stream
+    # workspaces the captured calls will use)
+    side = st.cap_stream
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(max(a.warmup - 1, 1)):
+            st.eager()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    # one more eager step with every instrumented kernel carrying HIP events on its dispatch:
+    # the per-kernel table, and the dominant HBM-bound kernel that is timed live below
     torch.cuda.synchronize()
     L.timing_enable('*')
-    step()
+    st.eager()
     torch.cuda.synchronize()
     kernel_us = {}
     for k in ALL_KERNELS:
@@ -205,75 +370,107 @@ def main():
         if n:
             kernel_us[k] = round(ms * 1e3, 1)
     dominant = max(HBM_KERNELS, key=lambda k: kernel_us.get(k, 0.0))
-    # live timing of the dominant kernel over the timed region, one launch in TIMING_EVERY: a timed
-    # launch carries its events on the dispatch (exact kernel time, agrees with rocprofv3) but
-    # costs host time, so only a sample of the steps pays it
-    L.call('sbod_timing_every', TIMING_EVERY)
-    L.timing_enable(dominant)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    dom_n, dom_ms = L.timing_query(dominant)
     L.timing_enable(None)
-    L.call('sbod_timing_every', 1)
-    # criterion fwd+bwd GPU time, from event-bracketed steps AFTER the timed region (the per-step
-    # event records would otherwise add host work to the steps being timed)
+
+    eager_ms = None
+    if st.use_graph:        # the same step without the graph, for the host-overhead comparison
+        n_e = min(a.steps, 20)
+        eager_ms = timed(st.eager, n_e, dist, dev) / n_e * 1e3
+
+    samples = []
+    if st.use_graph:
+        # the dominant kernel is captured with a device span slot it stamps itself on every
+        # replay (first workgroup start -> last workgroup end, stores drained); one replay in
+        # TIMING_EVERY is armed before and read after (two small host-synchronous copies)
+        L.timing_enable(dominant)
+        st.capture()
+        L.timing_enable(None)
+        for _ in range(3):
+            st()
+        count = [0]
+
+        def graph_step():
+            k = count[0]
+            count[0] += 1
+            if k % TIMING_EVERY:
+                return st()
+            L.call('sbod_timing_arm')
+            out = st()
+            n, ms = L.timing_query(dominant)
+            if n:
+                samples.append(ms / n)
+            return out
+        elapsed = timed(graph_step, a.steps, dist, dev)
+    else:
+        L.call('sbod_timing_every', TIMING_EVERY)
+        L.timing_enable(dominant)
+        elapsed = timed(st, a.steps, dist, dev)
+        n, ms = L.timing_query(dominant)
+        samples = [ms / n] * n if n else []
+        L.timing_enable(None)
+        L.call('sbod_timing_every', 1)
+    ms_step = elapsed / a.steps * 1e3
+
+    # GPU time of one step (events around the replay / the eager launches), after the timed region
+    gpu_ms = []
     for _ in range(min(a.steps, 20)):
-        step(record=True)
-        loss_ms.append(tuple(ev))
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    torch.cuda.synchronize()
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    crit_ms = sorted(e0.elapsed_time(e1) + e2.elapsed_time(e3) for e0, e1, e2, e3 in loss_ms)
-    crit_ms_med = crit_ms[len(crit_ms) // 2]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _, h = st.launch()
+        e1.record()
+        h.wait()
+        e1.synchronize()
+        gpu_ms.append(e0.elapsed_time(e1))
+    gpu_ms_med = sorted(gpu_ms)[len(gpu_ms) // 2]
+
+    dp = grad_allreduce_figure(st.replay if st.use_graph else st.eager, a, dist, dev, world) if dist else None
+
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
-    imgs = world * B * a.steps
-    value = imgs / elapsed
-    ms_step = elapsed / a.steps * 1e3
-    nbytes = bytes_per_step(B, P, N_CLASSES)
+    value = world * B * a.steps / elapsed
+    step_bytes = criterion_bytes(B, P, N_CLASSES) + detect_bytes(wl)
     line = {
         'metric': 'images/sec train step SSD512 batch=32 @1/2/4/8 GPU; IoU+NMS Manchors/sec',
         'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': a.steps,
         'warmup': a.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-        'config': {'workload': 'SSD512 per-GPU batch %d: MultiBoxLoss512(DIoU+focal) fwd+bwd + '
-                               'detect(min_score 0.01, iou 0.45, top_k 200)%s'
-                               % (B, '' if a.sync_detect else ', detect kernels overlapped with the backward'),
+        'config': {'workload': 'SSD512 per-GPU batch %d: GT packing + MultiBoxLoss512(DIoU+focal) '
+                               'fwd+bwd + detect(min_score 0.01, iou 0.45, top_k 200)%s'
+                               % (B, ', one hipGraph replay per step'
+                                  if st.use_graph else ', eager launches'),
                    'global_batch': world * B, 'n_priors': P, 'n_classes': N_CLASSES,
                    'parallelism': 'dp%d' % world},
         'manchors_per_sec': round(world * B * P * a.steps / elapsed / 1e6, 3),
-        'criterion_fwd_bwd_ms_median': round(crit_ms_med, 4),
-        'criterion_GBps_algorithmic': round(nbytes / (crit_ms_med * 1e-3) / 1e9, 1),
+        'step_gpu_ms_median': round(gpu_ms_med, 4),
+        'step_algorithmic_bytes': step_bytes,
+        'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
+        'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        'graph': st.use_graph,
+        'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }
-    avg_s = dom_ms / max(dom_n, 1) * 1e-3
+    avg_s = (sum(samples) / len(samples) * 1e-3) if samples else float('nan')
     algo = ALGO_BYTES[dominant](wl)
     achieved = algo / avg_s / 1e9
-    traffic = pmc_traffic(dominant)
     line['roofline'] = {
         'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-        'kernel': dominant, 'launches': dom_n, 'timed_every': TIMING_EVERY, 'avg_us': round(avg_s * 1e6, 2),
+        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(dominant),
+        'kernel': dominant, 'launches_timed': len(samples), 'avg_us': round(avg_s * 1e6, 2),
+        'timing': ('device span stamped by the kernel in the graph (first workgroup start to last '
+                   'workgroup end, s_memrealtime), one replay in %d' % TIMING_EVERY
+                   if st.use_graph else 'HIP events on the dispatch, one launch in %d' % TIMING_EVERY),
         'algorithmic_bytes_per_launch': algo,
     }
+    if st.use_graph:
+        line['roofline']['span_clock_hz'] = L.lib().sbod_timing_clock_hz()
     line['kernel_us_per_step'] = kernel_us
+    if dp is not None:
+        line['dp_train_step_with_grad_allreduce'] = dp
+    if not a.no_dcn:
+        line['dcn'] = dcn_figure(dev)
     if not a.no_cpu_baseline:
-        threads = min(os.cpu_count() or 1, 16)
-        line['cpu_baseline'] = cpu_baseline(a.cpu_sample_images, threads)
+        line['cpu_baseline'] = cpu_baseline(B, a.cpu_detect_images, min(os.cpu_count() or 1, 16))
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -55,12 +55,36 @@ int sbod_timing_query(const char *kernel, int *launches, double *total_ms);
  * (hipExtLaunchKernelGGL), which costs host time per timed launch; sampling keeps that out of
  * most steps of a benchmark. */
 int sbod_timing_every(int n);
+/* Under hipGraph stream capture a dispatch cannot carry events (and this runtime refuses
+ * external event nodes): a selected HBM-bound kernel (k_match_tile, k_multibox, k_det_prepare)
+ * is instead captured with a device span slot that the kernel itself writes on every replay —
+ * its first workgroup's start and last workgroup's end (after the block's stores have drained),
+ * in s_memrealtime ticks.  sbod_timing_arm() resets the slots (host-synchronous; call it between
+ * replays), and sbod_timing_query() then reports the span of the replay since the last arm.
+ * The capture records survive sbod_timing_enable(); sbod_timing_reset_graphs() releases the
+ * slots once the graphs holding them are gone. */
+int sbod_timing_arm(void);
+double sbod_timing_clock_hz(void);   /* the span clock (hipDeviceAttributeWallClockRate) */
+int sbod_timing_reset_graphs(void);
 
 /* Asynchronous device -> host copy on `stream` (hipMemcpyAsync; dst_host should be pinned, e.g.
  * torch's pin_memory buffers).  Used for detect's per-image counts (the one value the host needs
  * from a detect call, models/utils.py:274-290); the caller orders its host read after an event
  * recorded behind it.  Cheaper on the host than a framework-level non_blocking copy. */
 int sbod_memcpy_d2h_async(void *dst_host, const void *src_dev, size_t bytes, void *stream);
+
+/* ---------------------------------------------------------------- f1: ground-truth packing
+ * Replaces the per-step GT handling of every criterion: the collate_fn list-of-tensors batch
+ * (dataset/Datasets.py:58-86), moved to the device image by image (train_anchor.py:266-268) and
+ * indexed per image in the matching loop (models/SSD512.py:525-572).  One launch copies image
+ * i's `counts[i]` rows from the DEVICE pointers box_ptrs[i] ([G_i,4] f32) / label_ptrs[i]
+ * ([G_i] int64) into gt_boxes / gt_labels back to back and writes gt_offsets [B+1].
+ * box_ptrs, label_ptrs and counts are HOST arrays of B entries (they travel in the kernel
+ * arguments: no device pointer table, no host->device copy).  `capacity` = rows available in
+ * gt_boxes / gt_labels (a fixed-capacity destination can be read by a captured hipGraph). */
+int sbod_gt_pack(const void *const *box_ptrs, const void *const *label_ptrs,
+                 const int32_t *counts, int B, int64_t capacity, float *gt_boxes,
+                 int64_t *gt_labels, int32_t *gt_offsets, void *stream);
 
 /* ---------------------------------------------------------------- a1 / a4: pairwise IoU
  * Replaces metrics.find_jaccard_overlap (metrics.py:208-252; mode SBOD_IOU_METRICS: +1e-5

@@ -52,7 +52,11 @@ SIGNATURES = {
     'sbod_timing_enable': (I32, [ctypes.c_char_p]),
     'sbod_timing_query': (I32, [ctypes.c_char_p, P, P]),
     'sbod_timing_every': (I32, [I32]),
+    'sbod_timing_reset_graphs': (I32, []),
+    'sbod_timing_arm': (I32, []),
+    'sbod_timing_clock_hz': (ctypes.c_double, []),
     'sbod_memcpy_d2h_async': (I32, [P, P, SZ, P]),
+    'sbod_gt_pack': (I32, [P, P, P, I32, I64, P, P, P, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
     'sbod_dcn_fwd_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),
     'sbod_dcn_bwd_f32': (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, P,

@@ -3,6 +3,7 @@
 Everything here runs on ROCm device tensors; inputs on the CPU are rejected.  No call in this
 module synchronises with the host unless its docstring says so.
 """
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -12,51 +13,156 @@ class GtPack:
     """Ragged ground truth packed once per step (dataset/Datasets.py:58-86 list-of-tensors).
 
     boxes [sum G, 4] f32 xyxy, labels [sum G] int64, offsets [B+1] int32 on the device;
-    ``counts`` / ``gmax`` are host ints (taken from tensor shapes: no device sync)."""
+    ``counts`` / ``gmax`` are host ints (taken from tensor shapes: no device sync).  A pack
+    staged into fixed-capacity buffers (``GtStaging``) reports ``gmax`` = its per-image capacity,
+    so every launch that reads it has the same shape from step to step (hipGraph replay)."""
 
     __slots__ = ('boxes', 'labels', 'offsets', 'counts', 'gmax', 'batch')
 
-    def __init__(self, boxes, labels, offsets, counts):
+    def __init__(self, boxes, labels, offsets, counts, gmax=None):
         self.boxes, self.labels, self.offsets, self.counts = boxes, labels, offsets, counts
-        self.gmax = max(counts) if counts else 0
+        self.gmax = gmax if gmax is not None else (max(counts) if counts else 0)
         self.batch = len(counts)
 
 
-_OFFSET_CACHE = {}
+_PTR_TABLES = {}
 
 
-def _offsets_tensor(counts, device):
-    key = (tuple(counts), str(device))
-    t = _OFFSET_CACHE.get(key)
+def _ptr_tables(B):
+    """Host arrays (box pointers, label pointers, counts) handed to sbod_gt_pack, cached per B.
+    The C call reads them before it returns, so one set per batch size is enough."""
+    t = _PTR_TABLES.get(B)
     if t is None:
-        offs = [0]
-        for c in counts:
-            offs.append(offs[-1] + c)
-        t = torch.tensor(offs, dtype=torch.int32).pin_memory().to(device, non_blocking=True)
-        if len(_OFFSET_CACHE) > 256:
-            _OFFSET_CACHE.clear()
-        _OFFSET_CACHE[key] = t
+        bp, lp, cn = np.zeros(B, np.uint64), np.zeros(B, np.uint64), np.zeros(B, np.int32)
+        t = (bp, lp, cn, bp.ctypes.data, lp.ctypes.data, cn.ctypes.data)
+        _PTR_TABLES[B] = t
     return t
 
 
-def pack_gt(boxes, labels, device=None, allow_empty=False):
-    """Pack per-image lists into a GtPack.  An image with no objects raises like the reference
-    does (``overlap.max(dim=0)`` of an empty matrix, models/SSD512.py:538)."""
-    if len(boxes) != len(labels):
-        raise ValueError('boxes and labels must have the same length')
-    counts = [b.shape[0] for b in boxes]
+def _check_counts(counts, allow_empty):
     if not allow_empty and 0 in counts:
         raise RuntimeError('max(): Expected reduction dim 0 to have non-zero size (an image has no '
                            'ground-truth objects, as in the reference criterion)')
-    device = device or boxes[0].device
-    gb = torch.cat(boxes if boxes[0].dim() == 2 else [b.reshape(-1, 4) for b in boxes])
-    gl = torch.cat(labels if labels[0].dim() == 1 else [l.reshape(-1) for l in labels])
-    L.require_device(gb, gl, what='pack_gt')   # torch.cat already rejects mixed devices
-    if gb.dtype != torch.float32:
-        gb = gb.float()
-    if gl.dtype != torch.int64:
-        gl = gl.long()
-    return GtPack(gb, gl, _offsets_tensor(counts, device), counts)
+
+
+def _as_rows(boxes, labels):
+    """Per-image [G,4] f32 / [G] int64 contiguous device tensors (converted only when needed)."""
+    bx, lb = [], []
+    dev = None
+    for b, l in zip(boxes, labels):
+        if not (b.is_cuda and l.is_cuda):
+            L.require_device(b, l, what='pack_gt')
+        if dev is None:
+            dev = b.device
+        elif b.device != dev or l.device != dev:
+            raise RuntimeError('pack_gt: ground truth of one batch spans several devices')
+        if b.dtype != torch.float32 or not b.is_contiguous() or b.dim() != 2:
+            b = b.reshape(-1, 4).float().contiguous()
+        if l.dtype != torch.int64 or not l.is_contiguous() or l.dim() != 1:
+            l = l.reshape(-1).long().contiguous()
+        bx.append(b)
+        lb.append(l)
+    return bx, lb, dev
+
+
+def _launch_pack(bx, lb, counts, capacity, out_b, out_l, out_off):
+    B = len(counts)
+    bp, lp, cn, bpa, lpa, cna = _ptr_tables(B)
+    bp[:] = [b.data_ptr() for b in bx]
+    lp[:] = [l.data_ptr() for l in lb]
+    cn[:] = counts
+    L.call('sbod_gt_pack', bpa, lpa, cna, B, capacity, L.ptr(out_b), L.ptr(out_l), L.ptr(out_off),
+           L.stream_of(out_off))
+
+
+def pack_gt(boxes, labels, device=None, allow_empty=False):
+    """Pack per-image lists into a GtPack with ONE device launch (sbod_gt_pack: the pointers
+    and offsets travel in the kernel arguments).  An image with no objects raises like the
+    reference does (``overlap.max(dim=0)`` of an empty matrix, models/SSD512.py:538).  A GtPack
+    (e.g. from ``GtStaging.stage``) is returned as is."""
+    if isinstance(boxes, GtPack):
+        return boxes
+    if len(boxes) != len(labels):
+        raise ValueError('boxes and labels must have the same length')
+    counts = [b.shape[0] for b in boxes]
+    _check_counts(counts, allow_empty)
+    bx, lb, dev = _as_rows(boxes, labels)
+    n = sum(counts)
+    gb = torch.empty(max(n, 1), 4, dtype=torch.float32, device=dev)
+    gl = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    off = torch.empty(len(counts) + 1, dtype=torch.int32, device=dev)
+    _launch_pack(bx, lb, counts, max(n, 1), gb, gl, off)
+    return GtPack(gb[:n], gl[:n], off, counts)
+
+
+class GtStaging:
+    """Fixed-capacity device ground truth for batches of ``batch`` images with at most
+    ``capacity`` objects each.
+
+    ``stage(boxes, labels)`` packs a collate_fn batch into the SAME device buffers every step
+    and returns a GtPack whose ``gmax`` is the capacity, so a hipGraph captured over a criterion
+    call keeps reading valid ground truth when it is replayed with the next batch:
+      * device lists (train_anchor.py:266-268 already moved them): one sbod_gt_pack launch;
+      * host (CPU) lists, straight from the DataLoader: packed into a pinned host buffer and sent
+        with ONE host->device copy (double-buffered, so the host never overwrites a buffer whose
+        copy is still in flight) — replacing the training loop's per-image ``.to(device)``."""
+
+    def __init__(self, batch, capacity, device):
+        self.batch, self.capacity = int(batch), int(capacity)
+        self.device = torch.device(device)
+        rows = self.batch * self.capacity
+        # one device region, boxes | labels | offsets, so the host path is a single copy
+        self._nb = (rows * 16, rows * 8, (self.batch + 1) * 4)
+        region = torch.zeros(sum(self._nb), dtype=torch.uint8, device=self.device)
+        self.boxes, self.labels, self.offsets = self._views(region)
+        self._region = region
+        self._host = []
+        self._host_next = 0
+
+    def _views(self, region):
+        nb_b, nb_l, _ = self._nb
+        return (region[:nb_b].view(torch.float32).view(-1, 4),
+                region[nb_b:nb_b + nb_l].view(torch.int64),
+                region[nb_b + nb_l:].view(torch.int32))
+
+    def _pinned(self):
+        if not self._host:
+            n = sum(self._nb)
+            self._host = [(torch.empty(n, dtype=torch.uint8, pin_memory=True), torch.cuda.Event())
+                          for _ in range(2)]
+        buf, ev = self._host[self._host_next]
+        self._host_next ^= 1
+        ev.synchronize()   # the copy that last used this buffer has finished
+        return buf, ev
+
+    def stage(self, boxes, labels, allow_empty=False):
+        if len(boxes) != self.batch or len(labels) != self.batch:
+            raise ValueError('GtStaging: batch of %d images, staging holds %d'
+                             % (len(boxes), self.batch))
+        counts = [b.shape[0] for b in boxes]
+        _check_counts(counts, allow_empty)
+        if max(counts) > self.capacity:
+            raise ValueError('GtStaging: an image has %d objects, capacity is %d'
+                             % (max(counts), self.capacity))
+        if boxes[0].is_cuda:
+            bx, lb, dev = _as_rows(boxes, labels)
+            if dev != self.device:
+                raise RuntimeError('GtStaging: ground truth on %s, staging on %s' % (dev, self.device))
+            _launch_pack(bx, lb, counts, self.boxes.shape[0], self.boxes, self.labels, self.offsets)
+        else:
+            self._stage_host(boxes, labels, counts)
+        return GtPack(self.boxes, self.labels, self.offsets, counts, gmax=self.capacity)
+
+    def _stage_host(self, boxes, labels, counts):
+        buf, ev = self._pinned()
+        hb, hl, ho = self._views(buf)
+        n = sum(counts)
+        if n:
+            torch.cat([b.reshape(-1, 4).float() for b in boxes], out=hb[:n])
+            torch.cat([l.reshape(-1).long() for l in labels], out=hl[:n])
+        ho.copy_(torch.from_numpy(np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)))
+        self._region.copy_(buf, non_blocking=True)
+        ev.record(torch.cuda.current_stream(self.device))
 
 
 _WS = {}
@@ -239,14 +345,24 @@ def allgather_pool(group=None):
 
     def exchange(pool):
         world, rank = dist.get_world_size(group), dist.get_rank(group)
-        out = torch.empty(world * pool.numel(), dtype=pool.dtype, device=pool.device)
-        try:
-            dist.all_gather_into_tensor(out, pool, group=group)
-        except (RuntimeError, NotImplementedError, AttributeError):   # backends without it (gloo)
+        # every rank must contribute the same B*P (a DistributedSampler with drop_last): checked
+        # with one tiny MAX all-reduce of (n, -n), so unequal shards fail loudly on every rank
+        # instead of desynchronising the gather
+        n = pool.numel()
+        chk = torch.tensor([n, -n], dtype=torch.int64, device=pool.device)
+        dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=group)
+        hi, lo = chk.tolist()
+        if hi != -lo:
+            raise RuntimeError('sbod global mining: ranks hold unequal batches (B*P between %d and %d); '
+                               'use equal per-rank batches (drop_last=True)' % (-lo, hi))
+        out = torch.empty(world * n, dtype=pool.dtype, device=pool.device)
+        if dist.get_backend(group) == 'gloo':     # gloo has no all_gather_into_tensor
             parts = [torch.empty_like(pool) for _ in range(world)]
             dist.all_gather(parts, pool, group=group)
             out = torch.cat(parts)
-        return out, rank * pool.numel()
+        else:
+            dist.all_gather_into_tensor(out, pool, group=group)
+        return out, rank * n
     return exchange
 
 
@@ -266,13 +382,27 @@ class DetectHandle:
     """An in-flight ``detect``: the kernels are queued on the stream and the per-image counts are
     copied to pinned host memory behind an event.  ``wait()`` blocks on that event only (work
     queued after the detect — e.g. a training backward — keeps running) and returns the lists
-    ``detect`` returns.  The inputs must stay alive and unmodified until ``wait()``."""
+    ``detect`` returns.  The inputs must stay alive and unmodified until ``wait()``.
 
-    __slots__ = ('_args', '_out', '_cnt_host', '_event', '_full', '_res', '_window', '_launch', '_slot_key')
+    A handle made under hipGraph capture (``detect(..., capture=True)``) is persistent: its
+    outputs and pinned count buffer are the graph's, and after each replay ``replayed()`` arms
+    it again (event behind the replay, fresh result lists)."""
 
-    def __init__(self, args, out, cnt_host, event, full, window):
+    __slots__ = ('_args', '_out', '_cnt_host', '_event', '_full', '_res', '_window', '_launch',
+                 '_slot_key', '_persistent')
+
+    def __init__(self, args, out, cnt_host, event, full, window, persistent=False):
         self._args, self._out, self._cnt_host, self._event = args, out, cnt_host, event
         self._full, self._res, self._window = full, None, window
+        self._persistent = persistent
+
+    def replayed(self, stream=None):
+        """After a replay of the graph this handle was captured in: record its event behind the
+        replay (on ``stream``, default the current stream) so ``wait()`` returns this replay's
+        detections."""
+        self._event.record(stream if stream is not None else torch.cuda.current_stream())
+        self._res = None
+        return self
 
     def wait(self):
         if self._res is not None:
@@ -281,7 +411,8 @@ class DetectHandle:
         out_b, out_l, out_s, cnt, dbg_p, dbg_b = self._out
         self._event.synchronize()
         counts = self._cnt_host.tolist()
-        _COUNT_SLOTS.setdefault(self._slot_key, []).append((self._cnt_host, self._event))
+        if not self._persistent:
+            _COUNT_SLOTS.setdefault(self._slot_key, []).append((self._cnt_host, self._event))
         if min(counts) < 0:   # rare: some image needs the full candidate window (exactness)
             _detect_launch(*self._launch_args(4096))
             counts = cnt.cpu().tolist()
@@ -328,11 +459,14 @@ def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overl
 
 
 def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='offset',
-           act='softmax', pos_mask=None, final_nms=None, debug=False, window=0, async_=False):
+           act='softmax', pos_mask=None, final_nms=None, debug=False, window=0, async_=False,
+           capture=False):
     """Batched decode + per-class NMS + top-k.  Returns (boxes, labels, scores) lists of per-image
     tensors (views of batched device outputs).  ONE host sync: the per-image counts (waited on
     through an event).  ``async_=True`` returns a ``DetectHandle`` instead (``.wait()`` gives the
-    lists), so a caller can overlap the detect kernels with later host work."""
+    lists), so a caller can overlap the detect kernels with later host work.  ``capture=True``
+    (inside hipGraph capture) returns a persistent handle: call ``.replayed()`` after each replay,
+    then ``.wait()``."""
     L.require_device(locs, scores, what='detect')
     B, P, C = scores.shape
     if top_k <= 0:
@@ -358,17 +492,28 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     # counts -> pinned host memory behind an event, both cached per (device, B): a pinned
     # allocation per call goes through hipHostMalloc / the host allocator's event bookkeeping and
     # stalls the launching thread for the whole queue
-    cnt_host, ev = _count_slot(dev, B)
+    if capture:
+        # owned by the graph from now on (its memcpy node writes this buffer on every replay);
+        # pinned memory cannot be allocated under capture, so it comes from the pool an eager
+        # warm-up call filled
+        free = _COUNT_SLOTS.get((dev, B))
+        if not free:
+            raise L.SbodError('detect(capture=True): run detect eagerly once with this batch size '
+                              'before capturing (warm-up), so its pinned count buffer exists')
+        cnt_host, ev = free.pop()
+    else:
+        cnt_host, ev = _count_slot(dev, B)
     stream = L.stream_of(cnt)
     L.call('sbod_memcpy_d2h_async', cnt_host.data_ptr(), L.ptr(cnt), 4 * B, stream)
-    ev.record(torch.cuda.current_stream(dev))
+    if not capture:
+        ev.record(torch.cuda.current_stream(dev))
     # the per-image views for the usual all-full case are built while the kernels run
     full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
     h = DetectHandle((lc, locs, sc, B, top_k, in_place, debug), (out_b, out_l, out_s, cnt, dbg_p, dbg_b),
-                     cnt_host, ev, full, window)
+                     cnt_host, ev, full, window, persistent=capture)
     h._launch = launch
     h._slot_key = (dev, B)
-    return h if async_ else h.wait()
+    return h if (async_ or capture) else h.wait()
 
 
 def nms(boxes, scores, overlap, top_k=0, variant='tv', beta1=1.0):

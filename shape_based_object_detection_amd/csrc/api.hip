@@ -76,7 +76,15 @@ std::string g_filter;
 struct TimingRec {
   const char *name;
   hipEvent_t a, b;
+  bool graph;   // captured into a hipGraph: the kernel writes span slot `slot` on every replay
+  int slot;
 };
+// Device span slots for kernels captured into graphs: {start, end} u64 pairs in s_memrealtime
+// ticks (100 MHz).  Allocated by sbod_timing_enable (never under capture).
+constexpr int kSpanSlots = 256;
+double g_realtime_hz = 100.0e6;   // replaced by hipDeviceAttributeWallClockRate at allocation
+unsigned long long *g_span_dev = nullptr;
+int g_span_next = 0;
 std::vector<TimingRec> g_recs;
 int g_every = 1;                                  // time one launch in g_every (per kernel name)
 std::unordered_map<std::string, long long> g_seen;
@@ -99,6 +107,16 @@ KernelTimer::KernelTimer(const char *name, hipStream_t s, bool attached)
   std::lock_guard<std::mutex> g(g_tmu);
   if (g_filter.empty() || (g_filter != "*" && g_filter != name)) return;
   if (g_every > 1 && (g_seen[name]++ % g_every) != 0) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) {
+    attached_ = false;
+    if (g_span_dev != nullptr && g_span_next < kSpanSlots) {
+      const int slot = g_span_next++;
+      span_ = g_span_dev + 2 * slot;
+      g_recs.push_back({name, nullptr, nullptr, true, slot});
+    }
+    return;
+  }
   start_ = pooled_event();
   if (attached_) {
     stop_ = pooled_event();
@@ -112,11 +130,11 @@ KernelTimer::~KernelTimer() {
   if (!start_) return;
   std::lock_guard<std::mutex> g(g_tmu);
   if (attached_) {
-    g_recs.push_back({name_, start_, stop_});
+    g_recs.push_back({name_, start_, stop_, false, -1});
     return;
   }
   hipEvent_t e = pooled_event();
-  if (e && hipEventRecord(e, stream_) == hipSuccess) g_recs.push_back({name_, start_, e});
+  if (e && hipEventRecord(e, stream_) == hipSuccess) g_recs.push_back({name_, start_, e, false, -1});
 }
 
 }  // namespace sbod
@@ -125,13 +143,57 @@ extern "C" {
 
 int sbod_timing_enable(const char *kernel_filter) {
   std::lock_guard<std::mutex> g(sbod::g_tmu);
+  // eager records go back to the pool; records inside captured graphs stay (their events belong
+  // to graph nodes) until sbod_timing_reset_graphs()
+  std::vector<sbod::TimingRec> keep;
   for (auto &r : sbod::g_recs) {
+    if (r.graph) {
+      keep.push_back(r);
+      continue;
+    }
     sbod::g_pool.push_back(r.a);
     sbod::g_pool.push_back(r.b);
   }
-  sbod::g_recs.clear();
+  sbod::g_recs.swap(keep);
   sbod::g_seen.clear();
   sbod::g_filter = kernel_filter ? kernel_filter : "";
+  if (!sbod::g_filter.empty() && sbod::g_span_dev == nullptr &&
+      (hipMalloc(reinterpret_cast<void **>(&sbod::g_span_dev), sbod::kSpanSlots * 16) != hipSuccess ||
+       hipMemset(sbod::g_span_dev, 0, sbod::kSpanSlots * 16) != hipSuccess)) {
+    sbod::g_span_dev = nullptr;
+    return sbod::launch_status("sbod_timing_enable(span slots)");
+  }
+  if (!sbod::g_filter.empty()) {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+      sbod::g_realtime_hz = 1e3 * khz;
+  }
+  return SBOD_OK;
+}
+
+double sbod_timing_clock_hz(void) { return sbod::g_realtime_hz; }
+
+int sbod_timing_arm(void) {
+  std::lock_guard<std::mutex> g(sbod::g_tmu);
+  if (sbod::g_span_dev == nullptr || sbod::g_span_next == 0) return SBOD_OK;
+  std::vector<unsigned long long> init(2 * sbod::g_span_next);
+  for (int i = 0; i < sbod::g_span_next; ++i) {
+    init[2 * i] = ~0ull;
+    init[2 * i + 1] = 0ull;
+  }
+  if (hipMemcpy(sbod::g_span_dev, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return sbod::launch_status("sbod_timing_arm");
+  return SBOD_OK;
+}
+
+int sbod_timing_reset_graphs(void) {
+  std::lock_guard<std::mutex> g(sbod::g_tmu);
+  std::vector<sbod::TimingRec> keep;
+  for (auto &r : sbod::g_recs)
+    if (!r.graph) keep.push_back(r);
+  sbod::g_recs.swap(keep);
+  sbod::g_span_next = 0;   // the graphs holding the span pointers must be gone
   return SBOD_OK;
 }
 
@@ -150,6 +212,15 @@ int sbod_timing_query(const char *kernel, int *launches, double *total_ms) {
   double tot = 0.0;
   for (auto &r : sbod::g_recs) {
     if (std::strcmp(r.name, kernel) != 0) continue;
+    if (r.graph) {   // span slot of the last replay since sbod_timing_arm()
+      unsigned long long v[2] = {0ull, 0ull};
+      if (hipMemcpy(v, sbod::g_span_dev + 2 * r.slot, 16, hipMemcpyDeviceToHost) != hipSuccess)
+        return sbod::launch_status("sbod_timing_query(span)");
+      if (v[0] == ~0ull || v[1] == 0ull || v[1] == ~0ull || v[1] < v[0]) continue;   // not run since the last arm
+      tot += static_cast<double>(v[1] - v[0]) / sbod::g_realtime_hz * 1e3;
+      ++n;
+      continue;
+    }
     float ms = 0.f;
     if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess)
       return sbod::launch_status("sbod_timing_query");

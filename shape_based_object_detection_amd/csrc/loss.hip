@@ -283,6 +283,7 @@ struct LossArgs {
   int reg, cls, flags;
   float reg_weight, afg, abg, gamma;
   float *partials, *pool;
+  unsigned long long *span;   // KernelTimer span slot under graph capture, else null
 };
 
 // exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'
@@ -298,6 +299,7 @@ __global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__r
   extern __shared__ float s_sc[];
   __shared__ float s_red[16];
   STAMP_BEGIN();
+  span_begin(a.span);
   PHASE_DECL;
   SEG_PHASE(0);
   const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x;
@@ -536,6 +538,7 @@ __global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__r
     a.partials[2 * blk] = conf_l;
     a.partials[2 * blk + 1] = loc_l;
   }
+  span_end(a.span);
   STAMP_END(4, 1);
 }
 
@@ -838,7 +841,7 @@ int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const in
 #define SBOD_HNM(T, ST)                                                                         \
   do {                                                                                          \
     KernelTimer kt("k_hnm", s, true);                                                                 \
-    hipExtLaunchKernelGGL((k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, kt.start(), kt.stop(), 0, pool, P, B, global,    \
+    tlaunch(kt, (k_hnm<T, ST>), dim3(nseg), dim3(kHBlock), hl, s, pool, P, B, global,    \
                        n_pos, neg_pos_ratio, static_cast<const T *>(scores), static_cast<T *>(grad_scores), C, \
                        npos_total, ws.hnm, n_all, local_off);                                   \
   } while (0)
@@ -888,13 +891,14 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   hipStream_t s = as_stream(stream);
   LossArgs a{B, P, C, priors_cxcy, odm_arm_locs, arm_scores, gt_boxes, gt_labels, gt_offsets, obj,
              npos_total, ovl, threshold, neg_threshold, theta, reg, cls, flags, reg_weight,
-             focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool};
+             focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool, nullptr};
   dim3 grid((P + kLTile - 1) / kLTile, B);
   const size_t lds = static_cast<size_t>(kLTile) * C * sizeof(float);
   {
     KernelTimer kt("k_multibox", s, true);
+    a.span = kt.span();
 #define SBOD_MB(T, CM, CLS)                                                                       \
-  hipExtLaunchKernelGGL((k_multibox<T, CM, CLS>), grid, dim3(kLTile), lds, s, kt.start(), kt.stop(), 0, a, static_cast<const T *>(locs), \
+  tlaunch(kt, (k_multibox<T, CM, CLS>), grid, dim3(kLTile), lds, s, a, static_cast<const T *>(locs), \
                      static_cast<const T *>(scores), static_cast<T *>(grad_locs), static_cast<T *>(grad_scores))
     // rows of C <= CM classes in registers; wider rows take the LDS path
 #define SBOD_MB_C(T)                                                  \

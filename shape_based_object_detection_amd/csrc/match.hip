@@ -84,10 +84,11 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
     const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
     float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
     unsigned long long *__restrict__ part, int32_t *__restrict__ tcount, int32_t *__restrict__ npos,
-    int B) {
+    int B, unsigned long long *span) {
   extern __shared__ GtTile s_gt[];
   __shared__ unsigned long long s_key[kTile / 64][kMaxGLds];
   STAMP_BEGIN();
+  span_begin(span);
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) npos[B] = 0;  // phase 2 accumulates
   __shared__ int32_t s_lab[kMaxGLds];
   __shared__ int s_red[16];
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
     }
   }
   if (threadIdx.x == 0) tcount[b * ntile + blockIdx.x] = pos;
+  span_end(span);
   SEG_PHASE(3);
 #ifdef SBOD_PHASE_CLOCKS
   if (PHASE_PRINT_SEL)
@@ -487,14 +489,14 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
 #define SBOD_TILE(ODM, FL)                                                                      \
   do {                                                                                          \
     KernelTimer kt("k_match_tile", s, true);                                                          \
-    hipExtLaunchKernelGGL((k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, kt.start(), kt.stop(), 0, gt_boxes, gt_labels,   \
+    tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, gt_boxes, gt_labels,   \
                        gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, \
-                       ovl, w.part, w.tcount, n_pos, B);                                        \
+                       ovl, w.part, w.tcount, n_pos, B, kt.span());                              \
   } while (0)
 #define SBOD_FINAL(FL)                                                                          \
   do {                                                                                          \
     KernelTimer kt("k_match_final", s, true);                                                         \
-    hipExtLaunchKernelGGL((k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, kt.start(), kt.stop(), 0, gt_labels, gt_offsets, \
+    tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, gt_labels, gt_offsets, \
                        w.part, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B); \
   } while (0)
   if (odm) {

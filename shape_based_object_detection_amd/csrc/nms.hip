@@ -408,6 +408,7 @@ struct DetArgs {
   unsigned long long *cand;        // [B,C,P]
   uint32_t *cand_count;            // [B,C]
   float *dbg_probs, *dbg_boxes;
+  unsigned long long *span;        // KernelTimer span slot under graph capture, else null
 };
 
 // exp(x) and the logistic function on the hardware exp2 / rcp units (~1-2 ulp; the detect path's
@@ -448,6 +449,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   // sized to C so 6+ workgroups fit per CU (one round for B x ceil(P/256) workgroups at B=32)
   extern __shared__ float s_sc[];
   STAMP_BEGIN();
+  span_begin(a.span);
   const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
   const int P = a.P, C = a.C;
   unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_sc + kDTile * C);
@@ -595,6 +597,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
       for (int k = tid; k < np * C; k += kDTile) a.dbg_probs[rbase * C + k] = s_sc[k];
     }
   }
+  span_end(a.span);
   STAMP_END(1, 1);
 }
 #undef s_bal
@@ -1878,17 +1881,18 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   if (hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4, s) != hipSuccess)
     return launch_status("hipMemsetAsync(detect)");
   DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.boxes, ws.cand, ws.count,
-            debug_probs, debug_boxes};
+            debug_probs, debug_boxes, nullptr};
   {
     KernelTimer kt("k_det_prepare", s, true);
+    a.span = kt.span();
     const dim3 pg((P + kDTile - 1) / kDTile, B);
     const size_t pl = static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12;
-    if (C <= 8) hipExtLaunchKernelGGL(k_det_prepare<8>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
-    else if (C <= 16) hipExtLaunchKernelGGL(k_det_prepare<16>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
-    else if (C <= 24) hipExtLaunchKernelGGL(k_det_prepare<24>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
-    else if (C <= 32) hipExtLaunchKernelGGL(k_det_prepare<32>, pg, dim3(kDTile), pl, s, kt.start(), kt.stop(), 0, a, locs, scores);
-    else hipExtLaunchKernelGGL(k_det_prepare<0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
-                       static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, kt.start(), kt.stop(), 0, a, locs, scores);
+    if (C <= 8) tlaunch(kt, k_det_prepare<8>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 16) tlaunch(kt, k_det_prepare<16>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 24) tlaunch(kt, k_det_prepare<24>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 32) tlaunch(kt, k_det_prepare<32>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else tlaunch(kt, k_det_prepare<0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
+                 static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, locs, scores);
   }
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
@@ -1896,14 +1900,14 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     KernelTimer kt("k_det_segment", s, true);
     if (w1 <= 64)
 #ifdef SBOD_SEG_WAVE
-      hipExtLaunchKernelGGL(k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, kt.start(), kt.stop(), 0, ws.cand, ws.count, ws.boxes,
+      tlaunch(kt, k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, ws.boxes,
                          P, C, w1, w2, max_overlap, so, nullptr);
 #else
-      hipExtLaunchKernelGGL(k_det_segment_w4, dim3(C - 1, B), dim3(64 * kSegW), 0, s, kt.start(), kt.stop(), 0, ws.cand, ws.count, ws.boxes,
+      tlaunch(kt, k_det_segment_w4, dim3(C - 1, B), dim3(64 * kSegW), 0, s, ws.cand, ws.count, ws.boxes,
                          P, C, w1, w2, max_overlap, so);
 #endif
     else
-      hipExtLaunchKernelGGL(k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, kt.start(), kt.stop(), 0, ws.cand,
+      tlaunch(kt, k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
                          ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
   }
   SBOD_LAUNCHED("k_det_segment");
@@ -1912,7 +1916,7 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     // so the merge's dynamic LDS also covers one segment with window w2
     const size_t seg2 = two ? inline2_lds(w2) : 0;
     KernelTimer kt("k_det_merge", s, true);
-    hipExtLaunchKernelGGL(k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, kt.start(), kt.stop(), 0, ws.kept,
+    tlaunch(kt, k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, ws.kept,
                        ws.kc, ws.lastkey, ws.boxes, P, C, w2, w1, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
                        ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, ws.cand, ws.count,
                        max_overlap, so);

@@ -11,6 +11,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <tuple>
 
 #include "sbod.h"
 
@@ -51,13 +52,54 @@ class KernelTimer {
   KernelTimer &operator=(const KernelTimer &) = delete;
   hipEvent_t start() const { return attached_ ? start_ : nullptr; }
   hipEvent_t stop() const { return attached_ ? stop_ : nullptr; }
+  // Under hipGraph capture (where a dispatch cannot carry events and this runtime refuses
+  // external event nodes) a selected kernel instead gets a device span slot {first workgroup
+  // start, last workgroup end} in s_memrealtime ticks, written by the kernel itself
+  // (span_begin / span_end) on every replay; nullptr when not selected.
+  unsigned long long *span() const { return span_; }
 
  private:
   const char *name_;
   hipStream_t stream_;
   bool attached_;
   hipEvent_t start_ = nullptr, stop_ = nullptr;
+  unsigned long long *span_ = nullptr;
 };
+
+// Kernel-side span recording (see KernelTimer::span).  span_end synchronises the workgroup and
+// must be reached by all of its threads; the fence makes the block's stores complete before the
+// end stamp, so the span covers the write drain like a dispatch's completion signal does.
+__device__ __forceinline__ void span_begin(unsigned long long *span) {
+  if (span != nullptr && threadIdx.x == 0)
+    atomicMin(span, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+}
+__device__ __forceinline__ void span_end(unsigned long long *span) {
+  if (span == nullptr) return;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(span + 1, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+}
+
+// Launch through a KernelTimer: a timed launch carries the timer's events on the dispatch
+// (hipExtLaunchKernel); an untimed one is a plain hipLaunchKernel, the form stream capture
+// records into a hipGraph kernel node.  Arguments are converted to the kernel's parameter types
+// first, as the triple-chevron launch does.
+template <typename... KArgs, typename... Args>
+inline void tlaunch(const KernelTimer &kt, void (*kernel)(KArgs...), dim3 grid, dim3 block,
+                    size_t lds, hipStream_t s, Args... args) {
+  static_assert(sizeof...(KArgs) == sizeof...(Args), "tlaunch: argument count");
+  auto conv = std::tuple<KArgs...>{static_cast<KArgs>(args)...};
+  void *a[sizeof...(KArgs) > 0 ? sizeof...(KArgs) : 1];
+  std::apply([&a](auto &...v) {
+    int i = 0;
+    ((a[i++] = static_cast<void *>(&v)), ...);
+  }, conv);
+  const void *k = reinterpret_cast<const void *>(kernel);
+  if (kt.start())
+    (void)hipExtLaunchKernel(k, grid, block, a, lds, s, kt.start(), kt.stop(), 0);
+  else
+    (void)hipLaunchKernel(k, grid, block, a, lds, s);
+}
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 

@@ -2,7 +2,9 @@
 
 ``find_jaccard_overlap`` (metrics.py:208-252) is the IoU every criterion and the mAP use:
 inner / (gt_area + anchor_area - inner + 1e-5), GT with |w|,|h| < 1e-5 -> 0, anchors with
-w,h < 1e-5 -> -1 (applied last).  Bit-exact with the reference's CPU path.
+w,h < 1e-5 -> -1 (applied last).  Bit-exact with the reference's CPU path.  Device tensors run
+the HIP kernel; CPU tensors (DataLoader workers: random_crop, dataset/transforms.py:175-176) run
+the host path in ``host.py``.
 ``calculate_mAP`` (metrics.py:8-145): VOC 11-point mAP on the device —
 sorts, per-(class, image) greedy TP/FP assignment and per-class AP kernels (csrc/map.hip),
 one host sync for the returned Python values, like the reference's ``.item()``/``.tolist()``.
@@ -11,8 +13,34 @@ import torch
 
 from . import _lib as L
 from . import core
+from . import host
 
 _RTHR = {}
+_ONE_IMAGE_OFFSETS = {}
+
+
+def _one_image_offsets(G, device):
+    """gt_offsets [0, G] of a single-image call, cached per (G, device)."""
+    key = (G, str(device))
+    t = _ONE_IMAGE_OFFSETS.get(key)
+    if t is None:
+        if len(_ONE_IMAGE_OFFSETS) > 1024:
+            _ONE_IMAGE_OFFSETS.clear()
+        t = torch.tensor([0, G], dtype=torch.int32).pin_memory().to(device, non_blocking=True)
+        _ONE_IMAGE_OFFSETS[key] = t
+    return t
+
+
+def on_host(*tensors):
+    """True when every tensor is a CPU tensor (the host path); False when all are on the device;
+    mixed devices raise as torch's own ops would."""
+    cpu = [not t.is_cuda for t in tensors]
+    if all(cpu):
+        return True
+    if any(cpu):
+        raise RuntimeError('Expected all tensors to be on the same device, got %s'
+                           % [str(t.device) for t in tensors])
+    return False
 
 
 def _single(gt, anchors, mode, what):
@@ -22,18 +50,21 @@ def _single(gt, anchors, mode, what):
     G, P = g.shape[0], a.shape[0]
     if G == 0 or P == 0:
         return torch.zeros(G, P, dtype=torch.float32, device=g.device)
-    pack = core.GtPack(g, torch.zeros(G, dtype=torch.int64, device=g.device),
-                       core._offsets_tensor([G], g.device), [G])
+    pack = core.GtPack(g, None, _one_image_offsets(G, g.device), [G])
     return core.iou_pairwise(pack, a, mode=mode)[0]
 
 
 def find_jaccard_overlap(gt_boxes, anchors):
     """[G, P] IoU of metrics.py:208-252."""
+    if on_host(gt_boxes, anchors):
+        return host.find_jaccard_overlap(gt_boxes, anchors)
     return _single(gt_boxes, anchors, L.IOU_METRICS, 'find_jaccard_overlap')
 
 
 def intersect(box_a, box_b):
     """[A, B] intersection areas (metrics.py:192-205)."""
+    if on_host(box_a, box_b):
+        return host.intersect(box_a, box_b)
     return _single(box_a, box_b, L.IOU_INTER, 'intersect')
 
 

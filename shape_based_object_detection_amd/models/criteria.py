@@ -13,8 +13,12 @@ Returns a 0-d loss tensor with autograd.  ``last_components`` holds the device v
 {total, conf, loc, n_pos} of the last call (no sync).
 
 Data parallelism: set ``distributed = True`` (optionally ``process_group``) and every rank
-normalises by the all-reduced positive count, so summing model gradients over ranks gives the
-single-device batch gradient.
+normalises by the all-reduced positive count, so a rank's share of the loss is
+exactly its images' part of the single-device batch loss and the SUM of the ranks' gradients is
+the single-device batch gradient.  DDP AVERAGES gradients over ranks, so with the default
+``grad_reduction = 'mean'`` each rank returns world_size x its share (the mean of the returned
+values over ranks is the single-device loss, and DDP's averaged gradient is the single-device
+gradient).  Set ``grad_reduction = 'sum'`` for a trainer that sums gradients instead.
 """
 import torch
 from torch import nn
@@ -45,6 +49,7 @@ class _AnchorCriterion(nn.Module):
         self.config = config
         self.distributed = False
         self.process_group = None
+        self.grad_reduction = 'mean'
         self.last_components = None
 
     def increase_threshold(self, increment=0.1):
@@ -93,7 +98,18 @@ class _AnchorCriterion(nn.Module):
                                            self.priors_cxcy, spec, self.threshold,
                                            self.threshold - 0.1, exchange=exchange)
         self.last_components = comps
+        return _dp_scale(self, loss)
+
+
+def _dp_scale(crit, loss):
+    """Data parallel with a gradient-AVERAGING trainer (DDP): world_size x this rank's share."""
+    if not crit.distributed or crit.grad_reduction == 'sum':
         return loss
+    if crit.grad_reduction != 'mean':
+        raise ValueError("grad_reduction must be 'mean' or 'sum', got %r" % (crit.grad_reduction,))
+    import torch.distributed as dist
+    world = dist.get_world_size(crit.process_group)
+    return loss * world if world > 1 else loss
 
 
 class MultiBoxLoss512(_AnchorCriterion):
@@ -130,6 +146,7 @@ class RefineDetLoss(nn.Module):
         self.theta = theta
         self.distributed = False
         self.process_group = None
+        self.grad_reduction = 'mean'
         self.last_components = None
 
     def increase_threshold(self, increment=0.05):
@@ -179,7 +196,7 @@ class RefineDetLoss(nn.Module):
         arm = self.compute_arm_loss(arm_locs, arm_scores, boxes, labels)
         odm = self.compute_odm_loss(arm_locs.detach(), arm_scores.detach(), odm_locs, odm_scores,
                                     boxes, labels)
-        return arm + odm
+        return _dp_scale(self, arm + odm)
 
 
 def criterion_entry(arch):

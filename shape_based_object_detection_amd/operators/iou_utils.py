@@ -6,12 +6,17 @@
     ``intersect`` / ``jaccard`` (:192-233), ``match`` / ``match_ious`` (:236-321, in place into
     ``loc_t[idx]`` / ``conf_t[idx]``), ``encode`` / ``decode`` (:324-368), ``log_sum_exp`` (:371-379),
     ``nms`` / ``diounms`` (:385-530: (keep, count), or the bare zero ``keep`` for empty input).
+Device tensors run the HIP kernels.  CPU tensors run the host path (``host.py``) for the box
+utilities the data-loader side uses (point_form, intersect, jaccard, encode, decode); the rest
+is device-only and raises on CPU tensors.
 """
 import torch
 
 from .. import _lib as L
 from .. import core
+from .. import host
 from .. import metrics as _metrics
+from ..metrics import on_host
 
 
 def _overlaps(kind, bboxes1, bboxes2):
@@ -44,6 +49,8 @@ def bbox_overlaps_giou(bboxes1, bboxes2):
 
 def point_form(boxes):
     """(cx, cy, w, h) -> (xmin, ymin, xmax, ymax)."""
+    if on_host(boxes):
+        return host.point_form(boxes)
     L.require_device(boxes, what='point_form')
     return core.codec('cxcy_to_xy', boxes.float())
 
@@ -62,6 +69,8 @@ def intersect(box_a, box_b):
 
 def jaccard(box_a, box_b):
     """[A, B] plain IoU (no EPS, no degenerate masks)."""
+    if on_host(box_a, box_b):
+        return host.jaccard(box_a, box_b)
     return _metrics._single(box_a, box_b, L.IOU_PLAIN, 'jaccard')
 
 
@@ -92,11 +101,15 @@ def match(threshold, truths, priors, variances, labels, loc_t, conf_t, idx):
 
 
 def encode(matched, priors, variances):
+    if on_host(matched, priors):
+        return host.encode(matched, priors, variances)
     L.require_device(matched, priors, what='encode')
     return core.codec('encode_var', matched.float(), priors.float(), var=variances)
 
 
 def decode(loc, priors, variances):
+    if on_host(loc, priors):
+        return host.decode(loc, priors, variances)
     L.require_device(loc, priors, what='decode')
     return core.codec('decode_var', loc.float(), priors.float(), var=variances)
 

@@ -1,0 +1,182 @@
+"""Device-side ground-truth packing and the hipGraph-captured step.
+
+  * sbod_gt_pack (one launch, pointers in the kernel arguments) == torch.cat of the lists, and
+    GtStaging's device-list and host-list paths fill identical fixed-capacity buffers;
+  * a criterion forward+backward + detect captured with torch.cuda.graph and replayed gives the
+    eager results bit for bit, also after the staged ground truth changes between replays (the
+    graph reads the fixed-capacity buffers, not the capture-time lists);
+  * a timed kernel inside the capture stamps its own span slot on every replay.
+"""
+import numpy as np
+import pytest
+import torch
+
+from shape_based_object_detection_amd import _lib as L
+from shape_based_object_detection_amd import core, synth
+from shape_based_object_detection_amd.models import criteria as CR
+from shape_based_object_detection_amd.models.priors import prior_table
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda', 0)
+
+
+class Cfg(dict):
+    __getattr__ = dict.__getitem__
+
+
+def test_gt_pack_matches_cat():
+    boxes, labels = synth.make_gt(37, seed=4)           # > 1 chunk? no: 37 < 64; still ragged
+    boxes += [torch.zeros(0, 4)]                         # an empty image is packed as 0 rows
+    labels += [torch.zeros(0, dtype=torch.int64)]
+    bx = [b.to(DEV) for b in boxes]
+    lb = [l.to(DEV) for l in labels]
+    gt = core.pack_gt(bx, lb, allow_empty=True)
+    torch.testing.assert_close(gt.boxes, torch.cat(bx), rtol=0, atol=0)
+    assert torch.equal(gt.labels, torch.cat(lb))
+    offs = np.concatenate([[0], np.cumsum([b.shape[0] for b in boxes])]).astype(np.int32)
+    np.testing.assert_array_equal(gt.offsets.cpu().numpy(), offs)
+
+
+def test_gt_pack_many_images_chunks():
+    boxes, labels = synth.make_gt(150, seed=8)          # 3 launches of <= 64 images
+    bx = [b.to(DEV) for b in boxes]
+    lb = [l.to(DEV) for l in labels]
+    gt = core.pack_gt(bx, lb)
+    assert torch.equal(gt.boxes, torch.cat(bx)) and torch.equal(gt.labels, torch.cat(lb))
+    offs = np.concatenate([[0], np.cumsum([b.shape[0] for b in boxes])]).astype(np.int32)
+    np.testing.assert_array_equal(gt.offsets.cpu().numpy(), offs)
+
+
+def test_staging_device_and_host_paths_agree():
+    boxes, labels = synth.make_gt(16, seed=21)
+    st_d = core.GtStaging(16, 16, DEV)
+    st_h = core.GtStaging(16, 16, DEV)
+    gd = st_d.stage([b.to(DEV) for b in boxes], [l.to(DEV) for l in labels])
+    gh = st_h.stage(boxes, labels)                      # CPU lists: pinned pack + one copy
+    n = sum(b.shape[0] for b in boxes)
+    torch.cuda.synchronize()
+    assert gd.gmax == gh.gmax == 16
+    assert torch.equal(gd.boxes[:n], gh.boxes[:n]) and torch.equal(gd.labels[:n], gh.labels[:n])
+    assert torch.equal(gd.offsets, gh.offsets)
+    assert torch.equal(gd.boxes[:n].cpu(), torch.cat(boxes))
+    with pytest.raises(ValueError):
+        big, bl = synth.make_gt(16, seed=1, max_objects=40)
+        st_d.stage([b.to(DEV) for b in big] * 1, [l.to(DEV) for l in bl])
+
+
+def _setup(B=8, seed=31):
+    P = torch.from_numpy(prior_table('SSD512')).to(DEV)
+    cfg = Cfg(reg_weights=1.0, device=DEV, n_classes=21, reg_loss='diou', cls_loss='focal')
+    crit = CR.MultiBoxLoss512(priors_cxcy=P, config=cfg)
+    locs, scores = synth.make_preds(B, P.shape[0], 21, seed=seed)
+    det = scores.clone()
+    det[:, :, 0] += 6.0
+    return P, crit, locs.to(DEV).requires_grad_(True), scores.to(DEV).requires_grad_(True), det.to(DEV)
+
+
+def _gt(B, seed):
+    boxes, labels = synth.make_gt(B, seed=seed)
+    return [b.to(DEV) for b in boxes], [l.to(DEV) for l in labels]
+
+
+def _eager(P, crit, locs, scores, det, gt):
+    locs.grad = None
+    scores.grad = None
+    loss = crit(locs, scores, gt[0], gt[1])
+    res = core.detect(locs.detach(), det, 0.01, 0.45, 200, P)
+    loss.backward()
+    return loss.item(), locs.grad.clone(), scores.grad.clone(), res
+
+
+def _same_det(a, b):
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+
+
+def test_graph_replay_equals_eager():
+    B = 8
+    P, crit, locs, scores, det = _setup(B)
+    stage = core.GtStaging(B, 16, DEV)
+    side = torch.cuda.Stream()
+    ds = torch.cuda.Stream()
+
+    def body(gt, capture):
+        loss = crit(locs, scores, gt, None)
+        cur = torch.cuda.current_stream()
+        ds.wait_stream(cur)
+        with torch.cuda.stream(ds):
+            h = core.detect(locs.detach(), det, 0.01, 0.45, 200, P, async_=True, capture=capture)
+        loss.backward()
+        cur.wait_stream(ds)
+        return loss, h
+
+    gt1 = _gt(B, 100)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):                      # warm-up (lazy state) off the capture stream
+        for _ in range(2):
+            locs.grad = None
+            scores.grad = None
+            _, h = body(stage.stage(*gt1), False)
+            h.wait()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    locs.grad = None
+    scores.grad = None
+    g = torch.cuda.CUDAGraph()
+    pack = stage.stage(*gt1)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        g_loss, g_h = body(pack, True)
+    g_gl, g_gs = locs.grad, scores.grad
+    for seed in (100, 200, 300):                         # new ground truth every replay
+        gt = _gt(B, seed)
+        stage.stage(*gt)
+        g.replay()
+        res = g_h.replayed().wait()
+        gl, gs = g_gl.clone(), g_gs.clone()
+        lv = g_loss.item()
+        e_loss, e_gl, e_gs, e_res = _eager(P, crit, locs, scores, det, gt)
+        assert lv == e_loss
+        assert torch.equal(gl, e_gl) and torch.equal(gs, e_gs)
+        _same_det(res, e_res)
+        locs.grad, scores.grad = g_gl, g_gs
+
+
+def test_graph_span_timing():
+    """A timed kernel captured into a graph stamps its own span slot on every replay."""
+    B = 4
+    P, crit, locs, scores, det = _setup(B, seed=5)
+    gt = _gt(B, 7)
+    stage = core.GtStaging(B, 16, DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            locs.grad = None
+            crit(locs, scores, stage.stage(*gt), None).backward()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    L.timing_enable('k_multibox')
+    g = torch.cuda.CUDAGraph()
+    locs.grad = None
+    scores.grad = None
+    with torch.cuda.graph(g):
+        loss = crit(locs, scores, stage.stage(*gt), None)
+        loss.backward()
+    L.timing_enable(None)
+    assert L.timing_query('k_multibox')[0] == 0          # armed nothing yet / never replayed
+    times = []
+    for _ in range(3):
+        L.call('sbod_timing_arm')
+        g.replay()
+        torch.cuda.synchronize()
+        n, ms = L.timing_query('k_multibox')
+        assert n == 1
+        times.append(ms)
+    L.call('sbod_timing_arm')
+    assert L.timing_query('k_multibox')[0] == 0          # armed, not replayed since
+    assert all(0.0005 < t < 5.0 for t in times), times
+    del g
+    L.call('sbod_timing_reset_graphs')
