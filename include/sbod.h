@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SBOD_ABI_VERSION 1
+#define SBOD_ABI_VERSION 2
 
 typedef enum sbod_status {
   SBOD_OK = 0,
@@ -57,13 +57,12 @@ int sbod_timing_query(const char *kernel, int *launches, double *total_ms);
 int sbod_timing_every(int n);
 /* Under hipGraph stream capture a dispatch cannot carry events (and this runtime refuses
  * external event nodes): a selected HBM-bound kernel (k_match_tile, k_multibox, k_det_prepare)
- * is instead captured with a device span slot that the kernel itself writes on every replay —
- * its first workgroup's start and last workgroup's end (after the block's stores have drained),
- * in s_memrealtime ticks.  sbod_timing_arm() resets the slots (host-synchronous; call it between
- * replays), and sbod_timing_query() then reports the span of the replay since the last arm.
- * The capture records survive sbod_timing_enable(); sbod_timing_reset_graphs() releases the
- * slots once the graphs holding them are gone. */
-int sbod_timing_arm(void);
+ * is instead captured with a device span record that the kernel itself overwrites on every
+ * replay — each workgroup's start, and its end after its stores are acknowledged, in
+ * s_memrealtime ticks (plain per-workgroup stores: no atomics, no host writes between
+ * replays).  sbod_timing_query() then reports the latest completed replay's first-start to
+ * last-end span.  The capture records survive sbod_timing_enable();
+ * sbod_timing_reset_graphs() releases (and clears) them once the graphs holding them are gone. */
 double sbod_timing_clock_hz(void);   /* the span clock (hipDeviceAttributeWallClockRate) */
 int sbod_timing_reset_graphs(void);
 
@@ -247,15 +246,21 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
  *   outputs are observable, so NMS runs on each class's best `window` candidates; when a
  *   candidate outside a truncated window could still reach the output, det_count[b] = -1 and the
  *   caller re-runs with a larger window (results never depend on the window size).
+ *   flags: SBOD_DETECT_COUNTERS_ZEROED — the caller guarantees that the workspace's first
+ *   sbod_detect_counter_bytes(B, C) bytes are zero on entry (e.g. the workspace was allocated
+ *   zeroed); every call leaves them zero again, so repeated calls (and a captured hipGraph)
+ *   need no memset.  Without the flag the call zeroes them itself (one memset).
  * Workspace: sbod_detect_workspace_bytes(B, P, C). */
 enum { SBOD_BOX_OFFSET = 0, SBOD_BOX_CENTER = 1, SBOD_BOX_CORNER = 2 };
+enum { SBOD_DETECT_COUNTERS_ZEROED = 1 };
+size_t sbod_detect_counter_bytes(int B, int C);
 enum { SBOD_ACT_SOFTMAX = 0, SBOD_ACT_SIGMOID = 1 };
 size_t sbod_detect_workspace_bytes(int B, int P, int C);
 int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                     const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
                     float min_score, float max_overlap, int top_k, float final_nms, int window,
-                    float *det_boxes, int64_t *det_labels, float *det_scores, int32_t *det_count,
-                    float *debug_probs, float *debug_boxes, void *workspace,
+                    int flags, float *det_boxes, int64_t *det_labels, float *det_scores,
+                    int32_t *det_count, float *debug_probs, float *debug_boxes, void *workspace,
                     size_t workspace_bytes, void *stream);
 
 /* Single-segment greedy NMS (iou_utils.nms / diounms, iou_utils.py:385-530; torchvision.ops.nms).

@@ -1,7 +1,7 @@
 """Diagnostic: the bench step captured into a hipGraph, replayed with progress output per
 replay, in stages (mode argument):
   single       one-stream capture of criterion fwd + detect + backward, no timing
-  single_span  the same with the dominant kernel's span slot armed and read every replay
+  single_span  the same with the dominant kernel's span record read back every replay
 Prints one line per replay (flushed) so a fault names the replay it happened in."""
 import os
 import sys
@@ -38,8 +38,6 @@ st.capture()
 L.timing_enable(None)
 print('captured', flush=True)
 for i in range(12):
-    if mode == 'single_span':
-        L.call('sbod_timing_arm')
     loss, res = st()
     msg = 'replay %d loss %.6f n_det %d' % (i, loss.item(), sum(int(x.shape[0]) for x in res[0]))
     if mode == 'single_span':

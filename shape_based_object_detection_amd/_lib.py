@@ -43,8 +43,9 @@ SIGNATURES = {
     'sbod_smooth_l1_f32': (I32, [P, P, I64, F32, P, P, P]),
     'sbod_focal_f32': (I32, [I32, P, P, I64, I32, F32, F32, F32, P, P, P]),
     'sbod_detect_workspace_bytes': (SZ, [I32, I32, I32]),
-    'sbod_detect_f32': (I32, [P, P, I32, I32, I32, P, P, I32, I32, F32, F32, I32, F32, I32, P, P, P,
-                              P, P, P, P, SZ, P]),
+    'sbod_detect_counter_bytes': (SZ, [I32, I32]),
+    'sbod_detect_f32': (I32, [P, P, I32, I32, I32, P, P, I32, I32, F32, F32, I32, F32, I32, I32, P, P,
+                              P, P, P, P, P, SZ, P]),
     'sbod_nms_workspace_bytes': (SZ, [I64]),
     'sbod_nms_f32': (I32, [P, P, I64, F32, I32, I32, F32, P, P, P, SZ, P]),
     'sbod_map_workspace_bytes': (SZ, [I64, I64]),
@@ -53,7 +54,6 @@ SIGNATURES = {
     'sbod_timing_query': (I32, [ctypes.c_char_p, P, P]),
     'sbod_timing_every': (I32, [I32]),
     'sbod_timing_reset_graphs': (I32, []),
-    'sbod_timing_arm': (I32, []),
     'sbod_timing_clock_hz': (ctypes.c_double, []),
     'sbod_memcpy_d2h_async': (I32, [P, P, SZ, P]),
     'sbod_gt_pack': (I32, [P, P, P, I32, I64, P, P, P, P]),
@@ -79,6 +79,7 @@ FOCAL = dict(softmax=0, sigmoid=1, bce=2)
 BOX = dict(offset=0, center=1, corner=2)
 ACT = dict(softmax=0, sigmoid=1)
 NMS = dict(tv=0, ref=1, diou=2)
+DETECT_COUNTERS_ZEROED = 1
 
 
 class SbodError(RuntimeError):

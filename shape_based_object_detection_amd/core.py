@@ -177,7 +177,16 @@ def workspace(nbytes, device, slot='default'):
     buf = _WS.get(key)
     n = max(int(nbytes), 1)
     if buf is None or buf.numel() < n:
+        if dev.type == 'cuda' and torch.cuda.is_current_stream_capturing():
+            # a workspace first allocated under hipGraph capture has faulted replays on this
+            # runtime: the caller warms up on the capture stream so it exists beforehand
+            raise L.SbodError('sbod workspace %r (%d bytes) would be allocated under hipGraph capture: '
+                              'run the same calls once on the capture stream before capturing'
+                              % (slot, n))
+        if buf is not None:
+            _DET_CLEAN.pop(buf.data_ptr(), None)   # its memory returns to the allocator
         buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=dev)
+        _DET_CLEAN.pop(buf.data_ptr(), None)
         _WS[key] = buf
     return buf
 
@@ -449,13 +458,29 @@ def _count_slot(dev, B):
     return torch.empty(B, dtype=torch.int32, pin_memory=True), torch.cuda.Event()
 
 
+# Detect workspaces whose candidate counters are known to be zero: data_ptr -> bytes.  Every
+# sbod_detect_f32 call leaves its counters zero, so after the first call on a workspace no memset
+# is needed (none in a captured graph: SBOD_DETECT_COUNTERS_ZEROED).
+_DET_CLEAN = {}
+
+
 def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn, out,
                    dbg, ws, nb, window):
     out_b, out_l, out_s, cnt = out
+    need = L.lib().sbod_detect_counter_bytes(B, C)
+    flags = 0
+    if _DET_CLEAN.get(ws.data_ptr(), 0) >= need:
+        flags = L.DETECT_COUNTERS_ZEROED
+    elif torch.cuda.is_current_stream_capturing():
+        raise L.SbodError('detect under hipGraph capture: run it once on the capture stream with this '
+                          'batch shape first (its workspace counters are not known to be zero)')
     L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
-           L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(window), L.ptr(out_b),
-           L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg[0]), L.ptr(dbg[1]), L.ptr(ws), nb,
-           L.stream_of(sc))
+           L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(window), flags,
+           L.ptr(out_b), L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg[0]), L.ptr(dbg[1]),
+           L.ptr(ws), nb, L.stream_of(sc))
+    # only this call's prefix is known clean: a call with a smaller B * C writes other regions
+    # over the rest of a larger one's counters
+    _DET_CLEAN[ws.data_ptr()] = need
 
 
 def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='offset',

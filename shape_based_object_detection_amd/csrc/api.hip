@@ -79,11 +79,12 @@ struct TimingRec {
   bool graph;   // captured into a hipGraph: the kernel writes span slot `slot` on every replay
   int slot;
 };
-// Device span slots for kernels captured into graphs: {start, end} u64 pairs in s_memrealtime
-// ticks (100 MHz).  Allocated by sbod_timing_enable (never under capture).
-constexpr int kSpanSlots = 256;
+// Span rings for kernels captured into graphs (SpanRing: per-launch {start, end} in
+// s_memrealtime ticks, written by the kernel).  Allocated and initialised by
+// sbod_timing_enable, never under capture; the host only reads them afterwards.
+constexpr int kSpanSlots = 8;   // captured timed kernels (each record ~256 KB)
 double g_realtime_hz = 100.0e6;   // replaced by hipDeviceAttributeWallClockRate at allocation
-unsigned long long *g_span_dev = nullptr;
+SpanRing *g_span_dev = nullptr;
 int g_span_next = 0;
 std::vector<TimingRec> g_recs;
 int g_every = 1;                                  // time one launch in g_every (per kernel name)
@@ -112,7 +113,7 @@ KernelTimer::KernelTimer(const char *name, hipStream_t s, bool attached)
     attached_ = false;
     if (g_span_dev != nullptr && g_span_next < kSpanSlots) {
       const int slot = g_span_next++;
-      span_ = g_span_dev + 2 * slot;
+      span_ = g_span_dev + slot;
       g_recs.push_back({name, nullptr, nullptr, true, slot});
     }
     return;
@@ -158,10 +159,10 @@ int sbod_timing_enable(const char *kernel_filter) {
   sbod::g_seen.clear();
   sbod::g_filter = kernel_filter ? kernel_filter : "";
   if (!sbod::g_filter.empty() && sbod::g_span_dev == nullptr &&
-      (hipMalloc(reinterpret_cast<void **>(&sbod::g_span_dev), sbod::kSpanSlots * 16) != hipSuccess ||
-       hipMemset(sbod::g_span_dev, 0, sbod::kSpanSlots * 16) != hipSuccess)) {
+      (hipMalloc(reinterpret_cast<void **>(&sbod::g_span_dev), sizeof(sbod::SpanRing) * sbod::kSpanSlots) != hipSuccess ||
+       hipMemset(sbod::g_span_dev, 0, sizeof(sbod::SpanRing) * sbod::kSpanSlots) != hipSuccess)) {
     sbod::g_span_dev = nullptr;
-    return sbod::launch_status("sbod_timing_enable(span slots)");
+    return sbod::launch_status("sbod_timing_enable(span records)");
   }
   if (!sbod::g_filter.empty()) {
     int dev = 0, khz = 0;
@@ -174,19 +175,6 @@ int sbod_timing_enable(const char *kernel_filter) {
 
 double sbod_timing_clock_hz(void) { return sbod::g_realtime_hz; }
 
-int sbod_timing_arm(void) {
-  std::lock_guard<std::mutex> g(sbod::g_tmu);
-  if (sbod::g_span_dev == nullptr || sbod::g_span_next == 0) return SBOD_OK;
-  std::vector<unsigned long long> init(2 * sbod::g_span_next);
-  for (int i = 0; i < sbod::g_span_next; ++i) {
-    init[2 * i] = ~0ull;
-    init[2 * i + 1] = 0ull;
-  }
-  if (hipMemcpy(sbod::g_span_dev, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
-    return sbod::launch_status("sbod_timing_arm");
-  return SBOD_OK;
-}
-
 int sbod_timing_reset_graphs(void) {
   std::lock_guard<std::mutex> g(sbod::g_tmu);
   std::vector<sbod::TimingRec> keep;
@@ -194,6 +182,9 @@ int sbod_timing_reset_graphs(void) {
     if (!r.graph) keep.push_back(r);
   sbod::g_recs.swap(keep);
   sbod::g_span_next = 0;   // the graphs holding the span pointers must be gone
+  if (sbod::g_span_dev != nullptr &&   // no stale record can be read for a slot handed out again
+      hipMemset(sbod::g_span_dev, 0, sizeof(sbod::SpanRing) * sbod::kSpanSlots) != hipSuccess)
+    return sbod::launch_status("sbod_timing_reset_graphs");
   return SBOD_OK;
 }
 
@@ -212,12 +203,23 @@ int sbod_timing_query(const char *kernel, int *launches, double *total_ms) {
   double tot = 0.0;
   for (auto &r : sbod::g_recs) {
     if (std::strcmp(r.name, kernel) != 0) continue;
-    if (r.graph) {   // span slot of the last replay since sbod_timing_arm()
-      unsigned long long v[2] = {0ull, 0ull};
-      if (hipMemcpy(v, sbod::g_span_dev + 2 * r.slot, 16, hipMemcpyDeviceToHost) != hipSuccess)
+    if (r.graph) {   // the latest completed launch of the captured kernel (read only)
+      sbod::SpanRing *d = sbod::g_span_dev + r.slot;
+      unsigned long long nb = 0;
+      if (hipMemcpy(&nb, &d->nblocks, 8, hipMemcpyDeviceToHost) != hipSuccess)
         return sbod::launch_status("sbod_timing_query(span)");
-      if (v[0] == ~0ull || v[1] == 0ull || v[1] == ~0ull || v[1] < v[0]) continue;   // not run since the last arm
-      tot += static_cast<double>(v[1] - v[0]) / sbod::g_realtime_hz * 1e3;
+      if (nb == 0 || nb > (1ull << 31)) continue;   // never replayed
+      const size_t nr = nb < static_cast<unsigned long long>(sbod::kSpanBlocks) ? nb : sbod::kSpanBlocks;
+      std::vector<unsigned long long> t(2 * nr);
+      if (hipMemcpy(t.data(), d->t, 16 * nr, hipMemcpyDeviceToHost) != hipSuccess)
+        return sbod::launch_status("sbod_timing_query(span)");
+      unsigned long long lo = ~0ull, hi = 0ull;
+      for (size_t i = 0; i < nr; ++i) {
+        lo = t[2 * i] < lo ? t[2 * i] : lo;
+        hi = t[2 * i + 1] > hi ? t[2 * i + 1] : hi;
+      }
+      if (hi <= lo) continue;
+      tot += static_cast<double>(hi - lo) / sbod::g_realtime_hz * 1e3;
       ++n;
       continue;
     }

@@ -283,7 +283,7 @@ struct LossArgs {
   int reg, cls, flags;
   float reg_weight, afg, abg, gamma;
   float *partials, *pool;
-  unsigned long long *span;   // KernelTimer span slot under graph capture, else null
+  SpanRing *span;             // KernelTimer span ring under graph capture, else null
 };
 
 // exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'

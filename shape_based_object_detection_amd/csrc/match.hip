@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kTile) void k_match_tile(
     const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
     float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
     unsigned long long *__restrict__ part, int32_t *__restrict__ tcount, int32_t *__restrict__ npos,
-    int B, unsigned long long *span) {
+    int B, SpanRing *span) {
   extern __shared__ GtTile s_gt[];
   __shared__ unsigned long long s_key[kTile / 64][kMaxGLds];
   STAMP_BEGIN();

@@ -408,7 +408,7 @@ struct DetArgs {
   unsigned long long *cand;        // [B,C,P]
   uint32_t *cand_count;            // [B,C]
   float *dbg_probs, *dbg_boxes;
-  unsigned long long *span;        // KernelTimer span slot under graph capture, else null
+  SpanRing *span;                  // KernelTimer span ring under graph capture, else null
 };
 
 // exp(x) and the logistic function on the hardware exp2 / rcp units (~1-2 ulp; the detect path's
@@ -566,8 +566,9 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
       const float pc = softmax ? fast_exp(row[c] - m) * rs : fast_sigmoid(row[c]);
       // (plain store: these 8-byte scattered writes must merge into full lines in L2 first —
       // streamed through they cost 1.7x the kernel time)
-      a.cand[(static_cast<int64_t>(b) * C + c) * P + s_wb(wv, c) + __popcll(bal & lt)] =
-          make_key(pc, static_cast<uint32_t>(p));
+      const uint32_t slot = s_wb(wv, c) + __popcll(bal & lt);
+      if (slot < static_cast<uint32_t>(P))   // always, with counters zero on entry (memory-safe otherwise)
+        a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(pc, static_cast<uint32_t>(p));
     }
   } else {
     SEG_PHASE(2);
@@ -581,8 +582,9 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     for (int c = 1; c < C; ++c) {
       const unsigned long long bal = s_bal(wv, c);
       if (!((bal >> lane) & 1ull)) continue;
-      a.cand[(static_cast<int64_t>(b) * C + c) * P + s_wb(wv, c) + __popcll(bal & lt)] =
-          make_key(row[c], static_cast<uint32_t>(p));
+      const uint32_t slot = s_wb(wv, c) + __popcll(bal & lt);
+      if (slot < static_cast<uint32_t>(P))
+        a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(row[c], static_cast<uint32_t>(p));
     }
   }
   SEG_PHASE(4);
@@ -624,7 +626,7 @@ __device__ void segment_body(const unsigned long long *cand, const uint32_t *can
   int &s_nk = *s_nk_p;
   int &s_cnt = *s_cnt_p;
   const int64_t seg = static_cast<int64_t>(b) * C + c;
-  const int n = static_cast<int>(cand_count[seg]);
+  const int n = min(static_cast<int>(cand_count[seg]), P);   // counters never exceed P
   const unsigned long long *g = cand + seg * P;
   const int q = min(n, window);
   // LDS: raw keys [kSegSortCap] | window keys [pow2(window)] | boxes, areas, klist, keep, matrix
@@ -743,7 +745,7 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
   const int c = blockIdx.x + 1, b = blockIdx.y;
   const int64_t seg = static_cast<int64_t>(b) * C + c;
   if (need != nullptr && (need[b] == 0 || o.lastkey[seg] == 0ull)) return;
-  const int n = static_cast<int>(cand_count[seg]);
+  const int n = min(static_cast<int>(cand_count[seg]), P);   // counters never exceed P
   if (n == 0) {
     if (lane == 0) {
       o.kc[seg] = 0;
@@ -959,7 +961,7 @@ __global__ __launch_bounds__(64 * kSegW) void k_det_segment_w4(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int c = blockIdx.x + 1, b = blockIdx.y;
   const int64_t seg = static_cast<int64_t>(b) * C + c;
-  const int n = static_cast<int>(cand_count[seg]);
+  const int n = min(static_cast<int>(cand_count[seg]), P);   // counters never exceed P
   if (n == 0) {
     if (tid == 0) {
       o.kc[seg] = 0;
@@ -1716,15 +1718,24 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     const float *__restrict__ boxes_ws, int P, int C, int window, int wfirst, int top_k, float final_nms,
     int general, int pass, int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
-    int32_t *__restrict__ out_count, const unsigned long long *cand, const uint32_t *cand_count, float thr,
+    int32_t *__restrict__ out_count, const unsigned long long *cand, uint32_t *cand_count, float thr,
     SegOut so) {
   extern __shared__ unsigned char s_raw[];
   STAMP_BEGIN();
+  const int b = blockIdx.x;
+  // the last reader of this image's candidate counters leaves them at zero for the next call
+  // (no memset node in front of a captured detect)
+  auto clear_counters = [&]() {
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) cand_count[static_cast<int64_t>(b) * C + c] = 0u;
+  };
   const int st = merge_body(kept, kc, lastkey, boxes_ws, P, C, window, wfirst, top_k, final_nms, general, pass, need,
                             scratch, out_boxes, out_labels, out_scores, out_count);
   STAMP_END(3, 1);
-  if (st == 0 || pass != 1) return;
-  const int b = blockIdx.x;
+  if (st == 0 || pass != 1) {
+    clear_counters();
+    return;
+  }
   uint32_t *h2 = reinterpret_cast<uint32_t *>(s_raw + ((seg_lds(window) + 15) & ~static_cast<size_t>(15)));
   unsigned long long *m2 = reinterpret_cast<unsigned long long *>(h2 + 2048);
   unsigned long long *st2 = m2 + kMergeThreads, *fl2 = st2 + 2;
@@ -1741,6 +1752,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
   __syncthreads();
   merge_body(kept, kc, lastkey, boxes_ws, P, C, window, window, top_k, final_nms, general, 2, need, scratch, out_boxes,
              out_labels, out_scores, out_count);
+  clear_counters();
 }
 
 // ----------------------------------------------------------------------------- single segment
@@ -1812,12 +1824,14 @@ DetWs carve_det(void *w, int B, int P, int C, int window) {
   char *c = static_cast<char *>(w);
   DetWs r;
   size_t o = 0;
+  // the candidate counters first: their place depends on B * C only (sbod_detect_f32's
+  // SBOD_DETECT_COUNTERS_ZEROED contract)
+  r.count = reinterpret_cast<uint32_t *>(c + o);
+  o += align_up(static_cast<size_t>(B) * C * 4);
   r.boxes = reinterpret_cast<float *>(c + o);
   o += align_up(static_cast<size_t>(B) * P * 16);
   r.cand = reinterpret_cast<unsigned long long *>(c + o);
   o += align_up(static_cast<size_t>(B) * C * P * 8);
-  r.count = reinterpret_cast<uint32_t *>(c + o);
-  o += align_up(static_cast<size_t>(B) * C * 4);
   r.kept = reinterpret_cast<unsigned long long *>(c + o);
   o += align_up(static_cast<size_t>(B) * C * window * 8);
   r.kc = reinterpret_cast<uint32_t *>(c + o);
@@ -1841,6 +1855,8 @@ int clampw(int w, int P) {
 
 extern "C" {
 
+size_t sbod_detect_counter_bytes(int B, int C) { return align_up(static_cast<size_t>(B) * C * 4); }
+
 size_t sbod_detect_workspace_bytes(int B, int P, int C) {
   return carve_det(nullptr, B, P, C, clampw(kMaxWindow, P)).bytes;
 }
@@ -1848,9 +1864,10 @@ size_t sbod_detect_workspace_bytes(int B, int P, int C) {
 int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                     const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
                     float min_score, float max_overlap, int top_k, float final_nms, int window,
-                    float *det_boxes, int64_t *det_labels, float *det_scores, int32_t *det_count,
-                    float *debug_probs, float *debug_boxes, void *workspace,
+                    int flags, float *det_boxes, int64_t *det_labels, float *det_scores,
+                    int32_t *det_count, float *debug_probs, float *debug_boxes, void *workspace,
                     size_t workspace_bytes, void *stream) {
+  SBOD_REQUIRE((flags & ~SBOD_DETECT_COUNTERS_ZEROED) == 0, "sbod_detect_f32: unknown flags 0x%x", flags);
   SBOD_REQUIRE(B > 0 && P > 0 && C >= 2 && C <= 256 && locs && scores && det_boxes && det_labels &&
                    det_scores && det_count && top_k > 0,
                "sbod_detect_f32: bad arguments (B=%d P=%d C=%d top_k=%d)", B, P, C, top_k);
@@ -1878,7 +1895,8 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   const size_t merge_lds = head + static_cast<size_t>(kMergeStage) * 4 +
                            (final_nms >= 0.f ? (tools_general > tools_fast ? tools_general : tools_fast) : 0);
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4, s) != hipSuccess)
+  if ((flags & SBOD_DETECT_COUNTERS_ZEROED) == 0 &&
+      hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4, s) != hipSuccess)
     return launch_status("hipMemsetAsync(detect)");
   DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.boxes, ws.cand, ws.count,
             debug_probs, debug_boxes, nullptr};

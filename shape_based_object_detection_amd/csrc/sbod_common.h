@@ -39,6 +39,8 @@ constexpr float kIouEps = 1e-5f;  // metrics.py:233 EPS (compared as float32, li
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+struct SpanRing;
+
 // Brackets a launch with HIP events on its stream when sbod_timing_enable() selected it.
 // With `attached` the scope's launch carries the two events itself (hipExtLaunchKernelGGL(...,
 // kt.start(), kt.stop(), 0, ...)): the runtime stamps them at the dispatch's own start and end, so
@@ -53,31 +55,48 @@ class KernelTimer {
   hipEvent_t start() const { return attached_ ? start_ : nullptr; }
   hipEvent_t stop() const { return attached_ ? stop_ : nullptr; }
   // Under hipGraph capture (where a dispatch cannot carry events and this runtime refuses
-  // external event nodes) a selected kernel instead gets a device span slot {first workgroup
-  // start, last workgroup end} in s_memrealtime ticks, written by the kernel itself
-  // (span_begin / span_end) on every replay; nullptr when not selected.
-  unsigned long long *span() const { return span_; }
+  // external event nodes) a selected kernel instead gets a device span ring (SpanRing, below)
+  // that the kernel itself writes on every replay; nullptr when not selected.
+  SpanRing *span() const { return span_; }
 
  private:
   const char *name_;
   hipStream_t stream_;
   bool attached_;
   hipEvent_t start_ = nullptr, stop_ = nullptr;
-  unsigned long long *span_ = nullptr;
+  SpanRing *span_ = nullptr;
 };
 
-// Kernel-side span recording (see KernelTimer::span).  span_end synchronises the workgroup and
-// must be reached by all of its threads; the fence makes the block's stores complete before the
-// end stamp, so the span covers the write drain like a dispatch's completion signal does.
-__device__ __forceinline__ void span_begin(unsigned long long *span) {
-  if (span != nullptr && threadIdx.x == 0)
-    atomicMin(span, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+// Kernel-side span recording (see KernelTimer::span).  A captured kernel is replayed many
+// times and the host never writes the record between replays: every launch overwrites, per
+// workgroup, its own {start, end} pair (plain stores by thread 0, no atomics — thousands of
+// same-address atomics would themselves stretch the kernel), and workgroup 0 the grid size; the
+// host reduces min(start) / max(end) after the replay.
+constexpr int kSpanBlocks = 16384;   // workgroups recorded per launch (ids beyond are not)
+struct SpanRing {
+  unsigned long long nblocks;
+  unsigned long long t[kSpanBlocks][2];
+};
+
+__device__ __forceinline__ unsigned span_block_id() {
+  return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
 }
-__device__ __forceinline__ void span_end(unsigned long long *span) {
-  if (span == nullptr) return;
-  __threadfence();
+__device__ __forceinline__ void span_begin(SpanRing *r) {
+  if (r == nullptr || threadIdx.x != 0) return;
+  const unsigned blk = span_block_id();
+  if (blk == 0) r->nblocks = static_cast<unsigned long long>(gridDim.x) * gridDim.y * gridDim.z;
+  if (blk < kSpanBlocks) r->t[blk][0] = __builtin_amdgcn_s_memrealtime();
+}
+// Synchronises the workgroup; must be reached by all of its threads.  Each thread first waits
+// for its own outstanding memory operations (s_waitcnt 0: stores acknowledged by L2), so the end
+// stamp follows the block's stores.  (Not __threadfence(): a device-scope release writes the
+// XCD's L2 back on every block, ~10x the kernel's own time on MI355X.)
+__device__ __forceinline__ void span_end(SpanRing *r) {
+  if (r == nullptr) return;
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (threadIdx.x == 0) atomicMax(span + 1, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+  const unsigned blk = span_block_id();
+  if (threadIdx.x == 0 && blk < kSpanBlocks) r->t[blk][1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Launch through a KernelTimer: a timed launch carries the timer's events on the dispatch

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert missing == [], missing
     assert set(syms) <= set(L.SIGNATURES), set(syms) - set(L.SIGNATURES)
     assert L.MISSING == []
-    assert lib.sbod_abi_version() == 1
+    assert lib.sbod_abi_version() == 2
     assert b'gfx950' in lib.sbod_version()
 
 
@@ -130,3 +130,32 @@ def test_no_kernel_spills_to_scratch():
 def test_stress_anchor_generator_size():
     # SURVEY §8 C3 stress size: RetinaNet's generator on 896x896 maps
     assert prior_table('RETINA896').shape == (100254, 4)
+
+
+def test_model_entry_registry():
+    """models/__init__.py:8-32 contract: (network, criterion class) from config.model['arch']."""
+    from shape_based_object_detection_amd import models as MD
+
+    class Cfg(dict):
+        __getattr__ = dict.__getitem__
+
+    made = {}
+
+    def ssd512(n_classes, device=None):
+        made['ssd512'] = (n_classes, device)
+        return 'net512'
+
+    def refinedet(n_classes, config=None):
+        made['refine'] = (n_classes, config is not None)
+        return 'netrefine'
+
+    MD.register_network('SSD512', ssd512)
+    MD.register_network('refinedet', refinedet)
+    net, crit = MD.model_entry(Cfg(model={'arch': 'ssd512'}, n_classes=21, device='cpu'))
+    assert net == 'net512' and crit is MD.MultiBoxLoss512 and made['ssd512'] == (21, 'cpu')
+    net, crit = MD.model_entry(Cfg(model={'arch': 'RefineDet'}, n_classes=21, device='cpu'))
+    assert net == 'netrefine' and crit is MD.RefineDetLoss and made['refine'] == (21, True)
+    with pytest.raises(NotImplementedError, match='register_network'):
+        MD.model_entry(Cfg(model={'arch': 'RETINA50'}, n_classes=21, device='cpu'))
+    with pytest.raises(NotImplementedError):
+        MD.model_entry(Cfg(model={'arch': 'FCOS50'}, n_classes=21, device='cpu'))

@@ -1,0 +1,78 @@
+"""The reference's on-disk VOC format and list-of-tensors batches, on CPU:
+synthetic VOC-format JPEGs -> PascalVOCDataset -> DataLoader(collate_fn) with worker processes
+(random_crop's IoU runs in them through the host path of find_jaccard_overlap)."""
+import json
+import os
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader
+
+from shape_based_object_detection_amd.dataset import Datasets as D
+
+
+def _cfg(ops=()):
+    return {'model': {'operation_list': list(ops), 'return_percent_coords': True}}
+
+
+def test_voc_files_and_test_transform(tmp_path):
+    folder = D.write_synthetic_voc(str(tmp_path), 4, size=(300, 300), split='TEST', seed=3)
+    assert D.read_label_map(folder)['background'] == 0 and len(D.read_label_map(folder)) == 21
+    ds = D.PascalVOCDataset(folder, 'test', (300, 300), _cfg())
+    assert len(ds) == 4
+    with open(os.path.join(folder, 'TEST_objects.json')) as f:
+        objs = json.load(f)
+    dl = DataLoader(ds, batch_size=4, shuffle=False, collate_fn=ds.collate_fn)
+    images, boxes, labels, ids, diffs = next(iter(dl))
+    assert images.shape == (4, 3, 300, 300) and images.dtype == torch.float32
+    assert isinstance(boxes, list) and len(boxes) == 4
+    for i in range(4):
+        px = torch.tensor(objs[i]['bbox'], dtype=torch.float32)
+        want = px / torch.tensor([300., 300., 300., 300.])      # transforms.py:246-247
+        assert torch.equal(boxes[i], want)
+        assert labels[i].dtype == torch.int64 and labels[i].tolist() == objs[i]['labels']
+        assert diffs[i].tolist() == objs[i]['difficulties']
+        assert ids[i].endswith('%06d.jpg' % i)
+    # ImageNet normalisation of [0,1] pixels
+    assert images.min() >= (0 - 0.485) / 0.229 - 1e-5 and images.max() <= (1 - 0.406) / 0.225 + 1e-5
+
+
+def test_train_augmentation_in_worker_processes(tmp_path):
+    folder = D.write_synthetic_voc(str(tmp_path), 8, size=(300, 300), split='TRAIN', seed=5)
+    ds = D.PascalVOCDataset(folder, 'train', (300, 300), _cfg(['expand', 'random_crop']))
+    torch.manual_seed(0)
+    dl = DataLoader(ds, batch_size=4, shuffle=True, collate_fn=ds.collate_fn, num_workers=2)
+    n = 0
+    for images, boxes, labels, ids, diffs in dl:
+        assert images.shape == (4, 3, 300, 300)
+        for b, l in zip(boxes, labels):
+            assert b.dim() == 2 and b.shape[1] == 4 and b.shape[0] == l.shape[0] >= 1
+            assert (b[:, 2] >= b[:, 0]).all() and (b[:, 3] >= b[:, 1]).all()
+        n += len(boxes)
+    assert n == 8
+
+
+def test_random_crop_keeps_centred_objects():
+    import random
+    rng = random.Random(7)
+    img = torch.rand(3, 200, 300)
+    boxes = torch.tensor([[10., 10., 60., 80.], [100., 50., 250., 190.], [150., 20., 180., 40.]])
+    labels = torch.tensor([3, 7, 9])
+    for _ in range(20):
+        im, b, l = D.random_crop(img, boxes, labels, rng)
+        assert im.shape[0] == 3 and b.shape[0] == l.shape[0]
+        assert (b >= 0).all()
+        assert (b[:, 2] <= im.shape[2]).all() and (b[:, 3] <= im.shape[1]).all()
+
+
+def test_flip_and_expand_boxes():
+    from PIL import Image
+    im = Image.fromarray(np.zeros((50, 80, 3), np.uint8))
+    boxes = torch.tensor([[10., 5., 30., 25.]])
+    _, fb = D.flip(im, boxes)
+    assert fb.tolist() == [[80 - 30 - 1, 5., 80 - 10 - 1, 25.]]
+    import random
+    t, eb = D.expand(torch.rand(3, 50, 80), boxes, D.IMAGENET_MEAN, random.Random(1))
+    assert t.shape[1] >= 50 and t.shape[2] >= 80
+    d = eb - boxes
+    assert d[0, 0] == d[0, 2] and d[0, 1] == d[0, 3]

@@ -5,7 +5,7 @@
   * a criterion forward+backward + detect captured with torch.cuda.graph and replayed gives the
     eager results bit for bit, also after the staged ground truth changes between replays (the
     graph reads the fixed-capacity buffers, not the capture-time lists);
-  * a timed kernel inside the capture stamps its own span slot on every replay.
+  * a timed kernel inside the capture overwrites its own span record on every replay.
 """
 import numpy as np
 import pytest
@@ -127,7 +127,7 @@ def test_graph_replay_equals_eager():
     g = torch.cuda.CUDAGraph()
     pack = stage.stage(*gt1)
     torch.cuda.synchronize()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=side):            # capture on the warmed-up stream
         g_loss, g_h = body(pack, True)
     g_gl, g_gs = locs.grad, scores.grad
     for seed in (100, 200, 300):                         # new ground truth every replay
@@ -144,8 +144,24 @@ def test_graph_replay_equals_eager():
         locs.grad, scores.grad = g_gl, g_gs
 
 
+def test_workspace_allocation_under_capture_refused():
+    """A workspace the captured call would allocate under capture fails loudly instead."""
+    B = 2
+    P, crit, locs, scores, det = _setup(B, seed=6)
+    gt = _gt(B, 8)
+    stage = core.GtStaging(B, 16, DEV)
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    pack = stage.stage(*gt)
+    torch.cuda.synchronize()
+    with pytest.raises(L.SbodError, match='under hipGraph capture'):
+        with torch.cuda.graph(g, stream=s):               # never warmed up on s
+            crit(locs, scores, pack, None)
+
+
 def test_graph_span_timing():
-    """A timed kernel captured into a graph stamps its own span slot on every replay."""
+    """A timed kernel captured into a graph overwrites its own span record on every replay; the host
+    reads the latest launch without writing anything between replays."""
     B = 4
     P, crit, locs, scores, det = _setup(B, seed=5)
     gt = _gt(B, 7)
@@ -162,21 +178,18 @@ def test_graph_span_timing():
     g = torch.cuda.CUDAGraph()
     locs.grad = None
     scores.grad = None
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=s):
         loss = crit(locs, scores, stage.stage(*gt), None)
         loss.backward()
     L.timing_enable(None)
-    assert L.timing_query('k_multibox')[0] == 0          # armed nothing yet / never replayed
+    assert L.timing_query('k_multibox')[0] == 0          # never replayed yet
     times = []
     for _ in range(3):
-        L.call('sbod_timing_arm')
         g.replay()
         torch.cuda.synchronize()
         n, ms = L.timing_query('k_multibox')
         assert n == 1
         times.append(ms)
-    L.call('sbod_timing_arm')
-    assert L.timing_query('k_multibox')[0] == 0          # armed, not replayed since
     assert all(0.0005 < t < 5.0 for t in times), times
     del g
     L.call('sbod_timing_reset_graphs')

@@ -113,6 +113,21 @@ def test_codecs_and_match_api():
     np.testing.assert_allclose(loc_t.cpu().numpy(), m['match_loc'], rtol=1e-5, atol=1e-5)
 
 
-def test_cpu_tensors_rejected():
+def test_cpu_and_device_paths_agree():
+    """CPU tensors take the host path (DataLoader workers); device tensors the HIP
+    kernel: bit-identical IoU.  Mixed devices raise; device-only ops reject CPU tensors."""
+    from shape_based_object_detection_amd import _lib as L
+    from shape_based_object_detection_amd.operators import iou_utils as IU
+    g = torch.rand(7, 2)
+    gt = torch.cat([g, g + torch.rand(7, 2) * 0.5], 1)
+    a = torch.rand(300, 2)
+    an = torch.cat([a, a + torch.rand(300, 2) * 0.3], 1)
+    an[5, 2:] = an[5, :2]                        # a zero-size anchor (-1 mask)
+    host = metrics.find_jaccard_overlap(gt, an)
+    dev = metrics.find_jaccard_overlap(gt.cuda(), an.cuda()).cpu()
+    assert torch.equal(host, dev)
+    assert torch.equal(IU.jaccard(gt, an), IU.jaccard(gt.cuda(), an.cuda()).cpu())
     with pytest.raises(RuntimeError):
-        metrics.find_jaccard_overlap(torch.rand(2, 4), torch.rand(3, 4))
+        metrics.find_jaccard_overlap(gt, an.cuda())
+    with pytest.raises(L.SbodError):
+        IU.nms(torch.rand(4, 4), torch.rand(4))
