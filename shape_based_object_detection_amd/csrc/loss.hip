@@ -293,7 +293,7 @@ __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp
 // CM > 0: class rows of C <= CM in registers (padding slots -inf: no per-slot guards in the
 // max / exp / sum); CM == 0: any C, rows in LDS.
 template <typename T, int CM, int CLS>
-__global__ __launch_bounds__(kLTile, 6) void k_multibox(LossArgs a, const T *__restrict__ locs,
+__global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs a, const T *__restrict__ locs,
                                                      const T *__restrict__ scores,
                                                      T *__restrict__ glocs, T *__restrict__ gsc) {
   extern __shared__ float s_sc[];
