@@ -464,6 +464,14 @@ def _count_slot(dev, B):
 _DET_CLEAN = {}
 
 
+def reserve_count_slots(dev, B, n):
+    """Make ``n`` (pinned count buffer, event) pairs available for detects of batch B on ``dev``
+    — e.g. before capturing ``n`` graphs, since pinned memory cannot be allocated under capture."""
+    free = _COUNT_SLOTS.setdefault((dev, B), [])
+    while len(free) < n:
+        free.append((torch.empty(B, dtype=torch.int32, pin_memory=True), torch.cuda.Event()))
+
+
 def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn, out,
                    dbg, ws, nb, window):
     out_b, out_l, out_s, cnt = out
