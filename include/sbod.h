@@ -215,14 +215,15 @@ int sbod_scale2_inplace(void *a, int64_t na, void *b, int64_t nb, int dtype, con
  * The operators.Loss / iou_utils API on already-selected rows.  Each call writes the per-row
  * (or per-element) values and their local derivatives; the Python layer applies the
  * reference's own reductions (Loss.py:192-200, 219-226, 38, 80, 103) through autograd.
- *   aligned overlap (iou_utils.py:6-164): overlap [n] and d overlap / d b1 [n,4] (grad may be
- *     NULL); the reference's clamp masks and its min/max tie rule (gradient split in half).
+ *   aligned overlap (iou_utils.py:6-164): overlap [n], d overlap / d b1 [n,4] and d overlap /
+ *     d b2 [n,4] (either gradient may be NULL; autograd reaches both box sets in the reference);
+ *     the reference's clamp masks and its min/max tie rule (gradient split in half).
  *   smooth L1 (Loss.py:213-217): loss [n] and d loss / d pred [n] per element.
  *   focal (Loss.py:9-38 softmax, :41-80 sigmoid, :83-103 bce): loss [rows] and
  *     d loss / d logits [rows, C]. */
 enum { SBOD_OV_IOU = 0, SBOD_OV_GIOU = 1, SBOD_OV_DIOU = 2, SBOD_OV_CIOU = 3 };
 int sbod_aligned_overlap_f32(int kind, const float *b1, const float *b2, int64_t n,
-                             float *overlap, float *grad_b1, void *stream);
+                             float *overlap, float *grad_b1, float *grad_b2, void *stream);
 int sbod_smooth_l1_f32(const float *pred, const float *target, int64_t n, float beta,
                        float *loss, float *grad, void *stream);
 enum { SBOD_FOCAL_SOFTMAX = 0, SBOD_FOCAL_SIGMOID = 1, SBOD_FOCAL_BCE = 2 };

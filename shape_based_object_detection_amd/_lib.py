@@ -39,7 +39,7 @@ SIGNATURES = {
                                         P, P, SZ, P]),
     'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),
     'sbod_scale2_inplace': (I32, [P, I64, P, I64, I32, P, P]),
-    'sbod_aligned_overlap_f32': (I32, [I32, P, P, I64, P, P, P]),
+    'sbod_aligned_overlap_f32': (I32, [I32, P, P, I64, P, P, P, P]),
     'sbod_smooth_l1_f32': (I32, [P, P, I64, F32, P, P, P]),
     'sbod_focal_f32': (I32, [I32, P, P, I64, I32, F32, F32, F32, P, P, P]),
     'sbod_detect_workspace_bytes': (SZ, [I32, I32, I32]),

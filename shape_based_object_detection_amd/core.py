@@ -184,9 +184,9 @@ def workspace(nbytes, device, slot='default'):
                               'run the same calls once on the capture stream before capturing'
                               % (slot, n))
         if buf is not None:
-            _DET_CLEAN.pop(buf.data_ptr(), None)   # its memory returns to the allocator
+            _CLEAN.pop(buf.data_ptr(), None)   # its memory returns to the allocator
         buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=dev)
-        _DET_CLEAN.pop(buf.data_ptr(), None)
+        _CLEAN.pop(buf.data_ptr(), None)
         _WS[key] = buf
     return buf
 
@@ -422,13 +422,16 @@ class DetectHandle:
         counts = self._cnt_host.tolist()
         if not self._persistent:
             _COUNT_SLOTS.setdefault(self._slot_key, []).append((self._cnt_host, self._event))
-        if min(counts) < 0:   # rare: some image needs the full candidate window (exactness)
+        if min(counts) < 0:   # rare: some image needs a wider candidate window (exactness)
             _detect_launch(*self._launch_args(4096))
             counts = cnt.cpu().tolist()
             if min(counts) < 0:
-                raise L.SbodError('detect: a per-class candidate window of 4096 is not enough to decide '
-                                  'the top-%d outputs exactly (pathological suppression); unsupported'
-                                  % top_k)
+                # a class whose survivors a 4,096-candidate window cannot bound (thousands of
+                # near-duplicates): chunked greedy NMS over all of its candidates
+                _detect_launch(*self._launch_args(-1))
+                counts = cnt.cpu().tolist()
+                if min(counts) < 0:
+                    raise L.SbodError('detect: internal error, the exhaustive pass left an image undecided')
         if in_place and lc is not locs:
             locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
         if min(counts) == top_k:     # every image full (the usual eval case)
@@ -458,10 +461,21 @@ def _count_slot(dev, B):
     return torch.empty(B, dtype=torch.int32, pin_memory=True), torch.cuda.Event()
 
 
-# Detect workspaces whose candidate counters are known to be zero: data_ptr -> bytes.  Every
-# sbod_detect_f32 call leaves its counters zero, so after the first call on a workspace no memset
-# is needed (none in a captured graph: SBOD_DETECT_COUNTERS_ZEROED).
-_DET_CLEAN = {}
+# Workspaces whose leading counters are known to be zero: data_ptr -> bytes.  sbod_detect_f32
+# leaves its candidate counters zero, so after the first call on a workspace no memset is
+# needed — none in a captured graph (SBOD_DETECT_COUNTERS_ZEROED).
+_CLEAN = {}
+
+
+def _zeroed_flag(ws, need, flag, what):
+    """``flag`` when the first ``need`` bytes of ``ws`` are known zero, else 0 (the call zeroes
+    them itself: a memset, which must not be captured)."""
+    if _CLEAN.get(ws.data_ptr(), 0) >= need:
+        return flag
+    if torch.cuda.is_current_stream_capturing():
+        raise L.SbodError('%s under hipGraph capture: run it once on the capture stream with this '
+                          'shape first (its workspace counters are not known to be zero)' % what)
+    return 0
 
 
 def reserve_count_slots(dev, B, n):
@@ -476,19 +490,14 @@ def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overl
                    dbg, ws, nb, window):
     out_b, out_l, out_s, cnt = out
     need = L.lib().sbod_detect_counter_bytes(B, C)
-    flags = 0
-    if _DET_CLEAN.get(ws.data_ptr(), 0) >= need:
-        flags = L.DETECT_COUNTERS_ZEROED
-    elif torch.cuda.is_current_stream_capturing():
-        raise L.SbodError('detect under hipGraph capture: run it once on the capture stream with this '
-                          'batch shape first (its workspace counters are not known to be zero)')
+    flags = _zeroed_flag(ws, need, L.DETECT_COUNTERS_ZEROED, 'detect')
     L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
            L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(window), flags,
            L.ptr(out_b), L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg[0]), L.ptr(dbg[1]),
            L.ptr(ws), nb, L.stream_of(sc))
     # only this call's prefix is known clean: a call with a smaller B * C writes other regions
     # over the rest of a larger one's counters
-    _DET_CLEAN[ws.data_ptr()] = need
+    _CLEAN[ws.data_ptr()] = need
 
 
 def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='offset',
@@ -584,24 +593,39 @@ class _RowOp(torch.autograd.Function):
         return g * local, None, None
 
 
+class _Overlap(torch.autograd.Function):
+    """Row-wise overlap [n] of two box sets; the kernel writes the local derivatives w.r.t. both
+    (iou_utils.py:6-164 lets autograd reach both), backward scales them by the upstream grad."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, run, want1, want2):
+        val, g1, g2 = run(want1, want2)
+        ctx.save_for_backward(g1, g2)
+        return val
+
+    @staticmethod
+    def backward(ctx, g):
+        g1, g2 = ctx.saved_tensors
+        g = g.unsqueeze(-1)
+        return (g * g1 if g1 is not None else None), (g * g2 if g2 is not None else None), None, None, None
+
+
 def aligned_overlap(kind, b1, b2):
-    """Row-wise IoU / GIoU / DIoU / CIoU [n] with autograd w.r.t. ``b1``."""
+    """Row-wise IoU / GIoU / DIoU / CIoU [n] with autograd w.r.t. both box sets."""
     L.require_device(b1, b2, what='bbox_overlaps')
-    if b2.requires_grad and torch.is_grad_enabled():
-        raise NotImplementedError('sbod bbox_overlaps_*: gradients w.r.t. the second (target) box '
-                                  'set are not implemented')
     n = b1.shape[0]
-    x1, x2 = b1.contiguous().float(), b2.detach().contiguous().float()
+    x1, x2 = b1.contiguous().float(), b2.contiguous().float()
 
-    def run(want):
+    def run(want1, want2):
         ov = torch.empty(n, dtype=torch.float32, device=b1.device)
-        g = torch.empty(n, 4, dtype=torch.float32, device=b1.device) if want else None
-        L.call('sbod_aligned_overlap_f32', L.OV[kind], L.ptr(x1), L.ptr(x2), n, L.ptr(ov), L.ptr(g),
-               L.stream_of(x1))
-        return ov, g
+        g1 = torch.empty(n, 4, dtype=torch.float32, device=b1.device) if want1 else None
+        g2 = torch.empty(n, 4, dtype=torch.float32, device=b1.device) if want2 else None
+        L.call('sbod_aligned_overlap_f32', L.OV[kind], L.ptr(x1), L.ptr(x2), n, L.ptr(ov), L.ptr(g1),
+               L.ptr(g2), L.stream_of(x1))
+        return ov, g1, g2
 
-    want = torch.is_grad_enabled() and b1.requires_grad
-    return _RowOp.apply(x1, run, want)
+    grad_on = torch.is_grad_enabled()
+    return _Overlap.apply(x1, x2, run, grad_on and b1.requires_grad, grad_on and b2.requires_grad)
 
 
 def smooth_l1_elementwise(pred, target, beta):

@@ -114,12 +114,14 @@ __device__ __forceinline__ void tile_commit(float *dst, const V (&r)[NB], int n)
 
 struct OvOut {
   float v;
-  float g[4];  // d v / d b1 (x1, y1, x2, y2)
+  float g[4];   // d v / d b1 (x1, y1, x2, y2)
+  float g2[4];  // d v / d b2 (only with kG2)
 };
 
 // Row-wise IoU / GIoU / DIoU / CIoU of iou_utils.py:6-164 (forward in the reference's
 // evaluation order) and the hand-derived reverse mode of the same graph (clamp masks inclusive,
 // CIoU's alpha / arctan / w_temp treated as constants as under its torch.no_grad()).
+template <bool kG2 = false>
 __device__ OvOut aligned_overlap(int kind, Box4 p, Box4 t, bool want_grad) {
   const float x1 = p.a, y1 = p.b, x2 = p.c, y2 = p.d;
   const float X1 = t.a, Y1 = t.b, X2 = t.c, Y2 = t.d;
@@ -195,10 +197,37 @@ __device__ OvOut aligned_overlap(int kind, Box4 p, Box4 t, bool want_grad) {
   OvOut r;
   r.v = fminf(fmaxf(raw, lo), 1.f);
   r.g[0] = r.g[1] = r.g[2] = r.g[3] = 0.f;
+  if constexpr (kG2) r.g2[0] = r.g2[1] = r.g2[2] = r.g2[3] = 0.f;
   if (!want_grad || !(raw >= lo && raw <= 1.f)) return r;
   // U = a1 + a2 - ia
   const float g_a1 = g_U;
   g_ia -= g_U;
+  if constexpr (kG2) {
+    // the second box set: the same graph through X1..Y2 (min / max ties split in half; CIoU's
+    // alpha * ar term depends on b1 only, its arctan / alpha being constants)
+    const float g_iwr2 = iwr >= 0.f ? g_ia * ih : 0.f;
+    const float g_ihr2 = ihr >= 0.f ? g_ia * iw : 0.f;
+    float gX1 = -g_iwr2 * dmax_a(X1, x1), gX2 = g_iwr2 * dmin_a(X2, x2);
+    float gY1 = -g_ihr2 * dmax_a(Y1, y1), gY2 = g_ihr2 * dmin_a(Y2, y2);
+    if (kind != SBOD_OV_IOU) {
+      const float g_owr = owr >= 0.f ? g_ow : 0.f;
+      const float g_ohr = ohr >= 0.f ? g_oh : 0.f;
+      gX2 += g_owr * dmax_a(X2, x2);
+      gX1 -= g_owr * dmin_a(X1, x1);
+      gY2 += g_ohr * dmax_a(Y2, y2);
+      gY1 -= g_ohr * dmin_a(Y1, y1);
+    }
+    // centre distance: dx = cx2 - cx1, so d/dcx2 = -d/dcx1
+    const float g_w2 = g_U * h2, g_h2 = g_U * w2;   // a2 = w2 * h2 (U = a1 + a2 - ia)
+    gX1 += -0.5f * g_cx1 - g_w2;
+    gX2 += -0.5f * g_cx1 + g_w2;
+    gY1 += -0.5f * g_cy1 - g_h2;
+    gY2 += -0.5f * g_cy1 + g_h2;
+    r.g2[0] = gX1;
+    r.g2[1] = gY1;
+    r.g2[2] = gX2;
+    r.g2[3] = gY2;
+  }
   g_w1 += g_a1 * h1;
   g_h1 += g_a1 * w1;
   const float g_iwr = iwr >= 0.f ? g_ia * ih : 0.f;
@@ -712,11 +741,13 @@ __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ pa
 // ----------------------------------------------------------------------------- standalone
 __global__ __launch_bounds__(256) void k_aligned(int kind, const float *__restrict__ b1,
                                                  const float *__restrict__ b2, int64_t n,
-                                                 float *__restrict__ ov, float *__restrict__ g) {
+                                                 float *__restrict__ ov, float *__restrict__ g,
+                                                 float *__restrict__ g2) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  OvOut r = aligned_overlap(kind, ld4(b1 + 4 * i), ld4(b2 + 4 * i), g != nullptr);
+  OvOut r = aligned_overlap<true>(kind, ld4(b1 + 4 * i), ld4(b2 + 4 * i), g != nullptr || g2 != nullptr);
   ov[i] = r.v;
+  if (g2) st4(g2 + 4 * i, Box4{r.g2[0], r.g2[1], r.g2[2], r.g2[3]});
   if (g) st4(g + 4 * i, Box4{r.g[0], r.g[1], r.g[2], r.g[3]});
 }
 
@@ -958,12 +989,12 @@ int sbod_multibox_mine_global(const void *scores, int dtype, int B, int P, int C
 }
 
 int sbod_aligned_overlap_f32(int kind, const float *b1, const float *b2, int64_t n,
-                             float *overlap, float *grad_b1, void *stream) {
+                             float *overlap, float *grad_b1, float *grad_b2, void *stream) {
   SBOD_REQUIRE(kind >= 0 && kind <= 3 && n >= 0 && (n == 0 || (b1 && b2 && overlap)),
                "sbod_aligned_overlap_f32: bad arguments");
   if (n == 0) return SBOD_OK;
   hipLaunchKernelGGL(k_aligned, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), kind, b1,
-                     b2, n, overlap, grad_b1);
+                     b2, n, overlap, grad_b1, grad_b2);
   SBOD_LAUNCHED("k_aligned");
   return SBOD_OK;
 }

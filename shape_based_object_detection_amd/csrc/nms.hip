@@ -713,6 +713,141 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
                s_m, &s_nk, &s_cnt, s_misc);
 }
 
+// ----------------------------------------------------------------------------- K2 (exhaustive)
+// Segments no bounded window can decide (a class with more candidates than the largest window
+// whose survivors might still reach the image's top_k, e.g. thousands of near-duplicates): the
+// class's candidates are consumed in descending key order, kAllChunk at a time — each chunk is
+// the radix-selected top of the keys below the previous chunk's last key, straight from global
+// memory — every chunk candidate is first tested against all boxes kept so far, then the
+// chunk's survivors are resolved by block_greedy.  This is exactly the sequential greedy NMS of
+// the reference (models/utils.py:265, torchvision semantics) for any candidate count; it stops
+// once top_k boxes are kept, because a class's boxes beyond its own top_k can never rank in the
+// image's top_k.  kept[seg] holds the kept keys in rank order, lastkey[seg] = 0 (decided).
+constexpr int kAllChunk = 1024;
+constexpr int kAllThreads = 1024;
+
+// q-th largest of the unique keys below `upper` in global memory (8-bit digits from the top).
+__device__ unsigned long long radix_select_below(const unsigned long long *g, int n, int q,
+                                                 unsigned long long upper, uint32_t *hist,
+                                                 unsigned long long *st) {
+  unsigned long long prefix = 0, mask = 0;
+  int kk = q;
+  for (int level = 0; level < 8; ++level) {
+    const int shift = 56 - 8 * level;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const unsigned long long k = g[i];
+      if (k < upper && (k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255ull], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int acc = 0, d = 255;
+      for (; d > 0; --d) {
+        if (acc + static_cast<int>(hist[d]) >= kk) break;
+        acc += hist[d];
+      }
+      st[0] = prefix | (static_cast<unsigned long long>(d) << shift);
+      st[1] = static_cast<unsigned long long>(kk - acc);
+    }
+    __syncthreads();
+    prefix = st[0];
+    kk = static_cast<int>(st[1]);
+    mask |= 0xffull << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(kAllThreads) void k_det_segment_all(
+    const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
+    const float *__restrict__ boxes_ws, int P, int C, int stride, int top_k, float thr, SegOut o) {
+  extern __shared__ unsigned char s_raw[];   // kept so far: keys [stride] | boxes [stride] | areas [stride]
+  __shared__ unsigned long long s_key[kAllChunk];
+  __shared__ Box4 s_box[kAllChunk];
+  __shared__ float s_area[kAllChunk];
+  __shared__ unsigned long long c_key[kAllChunk];   // the chunk's survivors of the kept boxes
+  __shared__ Box4 c_box[kAllChunk];
+  __shared__ float c_area[kAllChunk];
+  __shared__ uint8_t s_keep[kAllChunk];
+  __shared__ int s_kl[kAllChunk];
+  __shared__ uint32_t s_hist[256];
+  __shared__ unsigned long long s_st[2];
+  __shared__ unsigned long long s_flag[16];
+  __shared__ unsigned long long s_m[kAllThreads];
+  __shared__ int s_wsum[kAllThreads / 64];
+  __shared__ int s_nk, s_cnt;
+  unsigned long long *kkey = reinterpret_cast<unsigned long long *>(s_raw);
+  Box4 *kbox = reinterpret_cast<Box4 *>(kkey + stride);
+  float *karea = reinterpret_cast<float *>(kbox + stride);
+  const int c = blockIdx.x + 1, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t seg = static_cast<int64_t>(b) * C + c;
+  const int n = min(static_cast<int>(cand_count[seg]), P);
+  const unsigned long long *g = cand + seg * P;
+  int kept = 0, remaining = n;
+  unsigned long long upper = ~0ull;
+  while (remaining > 0 && kept < top_k) {
+    const int q = min(kAllChunk, remaining);
+    const unsigned long long T = q == remaining ? 0ull : radix_select_below(g, n, q, upper, s_hist, s_st);
+    if (tid == 0) s_cnt = 0;
+    for (int i = tid; i < kAllChunk; i += blockDim.x) s_key[i] = 0ull;
+    __syncthreads();
+    for (int i = tid; i < n; i += blockDim.x) {
+      const unsigned long long k = g[i];
+      if (k >= T && k < upper) s_key[atomicAdd(&s_cnt, 1)] = k;   // exactly q (keys are unique)
+    }
+    __syncthreads();
+    bitonic_desc(s_key, kAllChunk);
+    // load the chunk's boxes; test each against every box kept so far
+    bool alive = false;
+    if (tid < q) {
+      const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(s_key[tid])));
+      const float ar = (bx.c - bx.a) * (bx.d - bx.b);
+      alive = true;
+      for (int i = 0; i < kept && alive; ++i)
+        if (suppresses<SBOD_NMS_TV>(kbox[i], karea[i], bx, ar, thr, 1.f)) alive = false;
+      s_box[tid] = bx;
+      s_area[tid] = ar;
+    }
+    // order-preserving compaction of the survivors
+    const unsigned long long bal = __ballot(alive);
+    if (lane == 0) s_wsum[wv] = __popcll(bal);
+    __syncthreads();
+    int base = 0, m = 0;
+    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) {
+      base += w < wv ? s_wsum[w] : 0;
+      m += s_wsum[w];
+    }
+    if (alive) {
+      const int at = base + __popcll(bal & ((1ull << lane) - 1ull));
+      c_key[at] = s_key[tid];
+      c_box[at] = s_box[tid];
+      c_area[at] = s_area[tid];
+    }
+    __syncthreads();
+    const int nk = m > 0 ? block_greedy<SBOD_NMS_TV>(c_box, c_area, m, thr, 1.f, s_keep, s_kl, s_flag, s_m,
+                                                     &s_nk, top_k - kept)
+                         : 0;
+    const int take = min(nk, top_k - kept);
+    for (int k = tid; k < take; k += blockDim.x) {
+      const int j = s_kl[k];
+      kkey[kept + k] = c_key[j];
+      kbox[kept + k] = c_box[j];
+      karea[kept + k] = c_area[j];
+    }
+    kept += take;
+    remaining -= q;
+    upper = s_key[q - 1];
+    __syncthreads();
+  }
+  unsigned long long *ko = o.kept + seg * stride;
+  for (int k = tid; k < kept; k += blockDim.x) ko[k] = kkey[k];
+  if (tid == 0) {
+    o.kc[seg] = kept;
+    o.lastkey[seg] = 0ull;
+  }
+}
+
 // ----------------------------------------------------------------------------- K2 (wave form)
 // Pass-1 segments (window <= 64): one wave per (image, class) segment, nothing block-wide.
 //   select: radix select of the q-th largest 64-bit key, 8-bit digits from the top, with a
@@ -1875,9 +2010,12 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   SBOD_REQUIRE(C * (kDTile * 4 + (kDTile / 64) * 12) <= 160 * 1024, "sbod_detect_f32: C=%d too large", C);
   SBOD_REQUIRE(P < (1 << 24), "sbod_detect_f32: P=%d >= 2^24 unsupported", P);
   // window 0 (auto): a first window of 64 candidates per class, then next_pow2(top_k + 1) for
-  // the truncated classes of images the first merge could not decide; window > 0: one pass.
-  const bool two = window <= 0;
-  const int w2 = clampw(two ? next_pow2_host(top_k + 1 > 64 ? top_k + 1 : 64) : window, P);
+  // the truncated classes of images the first merge could not decide; window > 0: one pass;
+  // window < 0: exhaustive (every class's candidates in chunks, k_det_segment_all).
+  const bool exhaustive = window < 0;
+  if (exhaustive) window = 0;
+  const bool two = window <= 0 && !exhaustive;
+  const int w2 = clampw(two || exhaustive ? next_pow2_host(top_k + 1 > 64 ? top_k + 1 : 64) : window, P);
   const int w1 = two ? clampw(kFirstWindow < w2 ? kFirstWindow : w2, P) : w2;
   DetWs ws = carve_det(workspace, B, P, C, w2);
   if (workspace_bytes < ws.bytes) {
@@ -1914,7 +2052,14 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   }
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
-  {
+  if (exhaustive) {
+    const size_t al = static_cast<size_t>(w2) * (8 + 16 + 4);
+    SBOD_REQUIRE((w2 >= top_k || w2 >= P) && al <= 64 * 1024,
+                 "sbod_detect_f32: exhaustive mode supports top_k <= 2047");
+    KernelTimer kt("k_det_segment", s, true);
+    tlaunch(kt, k_det_segment_all, dim3(C - 1, B), dim3(kAllThreads), al, s, ws.cand, ws.count, ws.boxes, P, C,
+            w2, top_k, max_overlap, so);
+  } else {
     KernelTimer kt("k_det_segment", s, true);
     if (w1 <= 64)
 #ifdef SBOD_SEG_WAVE

@@ -114,3 +114,62 @@ def test_nms_tv_vs_oracle(n, thr):
     ref = M.nms_greedy(boxes.numpy(), scores.numpy(), thr, variant='tv')
     assert int(count) == ref.size
     np.testing.assert_array_equal(keep.cpu().numpy()[:ref.size], ref)
+
+
+def test_detect_exhaustive_mode_equals_windowed():
+    """window < 0 (chunked greedy over every candidate) gives the windowed result at SSD512 size."""
+    Pn = prior_table('SSD512')
+    P = torch.from_numpy(Pn).to(DEV)
+    locs, scores = synth.make_preds(3, Pn.shape[0], 21, seed=31, bg_shift=6.0)
+    l, s = locs.to(DEV), scores.to(DEV)
+    a = _cat(core.detect(l, s, 0.01, 0.45, 200, P))
+    b = _cat(core.detect(l, s, 0.01, 0.45, 200, P, window=-1))
+    assert a[0] == b[0]
+    for x, y in zip(a[1:], b[1:]):
+        np.testing.assert_array_equal(x, y)
+
+
+def _near_duplicate_case(B, n_cand, n_clusters, seed):
+    """One class with n_cand candidates that are jittered copies of n_clusters well-separated
+    boxes (within a cluster IoU > 0.45, across clusters 0): n_clusters survivors per image, so no
+    bounded window can tell that the candidates it did not see are all suppressed."""
+    g = torch.Generator().manual_seed(seed)
+    P = 10248
+    scores = torch.full((B, P, 3), -10.0)
+    scores[:, :, 0] = 0.0
+    scores[:, :n_cand, 1] = 2.0 + torch.rand(B, n_cand, generator=g)          # distinct, > min_score
+    locs = torch.zeros(B, P, 4)
+    side = int(np.ceil(np.sqrt(n_clusters)))
+    cell = 1.0 / side
+    k = torch.arange(n_cand) % n_clusters
+    cx = (k % side).float() * cell + cell * 0.25
+    cy = (k // side).float() * cell + cell * 0.25
+    w = cell * 0.5
+    jit = torch.rand(B, n_cand, 4, generator=g) * (0.02 * w)
+    locs[:, :n_cand, 0] = cx + jit[..., 0]
+    locs[:, :n_cand, 1] = cy + jit[..., 1]
+    locs[:, :n_cand, 2] = cx + w - jit[..., 2]
+    locs[:, :n_cand, 3] = cy + w - jit[..., 3]
+    locs[:, n_cand:, 2:] = 0.01
+    return locs, scores
+
+
+def test_detect_beyond_largest_window_near_duplicates():
+    """More than 4,096 near-duplicate candidates in one class and fewer than top_k survivors: the
+    4,096 window cannot decide (count -1), and the public detect falls through to the exhaustive
+    pass — bit-exact vs the oracle on the kernel's own activations (models/utils.py:245-290 with
+    torchvision semantics)."""
+    B = 2
+    locs, scores = _near_duplicate_case(B, 6000, 20, seed=5)
+    l, s = locs.to(DEV), scores.to(DEV)
+    h = core.detect(l.clone(), s, 0.01, 0.45, 200, None, box_type='corner', window=4096, async_=True)
+    h._event.synchronize()
+    assert min(h._cnt_host.tolist()) < 0           # the widest window is undecided here
+    h.wait()
+    (ob, ol, os_), probs, boxes = core.detect(l, s, 0.01, 0.45, 200, None, box_type='corner', debug=True)
+    rb, rl, rs = M.detect(probs.cpu().numpy(), boxes.cpu().numpy(), 0.01, 0.45, 200, nms_variant='tv')
+    for b in range(B):
+        assert ob[b].shape[0] == 20
+        np.testing.assert_array_equal(ol[b].cpu().numpy(), rl[b])
+        np.testing.assert_array_equal(os_[b].cpu().numpy(), rs[b])
+        np.testing.assert_array_equal(ob[b].cpu().numpy(), rb[b])

@@ -131,3 +131,33 @@ def test_cpu_and_device_paths_agree():
         metrics.find_jaccard_overlap(gt, an.cuda())
     with pytest.raises(L.SbodError):
         IU.nms(torch.rand(4, 4), torch.rand(4))
+
+
+@pytest.mark.parametrize('kind', ['iou', 'giou', 'diou', 'ciou'])
+def test_overlap_gradients_both_box_sets(kind):
+    """Autograd reaches BOTH box sets in the reference (iou_utils.py:6-164): d/d bboxes2 vs the
+    oracle's torch-fp32 restatement of the same graph (with ties and the clamp masks)."""
+    from oracle import loss_ref as LR
+    d = load_golden('losses.npz')
+    p, q = torch.from_numpy(d['box_p']), torch.from_numpy(d['box_t'])
+    q = q.clone()
+    q[-3:, 0] = p[-3:, 0]                                 # exact min / max ties on x1 and y2
+    q[-3:, 3] = p[-3:, 3]
+    a, b = p.to(DEV).requires_grad_(True), q.to(DEV).requires_grad_(True)
+    o = getattr(IU, 'bbox_overlaps_' + kind)(a, b)
+    (o * torch.linspace(0.5, 1.5, o.numel(), device=DEV)).sum().backward()
+    ra, rb = p.clone().requires_grad_(True), q.clone().requires_grad_(True)
+    ro = LR.aligned_overlap(kind, ra, rb)
+    (ro * torch.linspace(0.5, 1.5, ro.numel())).sum().backward()
+    np.testing.assert_allclose(o.detach().cpu().numpy(), ro.detach().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(a.grad.cpu().numpy(), ra.grad.numpy(), rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(b.grad.cpu().numpy(), rb.grad.numpy(), rtol=1e-3, atol=1e-5)
+    # the reference exchanges the sets when rows > cols (and transposes back): a [1,4] x [n,4]
+    # call broadcasts the single box, whose gradient is the sum over the rows
+    one = p[:1].to(DEV).requires_grad_(True)
+    bb = q.to(DEV).requires_grad_(True)
+    getattr(IU, 'bbox_overlaps_' + kind)(bb, one).sum().backward()
+    r1, rbb = p[:1].clone().requires_grad_(True), q.clone().requires_grad_(True)
+    LR.aligned_overlap(kind, r1.expand_as(rbb), rbb).sum().backward()
+    np.testing.assert_allclose(one.grad.cpu().numpy(), r1.grad.numpy(), rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(bb.grad.cpu().numpy(), rbb.grad.numpy(), rtol=1e-3, atol=1e-5)
