@@ -63,6 +63,8 @@ def parse(argv=None):
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--eager', action='store_true', help='no hipGraph: launch every call each step')
+    ap.add_argument('--one-stream', action='store_true',
+                    help='graph mode: one graph per step (criterion and detect in stream order)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-dcn', action='store_true')
     ap.add_argument('--cpu-detect-images', type=int, default=2)
@@ -190,7 +192,7 @@ def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
 class Step:
     """Criterion forward+backward and detect on one batch; eager or captured in a hipGraph."""
 
-    def __init__(self, dev, B, rank, world, graph):
+    def __init__(self, dev, B, rank, world, graph, two_streams=True):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -209,6 +211,12 @@ class Step:
         # (cached per stream in core.workspace) already exists: nothing large is allocated
         # under capture
         self.cap_stream = torch.cuda.Stream(dev)
+        # graph mode: the criterion and detect are two graphs replayed on two streams, so their
+        # kernels (several latency-bound, few workgroups) run concurrently on the GPU; a
+        # fork/join INSIDE one graph costs ~30 us per edge on this runtime
+        # (scripts/probe_graph_launch.py), two graphs on two streams need no edge at all
+        self.det_stream = torch.cuda.Stream(dev)
+        self.two = two_streams
         self.graph = None
         self.use_graph = graph
         self.capture_error = None
@@ -234,6 +242,24 @@ class Step:
         loss, h = self.launch_eager()
         return loss, h.wait()
 
+    def eager_split(self):
+        """The two-stream form eagerly (warms both capture streams' workspaces): GT packing,
+        criterion forward and backward on cap_stream, detect on det_stream."""
+        self.locs.grad = None
+        self.scores.grad = None
+        with torch.cuda.stream(self.cap_stream):
+            gt = self.stage.stage(self.boxes, self.labels)
+            loss = self.crit(self.locs, self.scores, gt, None)
+        with torch.cuda.stream(self.det_stream):
+            h = self.detect(False)
+        with torch.cuda.stream(self.cap_stream):
+            loss.backward()
+        return loss, h.wait()
+
+    def detect(self, capture):
+        return core.detect(self.locs.detach(), self.det_scores, 0.01, 0.45, 200, self.priors,
+                           box_type='offset', act='softmax', async_=True, capture=capture)
+
     def capture(self, n=2, after_first=None):
         """Capture body() into ``n`` hipGraphs (the usual torch pattern: warm-up already done on
         the capture stream; gradients set to None so the captured backward owns them).  Each
@@ -246,23 +272,40 @@ class Step:
         for _ in range(n):
             self.locs.grad = None
             self.scores.grad = None
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.cap_stream):
-                loss, h = self.body(gt, capture=True)
-            self.slots.append((g, loss, h))
+            if self.two:
+                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga, stream=self.cap_stream):
+                    loss = self.crit(self.locs, self.scores, gt, None)
+                    loss.backward()
+                with torch.cuda.graph(gb, stream=self.det_stream):
+                    h = self.detect(True)
+                self.slots.append((ga, gb, loss, h))
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.cap_stream):
+                    loss, h = self.body(gt, capture=True)
+                self.slots.append((g, None, loss, h))
             if after_first is not None and len(self.slots) == 1:
                 after_first()
         torch.cuda.synchronize()
         self.graph = self.slots[0][0]
         self.k = 0
         self.pending = None
+        self.host_submit = self.host_collect = 0.0
 
     def launch_replay(self):
-        g, loss, h = self.slots[self.k % len(self.slots)]
+        ga, gb, loss, h = self.slots[self.k % len(self.slots)]
         self.k += 1
-        self.stage.stage(self.boxes, self.labels)
-        g.replay()
-        return loss, h.replayed()
+        if gb is None:
+            self.stage.stage(self.boxes, self.labels)
+            ga.replay()
+            return loss, h.replayed()
+        with torch.cuda.stream(self.cap_stream):
+            self.stage.stage(self.boxes, self.labels)
+            ga.replay()
+        with torch.cuda.stream(self.det_stream):
+            gb.replay()
+            return loss, h.replayed(self.det_stream)
 
     def replay(self):
         loss, h = self.launch_replay()
@@ -271,10 +314,15 @@ class Step:
     def pipelined(self):
         """One step, pipelined two deep: launch step k (GT packing + graph replay), then collect
         step k-1's per-image detection lists (its host sync overlaps step k on the GPU)."""
+        t0 = time.perf_counter()
         nxt = self.launch_replay()
+        t1 = time.perf_counter()
+        self.host_submit += t1 - t0
         prev, self.pending = self.pending, nxt
         if prev is not None:
-            return prev[0], prev[1].wait()
+            out = prev[0], prev[1].wait()
+            self.host_collect += time.perf_counter() - t1
+            return out
         return None
 
     def drain(self):
@@ -375,7 +423,7 @@ def main():
     torch.cuda.set_device(dev)
     L.lib()
     B = a.batch
-    st = Step(dev, B, rank, world, graph=not a.eager)
+    st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing)
     with torch.no_grad():
@@ -386,10 +434,14 @@ def main():
     # workspaces the captured calls will use)
     side = st.cap_stream
     side.wait_stream(torch.cuda.current_stream(dev))
+    st.det_stream.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
         for _ in range(max(a.warmup - 1, 1)):
-            st.eager()
-    torch.cuda.current_stream(dev).wait_stream(side)
+            if st.use_graph and st.two:
+                st.eager_split()
+            else:
+                st.eager()
+    torch.cuda.synchronize()
     # one more eager step with every instrumented kernel carrying HIP events on its dispatch:
     # the per-kernel table, and the dominant HBM-bound kernel that is timed live below
     torch.cuda.synchronize()
@@ -438,7 +490,9 @@ def main():
                 if n:
                     samples.append(ms / n)
             return out
+        st.host_submit = st.host_collect = 0.0
         elapsed = timed(graph_step, a.steps, dist, dev, finish=st.drain)
+        host_submit, host_collect = st.host_submit, st.host_collect
     else:
         L.call('sbod_timing_every', TIMING_EVERY)
         L.timing_enable(dominant)
@@ -448,18 +502,6 @@ def main():
         L.timing_enable(None)
         L.call('sbod_timing_every', 1)
     ms_step = elapsed / a.steps * 1e3
-
-    # GPU time of one step (events around the replay / the eager launches), after the timed region
-    gpu_ms = []
-    for _ in range(min(a.steps, 20)):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        _, h = st.launch()
-        e1.record()
-        h.wait()
-        e1.synchronize()
-        gpu_ms.append(e0.elapsed_time(e1))
-    gpu_ms_med = sorted(gpu_ms)[len(gpu_ms) // 2]
 
     dp = grad_allreduce_figure(st.replay if st.use_graph else st.eager, a, dist, dev, world) if dist else None
 
@@ -476,12 +518,12 @@ def main():
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
         'config': {'workload': 'SSD512 per-GPU batch %d: GT packing + MultiBoxLoss512(DIoU+focal) '
                                'fwd+bwd + detect(min_score 0.01, iou 0.45, top_k 200)%s'
-                               % (B, ', one hipGraph replay per step'
+                               % (B, (', criterion and detect hipGraphs replayed on two streams per step'
+                                      if st.two else ', one hipGraph replay per step')
                                   if st.use_graph else ', eager launches'),
                    'global_batch': world * B, 'n_priors': P, 'n_classes': N_CLASSES,
                    'parallelism': 'dp%d' % world},
         'manchors_per_sec': round(world * B * P * a.steps / elapsed / 1e6, 3),
-        'step_gpu_ms_median': round(gpu_ms_med, 4),
         'step_algorithmic_bytes': step_bytes,
         'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -504,6 +546,9 @@ def main():
     if st.use_graph:
         line['roofline']['span_clock_hz'] = L.lib().sbod_timing_clock_hz()
     line['kernel_us_per_step'] = kernel_us
+    if st.use_graph:   # host time per step: GT packing + replays, and collecting the lists
+        line['host_us_per_step'] = {'submit': round(host_submit / a.steps * 1e6, 1),
+                                    'collect_incl_wait': round(host_collect / a.steps * 1e6, 1)}
     if dp is not None:
         line['dp_train_step_with_grad_allreduce'] = dp
     if not a.no_dcn:
