@@ -12,6 +12,7 @@ import torch  # noqa: F401  (must precede the dlopen; see module docstring)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SBOD_LIB', os.path.join(_HERE, 'lib', 'libsbod_hip.so'))
 FAST_PATH = os.path.join(os.path.dirname(LIB_PATH), '_sbodcall.so')
+HOST_PATH = os.path.join(os.path.dirname(LIB_PATH), '_sbodhost.so')
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int
@@ -88,6 +89,7 @@ class SbodError(RuntimeError):
 
 _lib = None
 _fast = {}     # name -> _sbodcall wrapper (same C entry point, no ctypes argument conversion)
+host_ext = None  # the _sbodhost extension (csrc/hostpack.cpp), when built
 MISSING = []   # declared in include/sbod.h but not exported (tests assert this is empty)
 
 
@@ -129,6 +131,12 @@ def _load_fast():
         f = getattr(mod, name, None)
         if f is not None:
             _fast[name] = f
+    global host_ext
+    if os.path.exists(HOST_PATH):
+        spec = importlib.util.spec_from_file_location('_sbodhost', HOST_PATH)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        host_ext = mod
 
 
 def fastcall_names():

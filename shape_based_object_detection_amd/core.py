@@ -75,6 +75,20 @@ def _launch_pack(bx, lb, counts, capacity, out_b, out_l, out_off):
            L.stream_of(out_off))
 
 
+def _pack_fast(boxes, labels, capacity, per_image, dev_index, out_b, out_l, out_off, allow_empty):
+    """The whole list check + sbod_gt_pack launch in C++ (_sbodhost, csrc/hostpack.cpp).
+    Counts on success; None when the batch needs the Python path (conversions, errors)."""
+    ext = L.host_ext
+    if ext is None or type(boxes) is not list or type(labels) is not list:
+        return None
+    r = ext.pack_device_lists(boxes, labels, capacity, per_image, dev_index, out_b.data_ptr(),
+                              out_l.data_ptr(), out_off.data_ptr(), L.stream_of(out_off), allow_empty)
+    if type(r) is int:
+        raise L.SbodError('sbod_gt_pack failed (%d): %s'
+                          % (r, L.lib().sbod_last_error().decode(errors='replace')))
+    return r
+
+
 def pack_gt(boxes, labels, device=None, allow_empty=False):
     """Pack per-image lists into a GtPack with ONE device launch (sbod_gt_pack: the pointers
     and offsets travel in the kernel arguments).  An image with no objects raises like the
@@ -110,6 +124,8 @@ class GtStaging:
     def __init__(self, batch, capacity, device):
         self.batch, self.capacity = int(batch), int(capacity)
         self.device = torch.device(device)
+        if self.device.type == 'cuda' and self.device.index is None:
+            self.device = torch.device('cuda', torch.cuda.current_device())
         rows = self.batch * self.capacity
         # one device region, boxes | labels | offsets, so the host path is a single copy
         self._nb = (rows * 16, rows * 8, (self.batch + 1) * 4)
@@ -139,6 +155,11 @@ class GtStaging:
         if len(boxes) != self.batch or len(labels) != self.batch:
             raise ValueError('GtStaging: batch of %d images, staging holds %d'
                              % (len(boxes), self.batch))
+        if boxes[0].is_cuda:
+            counts = _pack_fast(boxes, labels, self.boxes.shape[0], self.capacity, self.device.index or 0,
+                                self.boxes, self.labels, self.offsets, allow_empty)
+            if counts is not None:
+                return GtPack(self.boxes, self.labels, self.offsets, counts, gmax=self.capacity)
         counts = [b.shape[0] for b in boxes]
         _check_counts(counts, allow_empty)
         if max(counts) > self.capacity:
