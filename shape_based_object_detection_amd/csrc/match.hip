@@ -15,6 +15,7 @@ namespace sbod {
 SBOD_STAMP_DECL
 
 constexpr int kTile = 256;
+constexpr int kMThreads = 256;   // k_match_tile: one prior per thread
 
 struct GtTile {
   float x1, y1, x2, y2, area;
@@ -70,161 +71,365 @@ __device__ __forceinline__ Anchor load_anchor(const float *anchors, const float 
   return Anchor{a.a, a.b, a.c, a.d, ax * ay, (ax < kIouEps) && (ay < kIouEps)};
 }
 
-// Phase 1 (B x P/256 workgroups): per prior the best object (first index on ties) and the
-// tile's positive count before the forced match; per object the tile's best prior as a packed
-// (ord(overlap) << 32 | ~prior) key — waves reduce through LDS and each tile writes its own
-// partial row (no global atomics: the per-object argmax is finished deterministically by
-// phase 2, equal to torch's first-index argmax because max is order independent).
-constexpr int kMaxGLds = 256;   // objects per image whose per-wave partials stay in LDS
+// Matching in two launches.
+//
+// k_match_tile (B x ceil(P / 256) workgroups, one prior per thread; 2 and 4 consecutive priors
+// per thread measured slower: fewer waves to hide the per-object latency chain):
+//   per prior: the best object (first index on ties) -> obj / ovl;
+//   per object: this tile's best prior as a packed (ord(overlap) << 32 | ~prior) key (the lowest
+//     prior on ties), for overlaps > 0 only (an object whose best overlap is <= 0 is never
+//     forced, so every such key may read 0).  No cross-lane work in the object loop: each thread
+//     leaves its overlap's ord per object in LDS, and after the loop one pass reduces the
+//     [objects x priors] table (a thread per (object, 16-prior segment), then a DPP max over the
+//     16 lanes holding one object) -> one 16-byte record per (tile, object) {key, obj and ovl of
+//     the key's prior (-1 when not known: objects beyond one LDS chunk)};
+//   a wave whose priors overlap none of an object (the common case: a wave's priors are one
+//     small patch of one feature map) skips that object's divisions: every overlap there is
+//     <= 0, which can neither raise a prior's best (>= 0 from object 0 on) nor make a key;
+//   the tile's positive count before the forced match -> tcount.
+// k_match_final (one workgroup per image): every record of the image in flight at once, the max
+// key per object through LDS, then the forced match of models/SSD512.py:546-553 (filter objects
+// whose best overlap > 0, overlap 1.0 and object j = the FILTERED position, last writer wins),
+// the positive count adjusted for exactly the priors it rewrites -> n_pos[b], n_pos[B].  Up to 64
+// objects the forced match runs in wave 0's registers (lane = object: ballots, readlanes and one
+// permute, no barrier); more objects take the LDS form.
+// (An in-launch finish by each image's last-arriving tile, with write-through records and
+// arrival counters, measured slower: the write-through drain, the counter round trip and the
+// fabric-latency record loads cost more than this launch boundary — DESIGN.md §9.)
+constexpr int kGc = 16;       // objects per chunk of the per-thread best table in LDS
+constexpr int kSegCols = 16;  // threads (columns) per first-pass reduction segment
+constexpr int kNSeg = kMThreads / kSegCols;
+
+struct MRec {   // 16-byte (tile, object) record
+  unsigned long long key;
+  int32_t obj;
+  float ovl;
+};
+
+// Max of a u64 over each row of 16 lanes, valid in every lane of the row (DPP quad swaps and
+// mirrors; keys are unique, so the max is the row's best).
+template <int kCtrl>
+__device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) {
+  const uint32_t lo = dpp_u32<kCtrl, 0xf>(static_cast<uint32_t>(v));
+  const uint32_t hi = dpp_u32<kCtrl, 0xf>(static_cast<uint32_t>(v >> 32));
+  const unsigned long long o = (static_cast<unsigned long long>(hi) << 32) | lo;
+  return o > v ? o : v;
+}
+__device__ __forceinline__ unsigned long long row16_max_u64(unsigned long long v) {
+  v = dpp_max_u64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v = dpp_max_u64<0x4E>(v);    // quad_perm [2,3,0,1]
+  v = dpp_max_u64<0x141>(v);   // row_half_mirror
+  return dpp_max_u64<0x140>(v);   // row_mirror
+}
 
 template <bool kOdm, int kFlags>
-__global__ __launch_bounds__(kTile) void k_match_tile(
+__global__ __launch_bounds__(kMThreads) void k_match_tile(
     const float *__restrict__ gt, const int64_t *__restrict__ labels,
     const int32_t *__restrict__ off, const float *__restrict__ anchors,
     const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
     float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
-    unsigned long long *__restrict__ part, int32_t *__restrict__ tcount, int32_t *__restrict__ npos,
-    int B, SpanRing *span) {
-  extern __shared__ GtTile s_gt[];
-  __shared__ unsigned long long s_key[kTile / 64][kMaxGLds];
+    MRec *__restrict__ rec, int32_t *__restrict__ tcount, int32_t *__restrict__ npos, int B,
+    SpanRing *span) {
+  // dynamic LDS: [4 * Gmax labels]
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  __shared__ __attribute__((aligned(16))) uint32_t s_ord[kGc][kMThreads];  // per object, per prior: ord
+  __shared__ uint32_t s_ev[kMThreads / 64];                                 // per wave: objects evaluated
+  __shared__ int32_t s_fo[kMThreads];                                       // final (obj, ovl) per prior
+  __shared__ float s_fv[kMThreads];
+  __shared__ int s_red[16];
   STAMP_BEGIN();
   span_begin(span);
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) npos[B] = 0;  // phase 2 accumulates
-  __shared__ int32_t s_lab[kMaxGLds];
-  __shared__ int s_red[16];
   PHASE_DECL;
   SEG_PHASE(0);
-  const int b = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t *s_lab = reinterpret_cast<int32_t *>(s_dyn);
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ntile = gridDim.x;
-  // the prior's own load goes out first: it does not wait on the ground-truth chain
-  const int p = blockIdx.x * kTile + threadIdx.x;
+  if (blockIdx.x == 0 && b == 0 && tid == 0) npos[B] = 0;   // k_match_final accumulates
+  const int tbase = blockIdx.x * kMThreads;
+  const int p = tbase + tid;
   const bool valid = p < P;
-  Anchor a{0.f, 0.f, 0.f, 0.f, 0.f, false};
-  if (valid) a = load_anchor<kOdm>(anchors, priors, b, P, p);
-  const int g0 = off[b], G = off[b + 1] - g0;
-  load_gt_tile(s_gt, gt, g0, G);
-  for (int i = threadIdx.x; i < G && i < kMaxGLds; i += blockDim.x)
-    s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
-  __syncthreads();
+  const Anchor a = load_anchor<kOdm>(anchors, priors, b, P, min(p, P - 1));
+  const int g0 = ld_i32_uniform(off + b), G = ld_i32_uniform(off + b + 1) - g0;
+  // labels are needed only after the object loop (the chunk barrier orders them)
+  for (int i = tid; i < G; i += kMThreads) s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
+  // the wave's prior bounding box as monotone integer keys, so each object's "does any prior of
+  // this wave overlap it" test runs on the scalar unit: an object outside the box has
+  // iw <= 0 or ih <= 0 for every prior of the wave (overlap 0 or -1, never a key, never a new
+  // best after object 0), so its divisions are skipped exactly
+  const bool live = valid && !a.zero;
+  const uint32_t wx1 = ~wave_max_u32(live ? ~f2ord(a.x1) : 0u), wy1 = ~wave_max_u32(live ? ~f2ord(a.y1) : 0u);
+  const uint32_t wx2 = wave_max_u32(live ? f2ord(a.x2) : 0u), wy2 = wave_max_u32(live ? f2ord(a.y2) : 0u);
+  const bool wlive = __ballot(live) != 0ull;
   SEG_PHASE(1);
   float best = 0.f;
   int bi = 0;
-  const int pw = blockIdx.x * kTile + wv * 64;   // prior of lane 0 of this wave
-  unsigned long long *prow = part + (static_cast<int64_t>(b) * ntile + blockIdx.x) * Gmax;
-  for (int g = 0; g < G; ++g) {
-    const float ov = iou_metrics(s_gt[g], a.x1, a.y1, a.x2, a.y2, a.area, a.zero);
-    if (g == 0 || ov > best) {
-      best = ov;
-      bi = g;
+  const bool one_chunk = G <= kGc;
+  MRec *rrow = rec + (static_cast<int64_t>(b) * ntile + blockIdx.x) * Gmax;
+  for (int gc = 0; gc < G; gc += kGc) {
+    const int gn = min(G - gc, kGc);
+    uint32_t ev = 0u;   // objects of this chunk evaluated by this wave (wave-uniform)
+    for (int j0 = 0; j0 < gn; j0 += 4) {
+      Box4 t[4];   // uniform loads: scalar registers, four objects in flight
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = ld4_uniform(gt + 4 * static_cast<int64_t>(g0 + gc + min(j0 + u, gn - 1)));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + u;
+        if (j >= gn) break;
+        const int g = gc + j;
+        const bool hitw = wlive && f2ord(t[u].c) > wx1 && f2ord(t[u].a) < wx2 && f2ord(t[u].d) > wy1 &&
+                          f2ord(t[u].b) < wy2;
+        // object 0 is always evaluated (it sets every prior's first best, ties included)
+        if (g == 0 || hitw) {   // metrics.py:224-250, in the reference's order
+          const float gx = t[u].c - t[u].a, gy = t[u].d - t[u].b;
+          const float garea = gx * gy;
+          const bool gzero = (fabsf(gx) < kIouEps) && (fabsf(gy) < kIouEps);
+          float iw = fminf(t[u].c, a.x2) - fmaxf(t[u].a, a.x1);
+          if (iw < 0.f) iw = 0.f;
+          float ih = fminf(t[u].d, a.y2) - fmaxf(t[u].b, a.y1);
+          if (ih < 0.f) ih = 0.f;
+          const float inner = iw * ih;
+          float ov = inner / (((garea + a.area) - inner) + kIouEps);
+          if (gzero) ov = 0.f;
+          if (a.zero) ov = -1.f;
+          if (g == 0 || ov > best) {
+            best = ov;
+            bi = g;
+          }
+          s_ord[j][tid] = (valid && ov > 0.f) ? f2ord(ov) : 0u;
+          ev |= 1u << j;
+        }
+      }
     }
-    // the wave's best (ord(overlap), lowest prior) — torch's first-index argmax over priors:
-    // max of the 32-bit ord over the wave (DPP), then the lowest lane holding it (ballot)
-    const uint32_t ko = valid ? f2ord(ov) : 0u;   // f2ord of any real overlap is > 0
-    const uint32_t mx = wave_max_u32(ko);
-    const unsigned long long hit = __ballot(valid && ko == mx);
-    if (lane == 0) {
-      const unsigned long long key =
-          hit ? ((static_cast<unsigned long long>(mx) << 32) |
-                 (0xffffffffull - static_cast<uint32_t>(pw + __builtin_ctzll(hit))))
-              : 0ull;
-      if (G <= kMaxGLds) s_key[wv][g] = key;
-      else if (key) atomicMax(prow + g, key);   // very large G: partial row via atomics
+    if (lane == 0) s_ev[wv] = ev;
+    if (one_chunk) {
+      s_fo[tid] = bi;
+      s_fv[tid] = best;
     }
+    __syncthreads();
+    // thread -> (object j = tid / 16, segment sg = tid % 16 of 16 priors): the segment's best
+    // (ord, lowest prior), then the max over the row of 16 lanes = the tile's key of object j
+    {
+      const int j = tid / kNSeg, sg = tid - j * kNSeg;
+      unsigned long long kb = 0ull;
+      if (j < gn && ((s_ev[sg / (64 / kSegCols)] >> j) & 1u)) {
+        const uint4 *row = reinterpret_cast<const uint4 *>(&s_ord[j][sg * kSegCols]);
+        uint32_t v[kSegCols];
+#pragma unroll
+        for (int q = 0; q < kSegCols / 4; ++q) {
+          const uint4 x = row[q];
+          v[4 * q] = x.x;
+          v[4 * q + 1] = x.y;
+          v[4 * q + 2] = x.z;
+          v[4 * q + 3] = x.w;
+        }
+        uint32_t m8[8], m4[4];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) m8[c] = max(v[c], v[c + 8]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) m4[c] = max(m8[c], m8[c + 4]);
+        const uint32_t mx = max(max(m4[0], m4[2]), max(m4[1], m4[3]));
+        uint32_t mask = 0u;
+#pragma unroll
+        for (int c = 0; c < kSegCols; ++c) mask |= (v[c] == mx ? 1u : 0u) << c;
+        const int c0 = __builtin_ctz(mask);   // mask != 0: mx is one of v
+        kb = mx ? ((static_cast<unsigned long long>(mx) << 32) |
+                   (0xffffffffull - static_cast<uint32_t>(tbase + sg * kSegCols + c0)))
+                : 0ull;
+      }
+      kb = row16_max_u64(kb);
+      if (sg == 0 && j < gn) {
+        // the prior's final (obj, ovl) when every object is in this chunk
+        int32_t o = -1;
+        float v = 0.f;
+        if (one_chunk && kb) {
+          const int lp = static_cast<int>(0xffffffffu - static_cast<uint32_t>(kb)) - tbase;
+          o = s_fo[lp];
+          v = s_fv[lp];
+        }
+        rrow[gc + j] = MRec{kb, o, v};
+      }
+    }
+    if (gc + kGc < G) __syncthreads();   // s_ord / s_ev are rewritten by the next chunk
   }
   SEG_PHASE(2);
   int pos = 0;
   if (valid) {
-    obj[static_cast<int64_t>(b) * P + p] = bi;
-    ovl[static_cast<int64_t>(b) * P + p] = best;
-    const int lab = G <= kMaxGLds ? s_lab[bi] : static_cast<int>(labels[g0 + bi]);
-    int c = best < thr ? 0 : lab;
+    const int64_t i = static_cast<int64_t>(b) * P + p;
+    obj[i] = bi;
+    ovl[i] = best;
+    int c = best < thr ? 0 : s_lab[bi];
     if ((kFlags & SBOD_MATCH_BINARY) != 0) c = c > 0;
     pos = c > 0;
     if constexpr (kOdm) {
-      const int64_t i = static_cast<int64_t>(b) * P + p;
       const float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
       const float m = fmaxf(z0, z1);
       const float e0 = expf(z0 - m), e1 = expf(z1 - m);
       if (e1 / (e0 + e1) < theta) pos = 0;
     }
   }
-  pos = block_sum(pos, s_red);  // contains __syncthreads: s_key complete after it
-  if (G <= kMaxGLds) {
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-      unsigned long long k = s_key[0][g];
-      for (int w = 1; w < kTile / 64; ++w) k = s_key[w][g] > k ? s_key[w][g] : k;
-      prow[g] = k;
-    }
-  }
-  if (threadIdx.x == 0) tcount[b * ntile + blockIdx.x] = pos;
+  pos = block_sum(pos, s_red);
+  if (tid == 0) tcount[b * ntile + blockIdx.x] = pos;
   span_end(span);
   SEG_PHASE(3);
 #ifdef SBOD_PHASE_CLOCKS
   if (PHASE_PRINT_SEL)
-    printf("match x%d b%d G=%d: gt %lld iou+argmax %lld store+sum %lld total %lld\n", blockIdx.x, b, G,
+    printf("match_tile x%d b%d G=%d: start %lld objects+keys %lld store+sum %lld total %lld\n", blockIdx.x, b, G,
            ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
 #endif
   STAMP_END(5, 1);
 }
 
-// Phase 2 (one wave per image): finish the per-object argmax over the tiles, then the forced
-// match of models/SSD512.py:546-553 applied serially — filter objects whose best overlap > 0,
-// overlap 1.0 and object j (the FILTERED position, last writer wins) — adjusting the positive
-// count for exactly the priors it rewrites.
+// k_match_final: one workgroup of kFThreads per image.
+constexpr int kFThreads = 256;
+constexpr int kFRegs = 4;   // records per thread kept in registers (G * ntile <= 1024)
+
 template <int kFlags>
-__global__ __launch_bounds__(256) void k_match_final(
-    const int64_t *__restrict__ labels, const int32_t *__restrict__ off,
-    const unsigned long long *__restrict__ part, const int32_t *__restrict__ tcount, int ntile,
-    int Gmax, int P, float thr, const float *__restrict__ arm_scores, float theta,
-    int32_t *__restrict__ obj, float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
-  // LDS per object g: best key, its prior, the prior's phase-1 (obj, ovl), easy flag, label
-  extern __shared__ unsigned long long s_best[];
-  int32_t *s_pr = reinterpret_cast<int32_t *>(s_best + Gmax);
-  int32_t *s_o0 = s_pr + Gmax;
+__global__ __launch_bounds__(kFThreads) void k_match_final(
+    const int64_t *__restrict__ labels, const int32_t *__restrict__ off, const MRec *__restrict__ rec,
+    const int32_t *__restrict__ tcount, int ntile, int Gmax, int P, float thr,
+    const float *__restrict__ arm_scores, float theta, int32_t *__restrict__ obj,
+    float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
+  // LDS per object g: best key, its prior's phase-1 (obj, ovl), label; the LDS forced-match
+  // form also uses prior / easy | previous writer / final object
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  unsigned long long *s_best = reinterpret_cast<unsigned long long *>(s_dyn);
+  int32_t *s_o0 = reinterpret_cast<int32_t *>(s_best + Gmax);
   float *s_v0 = reinterpret_cast<float *>(s_o0 + Gmax);
   int32_t *s_lab = reinterpret_cast<int32_t *>(s_v0 + Gmax);
-  int32_t *s_easy = s_lab + Gmax;
-  int32_t *s_new = s_easy + Gmax;     // final object written for this g's prior, -1 = superseded
+  int32_t *s_pr = s_lab + Gmax;
+  int32_t *s_easy = s_pr + Gmax;
+  int32_t *s_new = s_easy + Gmax;
   __shared__ int s_red[16];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int s_cnt;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g0 = off[b], G = off[b + 1] - g0;
-  const unsigned long long *pb = part + static_cast<int64_t>(b) * ntile * Gmax;
-  for (int g = tid; g < G; g += blockDim.x) {
+  const MRec *rb = rec + static_cast<int64_t>(b) * ntile * Gmax;
+  const int n = G * ntile;
+  const bool inreg = n <= kFRegs * kFThreads;
+  // every record of the image (and the tile counts) in flight at once
+  MRec r[kFRegs];
+#pragma unroll
+  for (int q = 0; q < kFRegs; ++q) {
+    const int it = min(tid + q * kFThreads, max(n - 1, 0));
+    const int g = it / ntile, t = it - g * ntile;
+    r[q] = (inreg && n > 0) ? rb[static_cast<int64_t>(t) * Gmax + g] : MRec{0ull, 0, 0.f};
+  }
+  int cnt = 0;
+  for (int t = tid; t < ntile; t += kFThreads) cnt += tcount[b * ntile + t];
+  for (int g = tid; g < G; g += kFThreads) {
     s_best[g] = 0ull;
     s_lab[g] = static_cast<int32_t>(labels[g0 + g]);
   }
+  if (tid == 0) s_cnt = 0;
   __syncthreads();
-  for (int it = tid; it < G * ntile; it += blockDim.x) {   // all tile partials in flight at once
-    const int g = it / ntile, t = it - g * ntile;
-    atomicMax(&s_best[g], pb[static_cast<int64_t>(t) * Gmax + g]);
-  }
-  int cnt = 0;
-  for (int t = tid; t < ntile; t += blockDim.x) cnt += tcount[b * ntile + t];
-  cnt = block_sum(cnt, s_red);
-  for (int g = tid; g < G; g += blockDim.x) {
-    const unsigned long long k = s_best[g];
-    int p = -1;
-    if (ord2f(static_cast<uint32_t>(k >> 32)) > 0.f) {
-      p = static_cast<int>(0xffffffffu - static_cast<uint32_t>(k));
-      const int64_t i = static_cast<int64_t>(b) * P + p;
-      s_o0[g] = obj[i];
-      s_v0[g] = ovl[i];
-      int easy = 0;
-      if constexpr ((kFlags & SBOD_MATCH_ODM) != 0) {
-        const float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
-        const float m = fmaxf(z0, z1);
-        const float e0 = expf(z0 - m), e1 = expf(z1 - m);
-        easy = e1 / (e0 + e1) < theta;
-      }
-      s_easy[g] = easy;
+  cnt = wave_sum_i32(cnt);
+  if (lane == 0 && cnt) atomicAdd(&s_cnt, cnt);
+  if (inreg) {
+#pragma unroll
+    for (int q = 0; q < kFRegs; ++q) {
+      const int it = tid + q * kFThreads;
+      if (it < n && r[q].key) atomicMax(&s_best[it / ntile], r[q].key);
     }
-    s_pr[g] = p;
+  } else {
+    for (int it = tid; it < n; it += kFThreads) {
+      const int g = it / ntile, t = it - g * ntile;
+      const unsigned long long k = rb[static_cast<int64_t>(t) * Gmax + g].key;
+      if (k) atomicMax(&s_best[g], k);
+    }
   }
   __syncthreads();
-  // The forced match (SSD512.py:546-553) without a serial loop: object g's filtered position j_g
-  // is the number of valid objects before it; a prior forced more than once keeps its LAST
-  // writer, and each writer's "old" state is the previous writer's (or the phase-1 state).
-  for (int g = tid; g < G; g += blockDim.x) {
+  // the winning record of each object supplies its prior's phase-1 (obj, ovl)
+  auto take = [&](int g, const MRec &x) {
+    if (x.key && x.key == s_best[g]) {
+      int32_t o = x.obj;
+      float v = x.ovl;
+      if (o < 0) {   // not carried (more objects than one tile chunk): phase 1's outputs
+        const int64_t i = static_cast<int64_t>(b) * P + static_cast<int>(0xffffffffu - static_cast<uint32_t>(x.key));
+        o = obj[i];
+        v = ovl[i];
+      }
+      s_o0[g] = o;
+      s_v0[g] = v;
+    }
+  };
+  if (inreg) {
+#pragma unroll
+    for (int q = 0; q < kFRegs; ++q) {
+      const int it = tid + q * kFThreads;
+      if (it < n) take(it / ntile, r[q]);
+    }
+  } else {
+    for (int it = tid; it < n; it += kFThreads) {
+      const int g = it / ntile, t = it - g * ntile;
+      take(g, rb[static_cast<int64_t>(t) * Gmax + g]);
+    }
+  }
+  __syncthreads();
+  const int cnt1 = s_cnt;
+  auto is_pos = [&](int o, float v, int easy) {
+    int c = v < thr ? 0 : s_lab[o];
+    if ((kFlags & SBOD_MATCH_BINARY) != 0) c = c > 0;
+    return c > 0 && !easy;
+  };
+  auto easy_of = [&](int p) {
+    int easy = 0;
+    if constexpr ((kFlags & SBOD_MATCH_ODM) != 0) {
+      const int64_t i = static_cast<int64_t>(b) * P + p;
+      const float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
+      const float m = fmaxf(z0, z1);
+      const float e0 = expf(z0 - m), e1 = expf(z1 - m);
+      easy = e1 / (e0 + e1) < theta;
+    }
+    return easy;
+  };
+  auto publish = [&](int delta) {   // one lane
+    const int nb = cnt1 + delta;
+    npos[b] = nb;
+    atomicAdd(npos + B, nb);
+  };
+  if (G <= 64) {
+    if (wv == 0) {   // lane = object, everything in registers
+      const unsigned long long k = lane < G ? s_best[lane] : 0ull;
+      const int p = k ? static_cast<int>(0xffffffffu - static_cast<uint32_t>(k)) : -1;
+      const unsigned long long valid = __ballot(p >= 0);
+      const int j = __popcll(valid & ((1ull << lane) - 1ull));   // filtered position
+      int prev = -1;      // the previous writer of the same prior
+      bool lastw = true;  // no later writer of the same prior
+      for (int h = 0; h < G; ++h) {
+        const int ph = __builtin_amdgcn_readlane(p, h);
+        if (p >= 0 && ph == p) {
+          if (h < lane) prev = h;
+          if (h > lane) lastw = false;
+        }
+      }
+      const int jprev = __shfl(j, prev < 0 ? lane : prev, 64);
+      int d = 0;
+      if (p >= 0) {
+        const int easy = easy_of(p);
+        const int o_old = prev >= 0 ? jprev : s_o0[lane];
+        const float v_old = prev >= 0 ? 1.0f : s_v0[lane];
+        d = (is_pos(j, 1.0f, easy) ? 1 : 0) - (is_pos(o_old, v_old, easy) ? 1 : 0);
+        if (lastw) {
+          const int64_t i = static_cast<int64_t>(b) * P + p;
+          obj[i] = j;
+          ovl[i] = 1.0f;
+        }
+      }
+      const int delta = wave_sum_i32(d);
+      if (lane == 0) publish(delta);
+    }
+    return;
+  }
+  // more objects: the LDS form of the same rules
+  for (int g = tid; g < G; g += kFThreads) {
+    const unsigned long long k = s_best[g];
+    const int p = k ? static_cast<int>(0xffffffffu - static_cast<uint32_t>(k)) : -1;
+    s_pr[g] = p;
+    s_easy[g] = p >= 0 ? easy_of(p) : 0;
+  }
+  __syncthreads();
+  for (int g = tid; g < G; g += kFThreads) {
     int j = 0, prev = -1;
     const int p = s_pr[g];
     for (int h = 0; h < g; ++h) {
@@ -234,18 +439,12 @@ __global__ __launch_bounds__(256) void k_match_final(
         if (ph == p) prev = h;
       }
     }
-    s_o0[g] = p >= 0 ? s_o0[g] : 0;
     s_new[g] = p >= 0 ? j : -1;
-    s_easy[g] = (s_easy[g] & 1) | (prev >= 0 ? ((prev + 1) << 1) : 0);  // pack prev into easy
+    s_easy[g] = p >= 0 ? ((s_easy[g] & 1) | (prev >= 0 ? ((prev + 1) << 1) : 0)) : 0;
   }
   __syncthreads();
-  auto is_pos = [&](int o, float v, int easy) {
-    int c = v < thr ? 0 : s_lab[o];
-    if ((kFlags & SBOD_MATCH_BINARY) != 0) c = c > 0;
-    return c > 0 && !easy;
-  };
   int delta = 0;
-  for (int g = tid; g < G; g += blockDim.x) {
+  for (int g = tid; g < G; g += kFThreads) {
     if (s_pr[g] < 0) continue;
     const int easy = s_easy[g] & 1, prev = (s_easy[g] >> 1) - 1;
     const int o_old = prev >= 0 ? s_new[prev] : s_o0[g];
@@ -253,21 +452,18 @@ __global__ __launch_bounds__(256) void k_match_final(
     delta += (is_pos(s_new[g], 1.0f, easy) ? 1 : 0) - (is_pos(o_old, v_old, easy) ? 1 : 0);
   }
   delta = block_sum(delta, s_red);
-  for (int g = tid; g < G; g += blockDim.x) {
+  for (int g = tid; g < G; g += kFThreads) {
     const int p = s_pr[g];
     if (p < 0) continue;
-    bool last = true;                                  // superseded by a later writer?
-    for (int h = g + 1; h < G && last; ++h)
-      if (s_pr[h] == p) last = false;
-    if (!last) continue;
+    bool lastw = true;   // superseded by a later writer?
+    for (int h = g + 1; h < G && lastw; ++h)
+      if (s_pr[h] == p) lastw = false;
+    if (!lastw) continue;
     const int64_t i = static_cast<int64_t>(b) * P + p;
     obj[i] = s_new[g];
     ovl[i] = 1.0f;
   }
-  if (tid == 0) {
-    npos[b] = cnt + delta;
-    atomicAdd(npos + B, cnt + delta);
-  }
+  if (tid == 0) publish(delta);
 }
 
 // Pairwise IoU matrix out[b, g, p].
@@ -417,20 +613,20 @@ __global__ __launch_bounds__(1024) void k_ssd_match_final(
 using namespace sbod;
 
 namespace {
+// Matcher workspace: the per-(tile, object) 16-byte records [B][ntile][Gmax], then the per-tile
+// positive counts [B][ntile].
 struct MatchWs {
-  unsigned long long *part, *best;
+  MRec *rec;
   int32_t *tcount;
   size_t bytes;
 };
 MatchWs carve_match(void *w, int B, int Gmax, int P) {
-  const size_t ntile = (P + kTile - 1) / kTile;
+  const size_t ntile = (P + kMThreads - 1) / kMThreads;
   char *c = static_cast<char *>(w);
   MatchWs r;
   size_t o = 0;
-  r.part = reinterpret_cast<unsigned long long *>(c + o);
-  o += align_up(static_cast<size_t>(B) * ntile * Gmax * 8);
-  r.best = reinterpret_cast<unsigned long long *>(c + o);
-  o += align_up(static_cast<size_t>(B) * Gmax * 8);
+  r.rec = reinterpret_cast<MRec *>(c + o);
+  o += align_up(static_cast<size_t>(B) * ntile * Gmax * sizeof(MRec));
   r.tcount = reinterpret_cast<int32_t *>(c + o);
   o += align_up(static_cast<size_t>(B) * ntile * 4);
   r.bytes = o;
@@ -479,41 +675,30 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
     return SBOD_E_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
-  const int ntile = (P + kTile - 1) / kTile;
+  const int ntile = (P + kMThreads - 1) / kMThreads;
   MatchWs w = carve_match(workspace, B, Gmax, P);
-  if (Gmax > kMaxGLds &&
-      hipMemsetAsync(w.part, 0, static_cast<size_t>(B) * ntile * Gmax * 8, s) != hipSuccess)
-    return launch_status("hipMemsetAsync(match)");
   dim3 grid(ntile, B);
-  const size_t lds = Gmax * sizeof(GtTile);
-#define SBOD_TILE(ODM, FL)                                                                      \
+#define SBOD_MATCH(ODM, FL)                                                                     \
   do {                                                                                          \
-    KernelTimer kt("k_match_tile", s, true);                                                          \
-    tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kTile), lds, s, gt_boxes, gt_labels,   \
-                       gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, \
-                       ovl, w.part, w.tcount, n_pos, B, kt.span());                              \
+    {                                                                                           \
+      KernelTimer kt("k_match_tile", s, true);                                                  \
+      tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads), static_cast<size_t>(Gmax) * 4, s, \
+              gt_boxes, gt_labels, gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, \
+              theta, obj, ovl, w.rec, w.tcount, n_pos, B, kt.span());                           \
+    }                                                                                           \
+    SBOD_LAUNCHED("k_match_tile");                                                              \
+    KernelTimer kt("k_match_final", s, true);                                                   \
+    tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(kFThreads), static_cast<size_t>(Gmax) * 32, s, \
+            gt_labels, gt_offsets, w.rec, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, \
+            obj, ovl, n_pos, B);                                                                \
   } while (0)
-#define SBOD_FINAL(FL)                                                                          \
-  do {                                                                                          \
-    KernelTimer kt("k_match_final", s, true);                                                         \
-    tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(256), Gmax * 32, s, gt_labels, gt_offsets, \
-                       w.part, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B); \
-  } while (0)
-  if (odm) {
-    SBOD_TILE(true, SBOD_MATCH_ODM);
-    SBOD_LAUNCHED("k_match_tile");
-    SBOD_FINAL(SBOD_MATCH_ODM);
-  } else if (flags & SBOD_MATCH_BINARY) {
-    SBOD_TILE(false, SBOD_MATCH_BINARY);
-    SBOD_LAUNCHED("k_match_tile");
-    SBOD_FINAL(SBOD_MATCH_BINARY);
-  } else {
-    SBOD_TILE(false, 0);
-    SBOD_LAUNCHED("k_match_tile");
-    SBOD_FINAL(0);
-  }
-#undef SBOD_TILE
-#undef SBOD_FINAL
+  if (odm)
+    SBOD_MATCH(true, SBOD_MATCH_ODM);
+  else if (flags & SBOD_MATCH_BINARY)
+    SBOD_MATCH(false, SBOD_MATCH_BINARY);
+  else
+    SBOD_MATCH(false, 0);
+#undef SBOD_MATCH
   SBOD_LAUNCHED("k_match_final");
   return SBOD_OK;
 }

@@ -81,11 +81,17 @@ struct SpanRing {
 __device__ __forceinline__ unsigned span_block_id() {
   return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
 }
+// (The grid values are read outside the thread-0 branch: a uniform value first read inside a
+// divergent branch becomes a per-lane phi at the join, and every later use of it — blockIdx,
+// gridDim, addresses built from them — is demoted from scalar to vector registers and loads.)
 __device__ __forceinline__ void span_begin(SpanRing *r) {
-  if (r == nullptr || threadIdx.x != 0) return;
+  if (r == nullptr) return;
   const unsigned blk = span_block_id();
-  if (blk == 0) r->nblocks = static_cast<unsigned long long>(gridDim.x) * gridDim.y * gridDim.z;
-  if (blk < kSpanBlocks) r->t[blk][0] = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long nb = static_cast<unsigned long long>(gridDim.x) * gridDim.y * gridDim.z;
+  if (threadIdx.x == 0) {
+    if (blk == 0) r->nblocks = nb;
+    if (blk < kSpanBlocks) r->t[blk][0] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 // Synchronises the workgroup; must be reached by all of its threads.  Each thread first waits
 // for its own outstanding memory operations (s_waitcnt 0: stores acknowledged by L2), so the end
@@ -226,6 +232,15 @@ __device__ __forceinline__ Box4 ld4(const float *p) {
   float4 v = *reinterpret_cast<const float4 *>(p);
   return Box4{v.x, v.y, v.z, v.w};
 }
+// A uniform load through the constant address space: becomes a scalar (s_load) when the address
+// is wave-uniform.  Only for data no workgroup writes during the kernel.
+__device__ __forceinline__ Box4 ld4_uniform(const float *p) {
+  const __attribute__((address_space(4))) float *q = (const __attribute__((address_space(4))) float *)(p);
+  return Box4{q[0], q[1], q[2], q[3]};
+}
+__device__ __forceinline__ int32_t ld_i32_uniform(const int32_t *p) {
+  return *(const __attribute__((address_space(4))) int32_t *)(p);
+}
 __device__ __forceinline__ void st4(float *p, Box4 b) {
   *reinterpret_cast<float4 *>(p) = make_float4(b.a, b.b, b.c, b.d);
 }
@@ -238,6 +253,33 @@ __device__ __forceinline__ void st4_nt(float *p, Box4 b) {
 }
 __device__ __forceinline__ void st4_nt(float *p, float4 b) { st4_nt(p, Box4{b.x, b.y, b.z, b.w}); }
 __device__ __forceinline__ void st_nt(unsigned long long *p, unsigned long long v) { __builtin_nontemporal_store(v, p); }
+
+// Write-through (sc1) stores and L1-bypassing (sc1) loads for in-launch hand-offs between
+// workgroups (MI355X_MICROARCH.md, inter-workgroup visibility: every handed-off byte stored sc1
+// and drained by its storing wave before the signalling add; every load of it sc1).  <= 8 bytes:
+// agent-scope relaxed atomics on global pointers (global_store/load ... sc1); 16 bytes: a raw
+// buffer store with the sc1 cache-policy bit over a wave-uniform descriptor.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+__device__ __forceinline__ void st_wt_u64(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store((gu64 *)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_wt_u64(const unsigned long long *p) {
+  return __hip_atomic_load((gu64 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt_u32(int32_t *p, uint32_t v) {
+  __hip_atomic_store((gu32 *)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_wt_u32(const int32_t *p) {
+  return __hip_atomic_load((gu32 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kCpolSc1 = 16;   // gfx950 cache-policy bit SC1 in the buffer intrinsics' aux word
+// 16 bytes written through at byte offset `off` of the wave-uniform region [base, base + bytes).
+__device__ __forceinline__ void st_wt_b128(void *base, uint32_t bytes, uint32_t off, u32x4_t v) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), static_cast<int>(bytes), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, static_cast<int>(off), 0, kCpolSc1);
+}
 
 // [n] floats global -> LDS, 16 bytes per lane when the source is 16-byte aligned.
 // Global -> LDS copy of n floats by the whole block.  Loads are issued in batches of 8 per

@@ -50,8 +50,10 @@ def test_match_golden():
 
 @pytest.mark.parametrize('arch,B,seed,maxg', [('SSD512', 32, 0, 16), ('SSD300', 4, 1, 16),
                                               ('RETINA', 32, 2, 16), ('REFINEDET', 16, 3, 40),
-                                              ('SSD512', 5, 4, 200)])
+                                              ('SSD512', 5, 4, 200), ('SSD512', 3, 5, 600),
+                                              ('SSD300', 2, 6, 4096)])
 def test_match_vs_oracle(arch, B, seed, maxg):
+    """maxg > 256: objects reduced in several LDS chunks per tile; 4096 = the ABI's maximum."""
     P = prior_table(arch)
     pri = torch.from_numpy(P).to(DEV)
     pxy_np = M.cxcy_to_xy(P)
@@ -71,6 +73,42 @@ def test_match_vs_oracle(arch, B, seed, maxg):
         assert int(npos[b]) == int((c > 0).sum())
         tot += int((c > 0).sum())
     assert int(npos[B]) == tot
+
+
+def _check_oracle(boxes, labels, obj, ovl, npos, pxy_np):
+    tot = 0
+    for b in range(len(boxes)):
+        o, v, c, n = M.match_criterion(boxes[b], labels[b], pxy_np)
+        np.testing.assert_array_equal(obj[b].cpu().numpy(), o)
+        np.testing.assert_array_equal(ovl[b].cpu().numpy(), v)
+        assert int(npos[b]) == int((c > 0).sum())
+        tot += int((c > 0).sum())
+    assert int(npos[len(boxes)]) == tot
+
+
+def test_match_forced_collisions_and_counter_reuse():
+    """Objects that share a best prior (identical boxes, tiny boxes around one point): the forced
+    match's last writer wins and the positive count follows it.  Calls with different batch
+    sizes on one workspace: the in-launch arrival counters are left zero by every call."""
+    P = prior_table('SSD512')
+    pxy_np = M.cxcy_to_xy(P)
+    pxy = torch.from_numpy(pxy_np).to(DEV)
+    rng = np.random.default_rng(7)
+    boxes, labels = [], []
+    for b in range(6):
+        xy = rng.uniform(0, 0.6, (5, 2)).astype(np.float32)
+        wh = rng.uniform(0.05, 0.35, (5, 2)).astype(np.float32)
+        base = np.concatenate([xy, xy + wh], 1)
+        c = rng.uniform(0.2, 0.8, 2).astype(np.float32)
+        tiny = np.concatenate([np.tile(c - 1e-3, (4, 1)), np.tile(c + 1e-3, (4, 1))], 1)
+        tiny[:, :2] -= np.arange(4, dtype=np.float32)[:, None] * 1e-4
+        bx = np.concatenate([np.repeat(base[:2], 3, 0), base[2:], tiny]).astype(np.float32)
+        boxes.append(bx)
+        labels.append(rng.integers(1, 21, bx.shape[0]).astype(np.int64))
+    for sel in (range(6), range(2), range(6), [5]):
+        bs, ls = [boxes[i] for i in sel], [labels[i] for i in sel]
+        obj, ovl, npos = core.match(_gt(bs, ls), pxy, P.shape[0])
+        _check_oracle(bs, ls, obj, ovl, npos, pxy_np)
 
 
 def test_refinedet_arm_odm():
