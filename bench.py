@@ -220,6 +220,7 @@ class Step:
         self.graph = None
         self.use_graph = graph
         self.capture_error = None
+        self.fast = None
 
     def body(self, gt, capture=False):
         """The step's device work, in stream order on the current stream: criterion forward,
@@ -289,13 +290,27 @@ class Step:
                 after_first()
         torch.cuda.synchronize()
         self.graph = self.slots[0][0]
+        # raw handles for the one-call submit (C++: GT packing + both replays + detect event)
+        self.fast = None
+        if self.two and L.host_ext is not None:
+            self.fast = []
+            for ga, gb, _, h in self.slots:
+                h.replayed(self.det_stream)          # creates the event (recorded once here)
+                self.fast.append((core.graph_launches([(ga, self.cap_stream), (gb, self.det_stream)]),
+                                  h._event.cuda_event, self.det_stream.cuda_stream))
+            torch.cuda.synchronize()
         self.k = 0
         self.pending = None
         self.host_submit = self.host_collect = 0.0
 
     def launch_replay(self):
-        ga, gb, loss, h = self.slots[self.k % len(self.slots)]
+        i = self.k % len(self.slots)
+        ga, gb, loss, h = self.slots[i]
         self.k += 1
+        if self.fast is not None:
+            launches, ev, ev_stream = self.fast[i]
+            if self.stage.stage_and_replay(self.boxes, self.labels, launches, ev, ev_stream) is not None:
+                return loss, h.rearmed()
         if gb is None:
             self.stage.stage(self.boxes, self.labels)
             ga.replay()

@@ -72,6 +72,13 @@ int sbod_timing_reset_graphs(void);
  * recorded behind it.  Cheaper on the host than a framework-level non_blocking copy. */
 int sbod_memcpy_d2h_async(void *dst_host, const void *src_dev, size_t bytes, void *stream);
 
+/* Replay of a captured step without a framework round trip per call: launch an instantiated
+ * hipGraphExec_t on `stream` (torch: CUDAGraph.raw_cuda_graph_exec()), and record a hipEvent_t
+ * (torch: Event.cuda_event) on `stream`.  Used by the host extension's one-call step submit
+ * (GT packing + the criterion and detect graphs on their streams + the detect event). */
+int sbod_graph_launch(void *graph_exec, void *stream);
+int sbod_event_record(void *event, void *stream);
+
 /* ---------------------------------------------------------------- f1: ground-truth packing
  * Replaces the per-step GT handling of every criterion: the collate_fn list-of-tensors batch
  * (dataset/Datasets.py:58-86), moved to the device image by image (train_anchor.py:266-268) and

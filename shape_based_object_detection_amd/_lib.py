@@ -57,6 +57,8 @@ SIGNATURES = {
     'sbod_timing_reset_graphs': (I32, []),
     'sbod_timing_clock_hz': (ctypes.c_double, []),
     'sbod_memcpy_d2h_async': (I32, [P, P, SZ, P]),
+    'sbod_graph_launch': (I32, [P, P]),
+    'sbod_event_record': (I32, [P, P]),
     'sbod_gt_pack': (I32, [P, P, P, I32, I64, P, P, P, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
     'sbod_dcn_fwd_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),

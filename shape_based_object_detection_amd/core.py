@@ -174,6 +174,26 @@ class GtStaging:
             self._stage_host(boxes, labels, counts)
         return GtPack(self.boxes, self.labels, self.offsets, counts, gmax=self.capacity)
 
+    def stage_and_replay(self, boxes, labels, launches, event=0, event_stream=0, allow_empty=False):
+        """One-call submit of a captured step: ``stage`` of device lists on the first launch's
+        stream, then every (graph exec, stream) of ``launches`` (from ``graph_launches``), then
+        ``event`` (a raw hipEvent_t, 0 for none) recorded on ``event_stream`` — all in C++
+        (_sbodhost.stage_and_replay).  Returns the GtPack, or None when the batch or the build
+        needs the Python path (nothing was launched then)."""
+        ext = L.host_ext
+        if (ext is None or type(boxes) is not list or type(labels) is not list or not launches
+                or len(boxes) != self.batch or not boxes[0].is_cuda):
+            return None
+        r = ext.stage_and_replay(boxes, labels, self.boxes.shape[0], self.capacity, self.device.index or 0,
+                                 self.boxes.data_ptr(), self.labels.data_ptr(), self.offsets.data_ptr(),
+                                 launches[0][1], allow_empty, launches, event or None, event_stream or None)
+        if r is None:
+            return None
+        if type(r) is int:
+            raise L.SbodError('stage_and_replay failed (%d): %s'
+                              % (r, L.lib().sbod_last_error().decode(errors='replace')))
+        return GtPack(self.boxes, self.labels, self.offsets, r, gmax=self.capacity)
+
     def _stage_host(self, boxes, labels, counts):
         buf, ev = self._pinned()
         hb, hl, ho = self._views(buf)
@@ -184,6 +204,12 @@ class GtStaging:
         ho.copy_(torch.from_numpy(np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)))
         self._region.copy_(buf, non_blocking=True)
         ev.record(torch.cuda.current_stream(self.device))
+
+
+def graph_launches(pairs):
+    """((graph exec, stream) raw handles) for ``GtStaging.stage_and_replay`` from
+    ((torch.cuda.CUDAGraph, torch.cuda.Stream), ...), computed once per captured step."""
+    return tuple((int(g.raw_cuda_graph_exec()), int(st.cuda_stream)) for g, st in pairs)
 
 
 _WS = {}
@@ -431,6 +457,12 @@ class DetectHandle:
         replay (on ``stream``, default the current stream) so ``wait()`` returns this replay's
         detections."""
         self._event.record(stream if stream is not None else torch.cuda.current_stream())
+        self._res = None
+        return self
+
+    def rearmed(self):
+        """As ``replayed`` when the event was already recorded behind the replay elsewhere
+        (``GtStaging.stage_and_replay``)."""
         self._res = None
         return self
 

@@ -246,6 +246,20 @@ int sbod_memcpy_d2h_async(void *dst_host, const void *src_dev, size_t bytes, voi
   return SBOD_OK;
 }
 
+int sbod_graph_launch(void *graph_exec, void *stream) {
+  SBOD_REQUIRE(graph_exec != nullptr, "sbod_graph_launch: null graph");
+  if (hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph_exec), sbod::as_stream(stream)) != hipSuccess)
+    return sbod::launch_status("sbod_graph_launch");
+  return SBOD_OK;
+}
+
+int sbod_event_record(void *event, void *stream) {
+  SBOD_REQUIRE(event != nullptr, "sbod_event_record: null event");
+  if (hipEventRecord(reinterpret_cast<hipEvent_t>(event), sbod::as_stream(stream)) != hipSuccess)
+    return sbod::launch_status("sbod_event_record");
+  return SBOD_OK;
+}
+
 int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, void *stream) {
   SBOD_REQUIRE(n >= 0 && scale != nullptr, "sbod_scale_inplace: bad arguments");
   if (n == 0) return SBOD_OK;

@@ -144,6 +144,58 @@ def test_graph_replay_equals_eager():
         locs.grad, scores.grad = g_gl, g_gs
 
 
+def test_stage_and_replay_equals_eager():
+    """The one-call submit (C++: GT packing, graph launch, detect event) gives the eager results."""
+    B = 8
+    P, crit, locs, scores, det = _setup(B, seed=9)
+    stage = core.GtStaging(B, 16, DEV)
+    side = torch.cuda.Stream()
+
+    def body(gt, capture):
+        loss = crit(locs, scores, gt, None)
+        h = core.detect(locs.detach(), det, 0.01, 0.45, 200, P, async_=True, capture=capture)
+        loss.backward()
+        return loss, h
+
+    gt1 = _gt(B, 11)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            locs.grad = None
+            scores.grad = None
+            _, h = body(stage.stage(*gt1), False)
+            h.wait()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    locs.grad = None
+    scores.grad = None
+    g = torch.cuda.CUDAGraph()
+    pack = stage.stage(*gt1)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=side):
+        g_loss, g_h = body(pack, True)
+    g_gl, g_gs = locs.grad, scores.grad
+    g_h._event.record(side)                             # the raw event exists from here on
+    torch.cuda.synchronize()
+    launches = core.graph_launches([(g, side)])
+    for seed in (12, 13):
+        gt = _gt(B, seed)
+        packed = stage.stage_and_replay(list(gt[0]), list(gt[1]), launches, g_h._event.cuda_event,
+                                        side.cuda_stream)
+        if L.host_ext is None:
+            pytest.skip('host extension not built')
+        assert packed is not None and packed.counts == [b.shape[0] for b in gt[0]]
+        res = g_h.rearmed().wait()
+        torch.cuda.synchronize()
+        gl, gs = g_gl.clone(), g_gs.clone()
+        lv = g_loss.item()
+        e_loss, e_gl, e_gs, e_res = _eager(P, crit, locs, scores, det, gt)
+        assert lv == e_loss
+        assert torch.equal(gl, e_gl) and torch.equal(gs, e_gs)
+        _same_det(res, e_res)
+        locs.grad, scores.grad = g_gl, g_gs
+
+
 def test_workspace_allocation_under_capture_refused():
     """A workspace the captured call would allocate under capture fails loudly instead."""
     B = 2
