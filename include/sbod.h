@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SBOD_ABI_VERSION 2
+#define SBOD_ABI_VERSION 3
 
 typedef enum sbod_status {
   SBOD_OK = 0,
@@ -248,6 +248,9 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
  *   pos_mask: [B,P] uint8 (prior_positives_idx) or NULL.
  *   Outputs: det_boxes [B,top_k,4], det_labels [B,top_k] int64, det_scores [B,top_k],
  *            det_count [B] int32 (rows beyond count are unspecified);
+ *            det_count_host: NULL, or a device-accessible PINNED host buffer [B] int32 (e.g. torch
+ *            pin_memory / hipHostMalloc) that the last kernel also writes det_count into — the
+ *            caller reads it after an event recorded behind the call, with no copy launch;
  *            debug_probs [B,P,C] / debug_boxes [B,P,4] may be NULL.
  *   final_nms < 0 disables the detect_tools final class-agnostic NMS.
  *   window: per-class candidate window (0 = auto: next_pow2(top_k + 1)).  Only the first top_k
@@ -268,8 +271,8 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                     const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
                     float min_score, float max_overlap, int top_k, float final_nms, int window,
                     int flags, float *det_boxes, int64_t *det_labels, float *det_scores,
-                    int32_t *det_count, float *debug_probs, float *debug_boxes, void *workspace,
-                    size_t workspace_bytes, void *stream);
+                    int32_t *det_count, int32_t *det_count_host, float *debug_probs,
+                    float *debug_boxes, void *workspace, size_t workspace_bytes, void *stream);
 
 /* Single-segment greedy NMS (iou_utils.nms / diounms, iou_utils.py:385-530; torchvision.ops.nms).
  *   variant: SBOD_NMS_TV (union (a_i + a_j) - inter, suppress iff IoU > thr),

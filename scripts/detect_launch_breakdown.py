@@ -26,7 +26,7 @@ for it in range(120):
     nb = L.lib().sbod_detect_workspace_bytes(B, P, C); ws = core.workspace(nb, dev, 'detect')
     t.append(time.perf_counter())
     L.call('sbod_detect_f32', L.ptr(locs), L.ptr(det), B, P, C, L.ptr(pri), None, 0, 0, 0.01, 0.45, top_k, -1.0,
-           0, 0, L.ptr(out_b), L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), None, None, L.ptr(ws), nb, L.stream_of(det))
+           0, 0, L.ptr(out_b), L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), None, None, None, L.ptr(ws), nb, L.stream_of(det))
     t.append(time.perf_counter())
     ch, ev = core._count_slot(dev, B)
     ch.copy_(cnt, non_blocking=True); ev.record()

@@ -86,7 +86,7 @@ def main():
 
     def det_kernels():
         L.call('sbod_detect_f32', L.ptr(locs), L.ptr(det), B, P, 21, L.ptr(pri), None, 0, 0, 0.01, 0.45,
-               top_k, -1.0, 0, 0, L.ptr(ob), L.ptr(ol), L.ptr(os_), L.ptr(cnt), None, None, L.ptr(ws), nb, stream)
+               top_k, -1.0, 0, 0, L.ptr(ob), L.ptr(ol), L.ptr(os_), L.ptr(cnt), None, None, None, L.ptr(ws), nb, stream)
     out['detect_kernels_only'] = timeit(det_kernels, a.iters)
     out['detect_api'] = timeit(lambda: core.detect(locs, det, 0.01, 0.45, top_k, pri), a.iters)
     print(json.dumps({k: {'gpu_us': round(v[0], 2), 'wall_us': round(v[1], 2)} for k, v in out.items()}))

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Where the graph-mode bench step's time goes (diagnostic): wall time per step of N back-to-back
+submits of (a) the criterion graph alone, (b) the detect graph alone, (c) both (one C++ submit,
+no host wait), (d) the bench's pipelined step (submit + collect of the previous detections), and
+the host cost of one C++ submit.  GPU-bound modes show the device time of their graphs; (c) vs
+max(a, b) shows how well the two streams overlap."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from shape_based_object_detection_amd import _lib as L  # noqa: E402
+
+N = 200
+dev = torch.device('cuda', 0)
+torch.cuda.set_device(dev)
+L.lib()
+st = bench.Step(dev, 32, 0, 1, graph=True, two_streams=True)
+st.cap_stream.wait_stream(torch.cuda.current_stream())
+st.det_stream.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(st.cap_stream):
+    for _ in range(3):
+        st.eager_split()
+torch.cuda.synchronize()
+st.capture()
+for _ in range(5):
+    st()
+torch.cuda.synchronize()
+
+
+def wall(fn, n=N):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) / n * 1e6, 2)
+
+
+ga, gb, _, h = st.slots[0]
+launches, ev, ev_stream = st.fast[0]
+out = {}
+with torch.cuda.stream(st.cap_stream):
+    out['criterion_graph_only'] = wall(ga.replay)
+with torch.cuda.stream(st.det_stream):
+    out['detect_graph_only'] = wall(gb.replay)
+out['both_one_submit_no_wait'] = wall(lambda: st.stage.stage_and_replay(st.boxes, st.labels, launches, ev, ev_stream))
+out['pipelined_step'] = wall(st.pipelined)
+st.drain()
+torch.cuda.synchronize()
+# host cost of one submit while the GPU is idle
+tt = []
+for _ in range(50):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st.stage.stage_and_replay(st.boxes, st.labels, launches, ev, ev_stream)
+    tt.append(time.perf_counter() - t0)
+tt.sort()
+out['submit_host_us_median'] = round(tt[len(tt) // 2] * 1e6, 2)
+for name, g, s in (('criterion', ga, st.cap_stream), ('detect', gb, st.det_stream)):
+    tt = []
+    for _ in range(50):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        L.call('sbod_graph_launch', g.raw_cuda_graph_exec(), s.cuda_stream)
+        tt.append(time.perf_counter() - t0)
+    tt.sort()
+    out['graph_launch_host_us_%s' % name] = round(tt[len(tt) // 2] * 1e6, 2)
+torch.cuda.synchronize()
+print(json.dumps(out), flush=True)

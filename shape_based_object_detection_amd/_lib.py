@@ -46,7 +46,7 @@ SIGNATURES = {
     'sbod_detect_workspace_bytes': (SZ, [I32, I32, I32]),
     'sbod_detect_counter_bytes': (SZ, [I32, I32]),
     'sbod_detect_f32': (I32, [P, P, I32, I32, I32, P, P, I32, I32, F32, F32, I32, F32, I32, I32, P, P,
-                              P, P, P, P, P, SZ, P]),
+                              P, P, P, P, P, P, SZ, P]),
     'sbod_nms_workspace_bytes': (SZ, [I64]),
     'sbod_nms_f32': (I32, [P, P, I64, F32, I32, I32, F32, P, P, P, SZ, P]),
     'sbod_map_workspace_bytes': (SZ, [I64, I64]),

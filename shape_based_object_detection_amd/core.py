@@ -540,14 +540,14 @@ def reserve_count_slots(dev, B, n):
 
 
 def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn, out,
-                   dbg, ws, nb, window):
+                   dbg, ws, nb, cnt_host, window):
     out_b, out_l, out_s, cnt = out
     need = L.lib().sbod_detect_counter_bytes(B, C)
     flags = _zeroed_flag(ws, need, L.DETECT_COUNTERS_ZEROED, 'detect')
     L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
            L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(window), flags,
-           L.ptr(out_b), L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(dbg[0]), L.ptr(dbg[1]),
-           L.ptr(ws), nb, L.stream_of(sc))
+           L.ptr(out_b), L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(cnt_host), L.ptr(dbg[0]),
+           L.ptr(dbg[1]), L.ptr(ws), nb, L.stream_of(sc))
     # only this call's prefix is known clean: a call with a smaller B * C writes other regions
     # over the rest of a larger one's counters
     _CLEAN[ws.data_ptr()] = need
@@ -581,14 +581,11 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     nb = L.lib().sbod_detect_workspace_bytes(B, P, C)
     ws = workspace(nb, dev, 'detect')
     fn = -1.0 if final_nms is None else float(final_nms)
-    launch = (lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn,
-              (out_b, out_l, out_s, cnt), (dbg_p, dbg_b), ws, nb)
-    _detect_launch(*launch, window)
-    # counts -> pinned host memory behind an event, both cached per (device, B): a pinned
-    # allocation per call goes through hipHostMalloc / the host allocator's event bookkeeping and
-    # stalls the launching thread for the whole queue
+    # counts -> pinned host memory (written by the last detect kernel itself) behind an event,
+    # both cached per (device, B): a pinned allocation per call goes through hipHostMalloc / the
+    # host allocator's event bookkeeping and stalls the launching thread for the whole queue
     if capture:
-        # owned by the graph from now on (its memcpy node writes this buffer on every replay);
+        # owned by the graph from now on (its last kernel writes this buffer on every replay);
         # pinned memory cannot be allocated under capture, so it comes from the pool an eager
         # warm-up call filled
         free = _COUNT_SLOTS.get((dev, B))
@@ -598,8 +595,9 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
         cnt_host, ev = free.pop()
     else:
         cnt_host, ev = _count_slot(dev, B)
-    stream = L.stream_of(cnt)
-    L.call('sbod_memcpy_d2h_async', cnt_host.data_ptr(), L.ptr(cnt), 4 * B, stream)
+    launch = (lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn,
+              (out_b, out_l, out_s, cnt), (dbg_p, dbg_b), ws, nb, cnt_host)
+    _detect_launch(*launch, window)
     if not capture:
         ev.record(torch.cuda.current_stream(dev))
     # the per-image views for the usual all-full case are built while the kernels run

@@ -1853,16 +1853,18 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     const float *__restrict__ boxes_ws, int P, int C, int window, int wfirst, int top_k, float final_nms,
     int general, int pass, int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
-    int32_t *__restrict__ out_count, const unsigned long long *cand, uint32_t *cand_count, float thr,
-    SegOut so) {
+    int32_t *__restrict__ out_count, int32_t *out_count_host, const unsigned long long *cand,
+    uint32_t *cand_count, float thr, SegOut so) {
   extern __shared__ unsigned char s_raw[];
   STAMP_BEGIN();
   const int b = blockIdx.x;
   // the last reader of this image's candidate counters leaves them at zero for the next call
-  // (no memset node in front of a captured detect)
+  // (no memset node in front of a captured detect); the image's count also goes straight to the
+  // caller's pinned host buffer (thread 0 wrote out_count[b] itself: no copy launch)
   auto clear_counters = [&]() {
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += blockDim.x) cand_count[static_cast<int64_t>(b) * C + c] = 0u;
+    if (out_count_host != nullptr && threadIdx.x == 0) out_count_host[b] = out_count[b];
   };
   const int st = merge_body(kept, kc, lastkey, boxes_ws, P, C, window, wfirst, top_k, final_nms, general, pass, need,
                             scratch, out_boxes, out_labels, out_scores, out_count);
@@ -2000,8 +2002,8 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
                     const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
                     float min_score, float max_overlap, int top_k, float final_nms, int window,
                     int flags, float *det_boxes, int64_t *det_labels, float *det_scores,
-                    int32_t *det_count, float *debug_probs, float *debug_boxes, void *workspace,
-                    size_t workspace_bytes, void *stream) {
+                    int32_t *det_count, int32_t *det_count_host, float *debug_probs,
+                    float *debug_boxes, void *workspace, size_t workspace_bytes, void *stream) {
   SBOD_REQUIRE((flags & ~SBOD_DETECT_COUNTERS_ZEROED) == 0, "sbod_detect_f32: unknown flags 0x%x", flags);
   SBOD_REQUIRE(B > 0 && P > 0 && C >= 2 && C <= 256 && locs && scores && det_boxes && det_labels &&
                    det_scores && det_count && top_k > 0,
@@ -2081,8 +2083,8 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     KernelTimer kt("k_det_merge", s, true);
     tlaunch(kt, k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, ws.kept,
                        ws.kc, ws.lastkey, ws.boxes, P, C, w2, w1, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
-                       ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, ws.cand, ws.count,
-                       max_overlap, so);
+                       ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, det_count_host,
+                       ws.cand, ws.count, max_overlap, so);
   }
   SBOD_LAUNCHED("k_det_merge");
   return SBOD_OK;

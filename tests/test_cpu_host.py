@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert missing == [], missing
     assert set(syms) <= set(L.SIGNATURES), set(syms) - set(L.SIGNATURES)
     assert L.MISSING == []
-    assert lib.sbod_abi_version() == 2
+    assert lib.sbod_abi_version() == 3
     assert b'gfx950' in lib.sbod_version()
 
 
