@@ -221,6 +221,8 @@ class Step:
         self.use_graph = graph
         self.capture_error = None
         self.fast = None
+        # the read-only unit upstream gradient: no ones-fill and no scale launch in the step
+        self.one = core.unit_grad(dev)
 
     def body(self, gt, capture=False):
         """The step's device work, in stream order on the current stream: criterion forward,
@@ -230,7 +232,7 @@ class Step:
         loss = self.crit(self.locs, self.scores, gt, None)
         h = core.detect(self.locs.detach(), self.det_scores, 0.01, 0.45, 200, self.priors,
                         box_type='offset', act='softmax', async_=True, capture=capture)
-        loss.backward()
+        loss.backward(self.one)
         return loss, h
 
     def launch_eager(self):
@@ -254,7 +256,7 @@ class Step:
         with torch.cuda.stream(self.det_stream):
             h = self.detect(False)
         with torch.cuda.stream(self.cap_stream):
-            loss.backward()
+            loss.backward(self.one)
         return loss, h.wait()
 
     def detect(self, capture):
@@ -277,7 +279,7 @@ class Step:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga, stream=self.cap_stream):
                     loss = self.crit(self.locs, self.scores, gt, None)
-                    loss.backward()
+                    loss.backward(self.one)
                 with torch.cuda.graph(gb, stream=self.det_stream):
                     h = self.detect(True)
                 self.slots.append((ga, gb, loss, h))

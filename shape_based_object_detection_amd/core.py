@@ -310,6 +310,24 @@ class CriterionSpec:
         self.alpha, self.gamma = alpha, gamma
 
 
+_UNIT = {}
+
+
+def unit_grad(device):
+    """The read-only upstream gradient 1.0 (a cached 0-d float32 device tensor).  A criterion loss
+    back-propagated with it — ``loss.backward(core.unit_grad(loss.device))`` — skips the
+    upstream-gradient launch entirely (the fused forward already wrote the gradients at scale
+    1), and autograd needs no ones-fill kernel either: two launches fewer per captured train
+    step.  Any other gradient (AMP scaling, a weighted sum of losses) takes the scale launch."""
+    dev = torch.device(device)
+    if dev.type == 'cuda' and dev.index is None:
+        dev = torch.device('cuda', torch.cuda.current_device())
+    t = _UNIT.get(dev)
+    if t is None:
+        t = _UNIT[dev] = torch.ones((), dtype=torch.float32, device=dev)
+    return t
+
+
 class _FusedLoss(torch.autograd.Function):
     """Forward computes the loss AND the gradients w.r.t. locs/scores in one pass (read once,
     write once); backward applies the upstream scalar on the device (no host sync, no pass at
@@ -334,6 +352,9 @@ class _FusedLoss(torch.autograd.Function):
         ctx.grads = None
         if g is None or gl is None:
             return None, None, None, None
+        u = _UNIT.get(g.device)
+        if u is not None and g.data_ptr() == u.data_ptr():   # unit_grad(): nothing to apply
+            return gl, gs, None, None
         if g.dtype != torch.float32 or not g.is_contiguous():
             g = g.detach().to(torch.float32).contiguous()
         L.call('sbod_scale2_inplace', L.ptr(gl), gl.numel(), L.ptr(gs), gs.numel(),

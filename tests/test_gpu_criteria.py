@@ -185,3 +185,31 @@ def test_ssd300_global_mining_sharded_equals_full_batch():
     np.testing.assert_allclose(total, full.item(), rtol=1e-5)
     np.testing.assert_allclose(np.concatenate(gls), lo.grad.cpu().numpy(), rtol=1e-5, atol=1e-9)
     np.testing.assert_allclose(np.concatenate(gss), sc.grad.cpu().numpy(), rtol=1e-5, atol=1e-9)
+
+
+def test_unit_grad_backward():
+    """loss.backward(core.unit_grad(dev)) skips the upstream-gradient launch and gives exactly the
+    gradients of loss.backward(); any other upstream gradient is applied (here 2.0)."""
+    from shape_based_object_detection_amd import core
+    P = torch.from_numpy(prior_table('SSD512'))
+    B, C = 4, 21
+    boxes, labels = synth.make_gt(B, seed=71)
+    locs, scores = synth.make_preds(B, P.shape[0], C, seed=71)
+    cfg = Cfg(reg_weights=1.0, device=DEV, n_classes=C, reg_loss='diou', cls_loss='focal')
+    crit = CR.MultiBoxLoss512(priors_cxcy=P.to(DEV), config=cfg)
+    bx, lb = [b.to(DEV) for b in boxes], [l.to(DEV) for l in labels]
+    grads = []
+    for how in ('plain', 'unit', 'twice'):
+        lo = locs.to(DEV).requires_grad_(True)
+        sc = scores.to(DEV).requires_grad_(True)
+        loss = crit(lo, sc, bx, lb)
+        if how == 'plain':
+            loss.backward()
+        elif how == 'unit':
+            loss.backward(core.unit_grad(DEV))
+        else:
+            (loss * 2.0).backward()
+        grads.append((lo.grad.clone(), sc.grad.clone()))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    assert torch.equal(grads[2][0], grads[0][0] * 2.0) and torch.equal(grads[2][1], grads[0][1] * 2.0)
+    assert float(core.unit_grad(DEV)) == 1.0
