@@ -370,13 +370,10 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
           ppy += dval * (-(1.f + cf.tlx) * v[0] + (1.f - cf.rbx) * v[1] + (1.f + cf.tlx) * v[2] - (1.f - cf.rbx) * v[3]);
         }
       }
-#pragma unroll
-      for (int off = 16; off > 0; off >>= 1) {
-        pm += __shfl_xor(pm, off, 32);
-        ppx += __shfl_xor(ppx, off, 32);
-        ppy += __shfl_xor(ppy, off, 32);
-      }
-      if (l31 == 0 && m < s.M) {
+      pm = half_sum_f32(pm);     // over the 32 channels of this half-wave (DPP, no LDS)
+      ppx = half_sum_f32(ppx);
+      ppy = half_sum_f32(ppy);
+      if (l31 == 31 && m < s.M) {
         atomicAdd(&s_red[0][mm], pm);
         atomicAdd(&s_red[1][mm], ppx);
         atomicAdd(&s_red[2][mm], ppy);

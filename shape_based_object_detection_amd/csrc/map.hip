@@ -241,12 +241,14 @@ struct MapWs {
 
 size_t map_temp_bytes(int64_t D, int64_t T) {
   size_t a = 0, b = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, a, static_cast<unsigned long long *>(nullptr),
+  // size queries only; a failed query makes the workspace requirement unsatisfiable (loud) rather than small
+  const hipError_t ea = hipcub::DeviceRadixSort::SortPairs(nullptr, a, static_cast<unsigned long long *>(nullptr),
                                      static_cast<unsigned long long *>(nullptr), static_cast<int32_t *>(nullptr),
                                      static_cast<int32_t *>(nullptr), static_cast<int>(D > 0 ? D : 1), 0, 64);
-  hipcub::DeviceRadixSort::SortPairs(nullptr, b, static_cast<uint32_t *>(nullptr), static_cast<uint32_t *>(nullptr),
+  const hipError_t eb = hipcub::DeviceRadixSort::SortPairs(nullptr, b, static_cast<uint32_t *>(nullptr), static_cast<uint32_t *>(nullptr),
                                      static_cast<int32_t *>(nullptr), static_cast<int32_t *>(nullptr),
                                      static_cast<int>(T > 0 ? T : 1), 0, 32);
+  if (ea != hipSuccess || eb != hipSuccess) return SIZE_MAX / 2;
   return a > b ? a : b;
 }
 

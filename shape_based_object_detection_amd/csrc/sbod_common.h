@@ -176,6 +176,21 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
 
+// Sum over each 32-lane half of the wave with DPP (no LDS): quad swaps and mirrors give every
+// lane its row-of-16 sum, then row_bcast:15 adds row 0 into row 1 and row 2 into row 3 (rows 0
+// and 2 add 0).  The lower half's total is in lanes 16..31, the upper half's in lanes 48..63.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ float dpp_f32_or0(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), kCtrl, kRowMask, 0xf, false));
+}
+__device__ __forceinline__ float half_sum_f32(float v) {
+  v += dpp_f32_or0<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f32_or0<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f32_or0<0x141, 0xf>(v);   // row_half_mirror
+  v += dpp_f32_or0<0x140, 0xf>(v);   // row_mirror
+  return v + dpp_f32_or0<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+}
+
 __device__ __forceinline__ float wave_sum_f32(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);

@@ -83,6 +83,10 @@ def _oracle_case(B, C, O, H, W, ks, pad, stride, modulation, off_scale, seed):
     (2, 6, 5, 7, 7, 3, 1, 1, True, 8.0),       # offsets far outside: border clamp everywhere
     (1, 64, 96, 13, 11, 3, 1, 1, True, 1.0),   # K, M, O not multiples of the tiles
     (2, 32, 300, 9, 9, 3, 1, 2, True, 1.0),    # O > 256: two output-channel groups
+    (2, 40, 64, 11, 13, 3, 1, 1, True, 1.0),   # C not a multiple of 32 (partial channel tiles)
+    (1, 16, 32, 9, 9, 3, 1, 1, True, 6.0),     # large offsets, stride 1
+    (1, 24, 32, 10, 10, 1, 0, 1, True, 1.0),   # kernel 1
+    (1, 8, 32, 8, 8, 2, 1, 1, False, 1.0),     # even kernel, no modulation
 ])
 def test_against_oracle(B, C, O, H, W, ks, pad, stride, mod, off_scale):
     _oracle_case(B, C, O, H, W, ks, pad, stride, mod, off_scale, seed=B * 1000 + C * 10 + ks)
