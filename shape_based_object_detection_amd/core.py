@@ -715,11 +715,28 @@ def smooth_l1_elementwise(pred, target, beta):
                L.stream_of(p))
         return loss, g
 
-    want = torch.is_grad_enabled() and pred.requires_grad
-    out = _RowOp.apply(p, run, want)
-    if target.requires_grad and torch.is_grad_enabled():
-        raise NotImplementedError('sbod SmoothL1Loss: gradients w.r.t. target are not implemented')
-    return out
+    grad_on = torch.is_grad_enabled()
+    return _SmoothL1.apply(p, t, run, grad_on and pred.requires_grad, grad_on and target.requires_grad)
+
+
+class _SmoothL1(torch.autograd.Function):
+    """Element-wise smooth-L1 of (pred - target): one kernel gives the loss and d/dpred; the
+    target's derivative is its negation (nn.SmoothL1Loss propagates to both inputs)."""
+
+    @staticmethod
+    def forward(ctx, p, t, run, want_p, want_t):
+        val, local = run(want_p or want_t)
+        ctx.want = (want_p, want_t)
+        ctx.save_for_backward(local)
+        return val
+
+    @staticmethod
+    def backward(ctx, g):
+        (local,) = ctx.saved_tensors
+        if local is None:
+            return None, None, None, None, None
+        gl = g * local
+        return (gl if ctx.want[0] else None), (-gl if ctx.want[1] else None), None, None, None
 
 
 def focal_rows(kind, logits, target, alpha_fg, alpha_bg, gamma):

@@ -62,6 +62,12 @@ def test_smooth_l1_and_focals():
     loss.backward()
     np.testing.assert_allclose(loss.item(), d['sl1_w_loss'], rtol=RTOL)
     np.testing.assert_allclose(aa.grad.cpu().numpy(), d['sl1_w_grad'], rtol=1e-5, atol=1e-7)
+    # gradient w.r.t. the target as well (autograd reaches both inputs in the reference): the
+    # loss depends on (pred - target) only, so d/dtarget is exactly -d/dpred
+    aa, bb = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    LS.SmoothL1Loss()(aa, bb).backward()
+    np.testing.assert_allclose(aa.grad.cpu().numpy(), d['sl1_mean_grad'], rtol=1e-5, atol=1e-7)
+    np.testing.assert_array_equal(bb.grad.cpu().numpy(), -aa.grad.cpu().numpy())
     x, y = t(d['logits']), t(d['y'])
 
     class C:
