@@ -13,8 +13,12 @@
 // 32-channel K'-tile into LDS from per-(pixel, kernel point) coefficients computed once
 // (k_dcn_coef), reading x channels-last (xt) so the four corner gathers of a pixel are
 // contiguous channel vectors, and it is shared by every output channel of the tile.
-// dx is accumulated channels-last with float atomics whose 32-lane groups cover 128 contiguous
-// bytes, then transposed back.  Roofline: MFMA-bound (2*M*O*C*N flops forward, 2x backward).
+// dx is a gather, not a scatter: the backward-data kernel writes the dcols rows, and one wave
+// per input pixel sums the rows whose bilinear corners land on it (lists built by a counting sort
+// on integer counters), channels-last, then transposed back.  Roofline: MFMA-bound (2*M*O*C*N
+// flops forward, 2x backward).
+#include <hipcub/hipcub.hpp>
+
 #include "sbod_common.h"
 
 namespace sbod {
@@ -41,7 +45,7 @@ struct DcnShape {
 
 __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__restrict__ offset,
                                                   const float *__restrict__ mlog,
-                                                  Coef *__restrict__ coef) {
+                                                  Coef *__restrict__ coef, uint32_t *__restrict__ tcount) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= static_cast<int64_t>(s.M) * s.N) return;
   const int n = static_cast<int>(t % s.N);
@@ -84,6 +88,12 @@ __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__res
   }
   c.inr = ((px >= 0.f && px <= hx) ? 1 : 0) | ((py >= 0.f && py <= hy) ? 2 : 0);
   coef[t] = c;
+  if (tcount) {   // backward: how many corner samples land on each input pixel (dx gather lists)
+    const int64_t ib = static_cast<int64_t>(b) * s.H * s.W;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (c.idx[q] >= 0) atomicAdd(tcount + ib + c.idx[q], 1u);
+  }
 }
 
 
@@ -246,43 +256,47 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd(DcnShape s, const fl
 }
 
 // ----------------------------------------------------------------------------- backward (data)
-// Block: 64 pixels x 256 channels for ONE kernel point n (blockIdx.z).  dcols[m, c] =
+// Block: 64 pixels x 256 channels for ONE kernel point n (blockIdx.z).  dcols[m, n, c] =
 // sum_o dout[o, m] Wb[n, o, c] on MFMA (dout staged in 32-channel chunks, Wb read straight
-// from L2 with lanes along c), then per element: corner values (channels-last, coalesced), dx
-// atomics (128-B segments), and d_mask / d_p partial sums reduced over c across the 32 lanes
-// of a row and the 4 waves before one write per (pixel, n).
+// from L2 with lanes along c), written as rows of the dcols buffer (128-B segments).  dx is a
+// gather over those rows (k_dcn_dx_gather); the offset / mask gradients need the corner values,
+// which k_dcn_bwd_weight already samples, so they are reduced there.
 constexpr int kBM = 64, kBOC = 32, kBLD = kBM + 2;
 
 __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
-    DcnShape s, const float *__restrict__ xt, const Coef *__restrict__ coef,
-    const float *__restrict__ wb, const float *__restrict__ gout, float *__restrict__ gxt,
-    float *__restrict__ goff, float *__restrict__ gmlog, int atomic_small) {
+    DcnShape s, const float *__restrict__ wb, const float *__restrict__ gout, float *__restrict__ dcols) {
   __shared__ float s_dout[2][kBOC][kBLD];     // A operand [o][m]
-  __shared__ Coef s_cf[kBM];
-  __shared__ float s_red[3][kBM];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
   const int m0 = blockIdx.x * kBM, cgb = blockIdx.y * 256, n = blockIdx.z;
-  const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
-  if (tid < kBM) {
-    const int m = m0 + tid;
-    if (m < s.M) s_cf[tid] = coef[static_cast<int64_t>(m) * s.N + n];
-  }
-  if (tid < 3 * kBM) (&s_red[0][0])[tid] = 0.f;
+  const int HWo = s.Ho * s.Wo;
   const int OT = (s.O + kBOC - 1) / kBOC;
+  // Operand loads are unconditional, through wave-uniform buffer descriptors (32-bit lane offsets):
+  // out-of-range rows read a clamped valid address and are zeroed (dout) or meet a zero dout
+  // (Wb), so no branch makes the compiler wait for the prefetch before the current MFMAs.
+  const int HWo_ = HWo;
+  const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(gout), static_cast<short>(0),
+                                                    static_cast<int>(static_cast<int64_t>(s.M) * s.O * 4), 0x00020000);
+  const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(wb), static_cast<short>(0),
+                                                    static_cast<int>(static_cast<int64_t>(s.N) * s.O * s.C * 4), 0x00020000);
+  int dvoff[8];   // dout element (o = oc * 32 + ol, m) at byte dvoff + oc * 32 * HWo * 4
+  bool dok[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + kDcnThreads * i;
+    const int ol = e >> 6, mm = e & 63, m = min(m0 + mm, s.M - 1);
+    const int b = m / HWo_, pix = m - b * HWo_;
+    dok[i] = m0 + mm < s.M;
+    dvoff[i] = ((b * s.O + ol) * HWo_ + pix) * 4;
+  }
   float dstage[8];
   float bcur[2][16], bnext[2][16];
   auto load_dout = [&](int oc) {
+    const int so = oc * kBOC * HWo_ * 4;   // wave-uniform: rows o >= O read finite data or 0 (range check)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int e = tid + kDcnThreads * i;
-      const int ol = e >> 6, mm = e & 63;
-      const int o = oc * kBOC + ol, m = m0 + mm;
-      float v = 0.f;
-      if (o < s.O && m < s.M) {
-        const int b = m / HWo, pix = m - b * HWo;
-        v = gout[(static_cast<int64_t>(b) * s.O + o) * HWo + pix];
-      }
-      dstage[i] = v;
+      const bool o_ok = oc * kBOC + ((tid + kDcnThreads * i) >> 6) < s.O;
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, dvoff[i], so, 0));
+      dstage[i] = (dok[i] && o_ok) ? v : 0.f;
     }
   };
   auto store_dout = [&](int buf) {
@@ -292,15 +306,19 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
       s_dout[buf][e >> 6][e & 63] = dstage[i];
     }
   };
+  int bvoff[2];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+    bvoff[ci] = ((16 * h) * s.C + min(cgb + 64 * wv + 32 * ci + l31, s.C - 1)) * 4;
   auto load_b = [&](int oc, float (&bb)[2][16]) {
 #pragma unroll
-    for (int ci = 0; ci < 2; ++ci) {
-      const int c = cgb + 64 * wv + 32 * ci + l31;
+    for (int st = 0; st < 16; ++st) {
+      // wave-uniform scalar offset; rows o >= O (their dout is zero) read the next kernel point's
+      // weights or 0 past the end (the descriptor's range check)
+      const int so = (n * s.O + oc * kBOC + st) * s.C * 4;
 #pragma unroll
-      for (int st = 0; st < 16; ++st) {
-        const int o = oc * kBOC + 16 * h + st;
-        bb[ci][st] = (o < s.O && c < s.C) ? wb[(static_cast<int64_t>(n) * s.O + o) * s.C + c] : 0.f;
-      }
+      for (int ci = 0; ci < 2; ++ci)
+        bb[ci][st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, bvoff[ci], so, 0));
     }
   };
   f32x16 acc[2][2];
@@ -314,92 +332,119 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
   store_dout(0);
   load_b(0, bcur);
   __syncthreads();
+  float a0[16], a1[16];
   for (int oc = 0; oc < OT; ++oc) {
     const int buf = oc & 1;
     const bool more = oc + 1 < OT;
-    if (more) {
-      load_dout(oc + 1);
-      load_b(oc + 1, bnext);
-    }
+    const int ocn = more ? oc + 1 : oc;
+    load_dout(ocn);
+    load_b(ocn, bnext);
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
-      const float a0 = s_dout[buf][16 * h + st][l31];
-      const float a1 = s_dout[buf][16 * h + st][32 + l31];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bcur[0][st], acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bcur[1][st], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bcur[0][st], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bcur[1][st], acc[1][1], 0, 0, 0);
+      a0[st] = s_dout[buf][16 * h + st][l31];
+      a1[st] = s_dout[buf][16 * h + st][32 + l31];
     }
-    if (more) {
-      store_dout(buf ^ 1);
+    __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
 #pragma unroll
-      for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-        for (int st = 0; st < 16; ++st) bcur[ci][st] = bnext[ci][st];
+    for (int st = 0; st < 16; ++st) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[st], bcur[0][st], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[st], bcur[1][st], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[st], bcur[0][st], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[st], bcur[1][st], acc[1][1], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) store_dout(buf ^ 1);
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) bcur[ci][st] = bnext[ci][st];
     __syncthreads();
   }
   // epilogue: row m = 32 ri + (r&3) + 8 (r>>2) + 4 h, column c = cgb + 64 wv + 32 ci + l31
 #pragma unroll
-  for (int ri = 0; ri < 2; ++ri) {
-#pragma unroll 2
+  for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int mm = 32 * ri + (r & 3) + 8 * (r >> 2) + 4 * h, m = m0 + mm;
-      float pm = 0.f, ppx = 0.f, ppy = 0.f;
-      if (m < s.M) {
-        const Coef &cf = s_cf[mm];
-        const int b = m / HWo;
-        const int64_t ib = static_cast<int64_t>(b) * HW;
+      const int m = m0 + 32 * ri + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m >= s.M) continue;
+      float *row = dcols + (static_cast<int64_t>(m) * s.N + n) * s.C;
 #pragma unroll
-        for (int ci = 0; ci < 2; ++ci) {
-          const int c = cgb + 64 * wv + 32 * ci + l31;
-          if (c >= s.C) continue;
-          float v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = cf.idx[q] >= 0 ? xt[(ib + cf.idx[q]) * s.C + c] : 0.f;
-          const float dcol = acc[ri][ci][r];
-          const float raw = ((cf.g[0] * v[0] + cf.g[1] * v[1]) + cf.g[2] * v[2]) + cf.g[3] * v[3];
-          const float dval = dcol * cf.mval;
-          if (gxt) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (cf.idx[q] >= 0) atomicAdd(gxt + (ib + cf.idx[q]) * s.C + c, dval * cf.g[q]);
-          }
-          pm += dcol * raw;
-          ppx += dval * (-(1.f + cf.tly) * v[0] + (1.f - cf.rby) * v[1] - (1.f - cf.rby) * v[2] + (1.f + cf.tly) * v[3]);
-          ppy += dval * (-(1.f + cf.tlx) * v[0] + (1.f - cf.rbx) * v[1] + (1.f + cf.tlx) * v[2] - (1.f - cf.rbx) * v[3]);
-        }
-      }
-      pm = half_sum_f32(pm);     // over the 32 channels of this half-wave (DPP, no LDS)
-      ppx = half_sum_f32(ppx);
-      ppy = half_sum_f32(ppy);
-      if (l31 == 31 && m < s.M) {
-        atomicAdd(&s_red[0][mm], pm);
-        atomicAdd(&s_red[1][mm], ppx);
-        atomicAdd(&s_red[2][mm], ppy);
+      for (int ci = 0; ci < 2; ++ci) {
+        const int c = cgb + 64 * wv + 32 * ci + l31;
+        if (c < s.C) row[c] = acc[ri][ci][r];
       }
     }
+}
+
+// ----------------------------------------------------------------------------- backward (dx gather)
+// dx[b, y, x, c] = sum over the samples (pixel m, kernel point n, corner q) whose corner q lands
+// on input pixel (y, x) of  g_q(m, n) * mask(m, n) * dcols[m, n, c].  k_dcn_bwd_data writes the
+// dcols rows; k_dcn_coef counted the samples per input pixel, an exclusive scan gives each pixel
+// its entry range, k_dcn_dx_fill places (row, weight) entries with integer atomics on those
+// counters, and k_dcn_dx_gather (one wave per input pixel) sums its rows in registers and stores
+// dx once: no float atomics (the per-pixel entry order is arbitrary; fp32 sums stay within the
+// tests' tolerance, as with the atomics they replace).
+struct DxEnt {
+  uint32_t row;   // m * N + n
+  float w;        // g_q * mask
+};
+
+__global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__restrict__ coef,
+                                                     const uint32_t *__restrict__ toff,
+                                                     uint32_t *__restrict__ tcount, DxEnt *__restrict__ ent) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<int64_t>(s.M) * s.N) return;
+  const int m = static_cast<int>(t / s.N);
+  const int64_t ib = static_cast<int64_t>(m / (s.Ho * s.Wo)) * s.H * s.W;
+  const Coef cf = coef[t];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (cf.idx[q] < 0) continue;
+    const int64_t tp = ib + cf.idx[q];
+    const uint32_t k = atomicSub(tcount + tp, 1u) - 1u;   // the counters return to zero
+    ent[toff[tp] + k] = DxEnt{static_cast<uint32_t>(t), cf.g[q] * cf.mval};
   }
-  __syncthreads();
-  if (tid < kBM) {
-    const int mm = tid, m = m0 + mm;
-    if (m < s.M) {
-      const Coef &cf = s_cf[mm];
-      const int b = m / HWo, pix = m - b * HWo;
-      const float vx = (cf.inr & 1) ? s_red[1][mm] : 0.f;
-      const float vy = (cf.inr & 2) ? s_red[2][mm] : 0.f;
-      const float vm = s_red[0][mm] * cf.mval * (1.f - cf.mval);
-      float *px = goff ? goff + (static_cast<int64_t>(b) * 2 * s.N + n) * HWo + pix : nullptr;
-      float *py = goff ? goff + (static_cast<int64_t>(b) * 2 * s.N + s.N + n) * HWo + pix : nullptr;
-      float *pmk = gmlog ? gmlog + (static_cast<int64_t>(b) * s.N + n) * HWo + pix : nullptr;
-      if (atomic_small) {
-        if (px) { atomicAdd(px, vx); atomicAdd(py, vy); }
-        if (pmk) atomicAdd(pmk, vm);
-      } else {
-        if (px) { *px = vx; *py = vy; }
-        if (pmk) *pmk = vm;
+}
+
+// One wave per input pixel; lanes hold 4 consecutive channels (C % 4 == 0) or 1.
+template <int VEC>
+__global__ __launch_bounds__(256) void k_dcn_dx_gather(int C, int ntarget, const uint32_t *__restrict__ toff,
+                                                       const DxEnt *__restrict__ ent,
+                                                       const float *__restrict__ dcols, float *__restrict__ gxt) {
+  const int lane = threadIdx.x & 63;
+  const int tp = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (tp >= ntarget) return;
+  const uint32_t e0 = __builtin_amdgcn_readfirstlane(toff[tp]), e1 = __builtin_amdgcn_readfirstlane(toff[tp + 1]);
+  for (int c0 = VEC * lane; c0 < C; c0 += 64 * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+    uint32_t e = e0;
+    for (; e + 4 <= e1; e += 4) {   // four rows in flight
+      DxEnt d[4];
+      float x[4][VEC];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        d[u] = ent[e + u];
+        load_vec<VEC>(dcols + static_cast<int64_t>(d[u].row) * C + c0, true, x[u]);
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] += d[u].w * x[u][v];
     }
+    for (; e < e1; ++e) {
+      const DxEnt d = ent[e];
+      float x[VEC];
+      load_vec<VEC>(dcols + static_cast<int64_t>(d.row) * C + c0, true, x);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] += d.w * x[v];
+    }
+    float *dst = gxt + static_cast<int64_t>(tp) * C + c0;
+    if (VEC == 4)
+      *reinterpret_cast<float4 *>(dst) = make_float4(acc[0], acc[1], acc[VEC > 2 ? 2 : 0], acc[VEC > 3 ? 3 : 0]);
+    else
+      dst[0] = acc[0];
   }
 }
 
@@ -409,12 +454,18 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
 // the forward kernel: dout rows go straight from HBM into the MFMA A registers (float4 when a
 // 32-pixel chunk never straddles two images), the columns are re-sampled channels-last into
 // double-buffered LDS, and the next chunk's gathers are in flight during the current MFMAs.
+// The same corner samples give the offset / mask gradients (Deformable_convolution.py:59-91 by
+// autograd): with dcols from k_dcn_bwd_data, each pixel's partial sums over this block's 64
+// channels, pm = sum dcol * raw and d/dp = sum dcol * mask * (corner-difference terms), are
+// reduced over the 8 lanes holding the pixel (DPP) and added to d_offset / d_mask (C / 64
+// partials per (pixel, kernel point); output-channel block 0 only).
 constexpr int kWC = 64, kWMs = 32, kWLD = kWC + 2;
 
 template <int VEC, bool AVEC>
 __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
     DcnShape s, const float *__restrict__ xt, const Coef *__restrict__ coef,
-    const float *__restrict__ gout, float *__restrict__ gwp, int m_slice) {
+    const float *__restrict__ gout, float *__restrict__ gwp, int m_slice,
+    const float *__restrict__ dcols, float *__restrict__ goff, float *__restrict__ gmlog) {
   __shared__ float s_cols[2][kWMs][kWLD];      // B operand [m][c]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
   const int CTw = (s.C + kWC - 1) / kWC;
@@ -423,8 +474,12 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
   const int mend = min(ms0 + m_slice, s.M);
   const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
   const int smm = tid >> 3, scg = (tid & 7) * 8;
-  float X[4][8];
+  const bool dofs = dcols != nullptr && blockIdx.z == 0;   // offset / mask gradients here
+  const bool dow = gwp != nullptr;
+  float X[4][8], D[8];
   float cg[4] = {0.f, 0.f, 0.f, 0.f}, cm = 0.f;
+  float ctlx = 0.f, crbx = 0.f, ctly = 0.f, crby = 0.f;
+  int cinr = 0, cmpix = -1;
   float acur[2][16], anext[2][16];
   f32x16 acc[2][2];
 #pragma unroll
@@ -438,11 +493,14 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
     const int m = m0 + smm;
     const bool ok = m < mend;
     int idx[4] = {-1, -1, -1, -1};
+    cmpix = -1;
     if (ok) {
       const Coef cf = coef[static_cast<int64_t>(m) * s.N + n];
 #pragma unroll
       for (int q = 0; q < 4; ++q) { idx[q] = cf.idx[q]; cg[q] = cf.g[q]; }
       cm = cf.mval;
+      ctlx = cf.tlx; crbx = cf.rbx; ctly = cf.tly; crby = cf.rby; cinr = cf.inr;
+      cmpix = m;
     }
     const float *xb = xt + static_cast<int64_t>(ok ? m / HWo : 0) * HW * s.C + c0 + scg;
 #pragma unroll
@@ -450,11 +508,43 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
 #pragma unroll
       for (int v = 0; v < 8; v += VEC)
         load_vec<VEC>(xb + static_cast<int64_t>(idx[q]) * s.C + v, idx[q] >= 0 && c0 + scg + v < s.C, &X[q][v]);
+    if (dofs) {
+      const float *dr = dcols + (static_cast<int64_t>(ok ? m : 0) * s.N + n) * s.C + c0 + scg;
+#pragma unroll
+      for (int v = 0; v < 8; v += VEC) load_vec<VEC>(dr + v, ok && c0 + scg + v < s.C, &D[v]);
+    }
   };
   auto store_cols = [&](int buf) {
+    float pm = 0.f, ppx = 0.f, ppy = 0.f;
 #pragma unroll
-    for (int v = 0; v < 8; ++v)
-      s_cols[buf][smm][scg + v] = combine(cg, cm, X[0][v], X[1][v], X[2][v], X[3][v]);
+    for (int v = 0; v < 8; ++v) {
+      const float raw = ((cg[0] * X[0][v] + cg[1] * X[1][v]) + cg[2] * X[2][v]) + cg[3] * X[3][v];
+      s_cols[buf][smm][scg + v] = raw * cm;   // == combine(): the forward's column value
+      if (dofs) {
+        pm += D[v] * raw;
+        ppx += D[v] * (-(1.f + ctly) * X[0][v] + (1.f - crby) * X[1][v] - (1.f - crby) * X[2][v] + (1.f + ctly) * X[3][v]);
+        ppy += D[v] * (-(1.f + ctlx) * X[0][v] + (1.f - crbx) * X[1][v] + (1.f + ctlx) * X[2][v] - (1.f - crbx) * X[3][v]);
+      }
+    }
+    if (dofs) {   // the 8 lanes of this pixel are lanes 8k..8k+7: quad swaps + half-row mirror
+      pm += dpp_f32_or0<0xB1, 0xf>(pm);
+      ppx += dpp_f32_or0<0xB1, 0xf>(ppx);
+      ppy += dpp_f32_or0<0xB1, 0xf>(ppy);
+      pm += dpp_f32_or0<0x4E, 0xf>(pm);
+      ppx += dpp_f32_or0<0x4E, 0xf>(ppx);
+      ppy += dpp_f32_or0<0x4E, 0xf>(ppy);
+      pm += dpp_f32_or0<0x141, 0xf>(pm);
+      ppx += dpp_f32_or0<0x141, 0xf>(ppx);
+      ppy += dpp_f32_or0<0x141, 0xf>(ppy);
+      if ((tid & 7) == 0 && cmpix >= 0) {
+        const int b = cmpix / HWo, pix = cmpix - b * HWo;
+        if (goff) {
+          atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + n) * HWo + pix, (cinr & 1) ? ppx * cm : 0.f);
+          atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + s.N + n) * HWo + pix, (cinr & 2) ? ppy * cm : 0.f);
+        }
+        if (gmlog) atomicAdd(gmlog + (static_cast<int64_t>(b) * s.N + n) * HWo + pix, pm * cm * (1.f - cm));
+      }
+    }
   };
   auto load_a = [&](int m0, float (&a)[2][16]) {
     const int mb = m0 + 16 * h;
@@ -513,6 +603,7 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
     }
     __syncthreads();
   }
+  if (!dow) return;   // (offset / mask gradients only: the MFMA result is not wanted)
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -543,7 +634,22 @@ DcnShape make_shape(int B, int C, int H, int W, int O, int k, int stride, int pa
 struct DcnWs {
   Coef *coef;
   float *xt, *gxt, *wt, *gwp;
+  // backward dx gather: dcols rows [M][N][C], per-input-pixel counters / entry offsets, entries
+  float *dcols;
+  uint32_t *tcount, *toff;
+  DxEnt *ent;
+  void *scan_tmp;
+  size_t scan_bytes;
 };
+
+size_t dcn_scan_bytes(int64_t n) {
+  size_t b = 0;
+  // size query only; a failed query makes the workspace requirement unsatisfiable (loud)
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<uint32_t *>(nullptr), static_cast<uint32_t *>(nullptr),
+                                       static_cast<int>(n)) != hipSuccess)
+    return SIZE_MAX / 4;
+  return b;
+}
 
 size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w) {
   char *p = static_cast<char *>(base);
@@ -551,12 +657,20 @@ size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w) {
   auto take = [&](size_t bytes) { char *r = p ? p + off : nullptr; off += align_up(bytes); return r; };
   const size_t xbytes = static_cast<size_t>(s.B) * s.C * s.H * s.W * 4;
   const size_t wbytes = static_cast<size_t>(s.O) * s.K * 4;
+  const size_t rows = static_cast<size_t>(s.M) * s.N;
+  const size_t npix = static_cast<size_t>(s.B) * s.H * s.W;
   DcnWs t;
-  t.coef = reinterpret_cast<Coef *>(take(static_cast<size_t>(s.M) * s.N * sizeof(Coef)));
+  t.coef = reinterpret_cast<Coef *>(take(rows * sizeof(Coef)));
   t.xt = reinterpret_cast<float *>(take(xbytes));
   t.gxt = reinterpret_cast<float *>(take(xbytes));
   t.wt = reinterpret_cast<float *>(take(wbytes));
   t.gwp = reinterpret_cast<float *>(take(wbytes));
+  t.dcols = reinterpret_cast<float *>(take(rows * s.C * 4));
+  t.tcount = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
+  t.toff = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
+  t.ent = reinterpret_cast<DxEnt *>(take(rows * 4 * sizeof(DxEnt)));
+  t.scan_bytes = dcn_scan_bytes(static_cast<int64_t>(npix) + 1);
+  t.scan_tmp = take(t.scan_bytes);
   if (w) *w = t;
   return off;
 }
@@ -587,7 +701,8 @@ static int dcn_check(const DcnShape &s, const float *x, const float *offset, con
 }
 
 static int dcn_prepare(const DcnShape &s, const float *x, const float *offset, const float *mask_logits,
-                       void *workspace, size_t workspace_bytes, DcnWs *w, hipStream_t hs, const char *who) {
+                       void *workspace, size_t workspace_bytes, DcnWs *w, hipStream_t hs, const char *who,
+                       bool count_targets) {
   const size_t need = dcn_carve(s, nullptr, nullptr);
   if (workspace == nullptr || workspace_bytes < need) {
     set_error("%s: workspace %zu < %zu", who, workspace_bytes, need);
@@ -595,7 +710,11 @@ static int dcn_prepare(const DcnShape &s, const float *x, const float *offset, c
   }
   dcn_carve(s, workspace, w);
   const int64_t nc = static_cast<int64_t>(s.M) * s.N;
-  hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, w->coef);
+  if (count_targets &&
+      hipMemsetAsync(w->tcount, 0, (static_cast<size_t>(s.B) * s.H * s.W + 1) * 4, hs) != hipSuccess)
+    return launch_status("hipMemsetAsync(dcn dx counters)");
+  hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, w->coef,
+                     count_targets ? w->tcount : nullptr);
   SBOD_LAUNCHED("k_dcn_coef");
   launch_transpose(x, w->xt, s.B, s.C, s.H * s.W, hs);   // x [B][C][HW] -> xt [B][HW][C]
   SBOD_LAUNCHED("k_transpose(x)");
@@ -611,7 +730,7 @@ int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logi
   SBOD_REQUIRE(out != nullptr, "sbod_dcn_fwd_f32: out is NULL");
   hipStream_t hs = as_stream(stream);
   DcnWs w;
-  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_fwd_f32");
+  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_fwd_f32", false);
   if (st != SBOD_OK) return st;
   launch_transpose(weight, w.wt, s.O, s.C, s.N, hs);   // W [O][C][N] -> Wf [O][N][C]
   SBOD_LAUNCHED("k_transpose(w)");
@@ -642,36 +761,57 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
   SBOD_REQUIRE(grad_out != nullptr, "sbod_dcn_bwd_f32: grad_out is NULL");
   hipStream_t hs = as_stream(stream);
   DcnWs w;
-  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_bwd_f32");
+  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_bwd_f32",
+                   grad_x != nullptr);
   if (st != SBOD_OK) return st;
   if (!mask_logits) grad_mask_logits = nullptr;
-  const size_t xbytes = static_cast<size_t>(B) * C * H * W * 4;
-  if (grad_x || grad_offset || grad_mask_logits) {
+  const int npix = B * H * W;
+  const bool need_cols = grad_x || grad_offset || grad_mask_logits;
+  SBOD_REQUIRE(!need_cols || (static_cast<int64_t>(s.M) * s.O * 4 < (1ll << 31) &&
+                              static_cast<int64_t>(s.N) * s.O * s.C * 4 < (1ll << 31)),
+               "sbod_dcn_bwd_f32: grad_out / weight exceed the 2 GiB buffer-descriptor range");
+  if (grad_x) {   // the input pixels' entry ranges (scan of the counts k_dcn_coef made)
+    size_t tb = w.scan_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tb, w.tcount, w.toff, npix + 1, hs) != hipSuccess)
+      return launch_status("DeviceScan(dcn dx offsets)");
+    const int64_t nc = static_cast<int64_t>(s.M) * s.N;
+    hipLaunchKernelGGL(k_dcn_dx_fill, dim3((nc + 255) / 256), dim3(256), 0, hs, s, w.coef, w.toff, w.tcount, w.ent);
+    SBOD_LAUNCHED("k_dcn_dx_fill");
+  }
+  if (need_cols) {
     launch_transpose(weight, w.wt, 1, s.O * s.C, s.N, hs);   // W [O*C][N] -> Wb [N][O][C]
     SBOD_LAUNCHED("k_transpose(wb)");
-    if (grad_x && hipMemsetAsync(w.gxt, 0, xbytes, hs) != hipSuccess) return launch_status("hipMemsetAsync(dcn dx)");
-    const int cgs = (s.C + 255) / 256;
-    const size_t ob = static_cast<size_t>(s.M) * s.N * 4;
-    if (cgs > 1) {
-      if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob, hs) != hipSuccess) return launch_status("memset");
-      if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob, hs) != hipSuccess) return launch_status("memset");
-    }
     {
       KernelTimer kt("k_dcn_bwd_data", hs);
-      hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, cgs, s.N), dim3(kDcnThreads), 0, hs, s,
-                         w.xt, w.coef, w.wt, grad_out, grad_x ? w.gxt : nullptr, grad_offset, grad_mask_logits,
-                         cgs > 1 ? 1 : 0);
+      hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
+                         hs, s, w.wt, grad_out, w.dcols);
     }
     SBOD_LAUNCHED("k_dcn_bwd_data");
-    if (grad_x) {
-      launch_transpose(w.gxt, grad_x, s.B, s.H * s.W, s.C, hs);   // [B][HW][C] -> [B][C][HW]
-      SBOD_LAUNCHED("k_transpose(dx)");
-    }
   }
-  if (grad_weight) {
-    if (hipMemsetAsync(w.gwp, 0, static_cast<size_t>(O) * s.K * 4, hs) != hipSuccess)
+  if (grad_x) {
+    {
+      KernelTimer kt("k_dcn_dx_gather", hs);
+      if (s.C % 4 == 0)
+        hipLaunchKernelGGL(k_dcn_dx_gather<4>, dim3((npix + 3) / 4), dim3(256), 0, hs, s.C, npix, w.toff, w.ent,
+                           w.dcols, w.gxt);
+      else
+        hipLaunchKernelGGL(k_dcn_dx_gather<1>, dim3((npix + 3) / 4), dim3(256), 0, hs, s.C, npix, w.toff, w.ent,
+                           w.dcols, w.gxt);
+    }
+    SBOD_LAUNCHED("k_dcn_dx_gather");
+    launch_transpose(w.gxt, grad_x, s.B, s.H * s.W, s.C, hs);   // [B][HW][C] -> [B][C][HW]
+    SBOD_LAUNCHED("k_transpose(dx)");
+  }
+  const bool need_om = grad_offset || grad_mask_logits;
+  if (grad_weight || need_om) {
+    // weight gradient, and the offset / mask gradients from the same corner samples (C / 64
+    // channel-block partials added into zeroed outputs)
+    const size_t ob = static_cast<size_t>(s.M) * s.N * 4;
+    if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob, hs) != hipSuccess) return launch_status("memset");
+    if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob, hs) != hipSuccess) return launch_status("memset");
+    if (grad_weight && hipMemsetAsync(w.gwp, 0, static_cast<size_t>(O) * s.K * 4, hs) != hipSuccess)
       return launch_status("hipMemsetAsync(dcn dw)");
-    const int gx = s.N * ((s.C + kWC - 1) / kWC), gz = (s.O + 255) / 256;
+    const int gx = s.N * ((s.C + kWC - 1) / kWC), gz = grad_weight ? (s.O + 255) / 256 : 1;
     // one round of resident blocks (256 CUs x 2): a partial second round would double the time
     int slices = std::max(1, 512 / (gx * gz));
     slices = std::max(1, std::min(slices, (s.M + kWMs - 1) / kWMs));
@@ -680,18 +820,25 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
     slices = (s.M + m_slice - 1) / m_slice;
     const dim3 grid(gx, slices, gz);
     const bool avec = (s.Ho * s.Wo) % kWMs == 0;   // 32-pixel chunks never straddle images
+    float *gwp = grad_weight ? w.gwp : nullptr;
+    const float *dc = need_om ? w.dcols : nullptr;
     {
       KernelTimer kt("k_dcn_bwd_weight", hs);
       if (s.C % 4 == 0 && avec)
-        hipLaunchKernelGGL((k_dcn_bwd_weight<4, true>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+        hipLaunchKernelGGL((k_dcn_bwd_weight<4, true>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp,
+                           m_slice, dc, grad_offset, grad_mask_logits);
       else if (s.C % 4 == 0)
-        hipLaunchKernelGGL((k_dcn_bwd_weight<4, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+        hipLaunchKernelGGL((k_dcn_bwd_weight<4, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp,
+                           m_slice, dc, grad_offset, grad_mask_logits);
       else
-        hipLaunchKernelGGL((k_dcn_bwd_weight<1, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, w.gwp, m_slice);
+        hipLaunchKernelGGL((k_dcn_bwd_weight<1, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp,
+                           m_slice, dc, grad_offset, grad_mask_logits);
     }
     SBOD_LAUNCHED("k_dcn_bwd_weight");
-    launch_transpose(w.gwp, grad_weight, s.O, s.N, s.C, hs);   // [O][N][C] -> [O][C][N]
-    SBOD_LAUNCHED("k_transpose(dw)");
+    if (grad_weight) {
+      launch_transpose(w.gwp, grad_weight, s.O, s.N, s.C, hs);   // [O][N][C] -> [O][C][N]
+      SBOD_LAUNCHED("k_transpose(dw)");
+    }
   }
   return SBOD_OK;
 }
