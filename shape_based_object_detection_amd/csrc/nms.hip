@@ -700,7 +700,7 @@ __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
     const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
     const int32_t *__restrict__ need) {
-  extern __shared__ unsigned char s_raw[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   __shared__ uint32_t s_hist[2048];
   __shared__ unsigned long long s_st[2];
   __shared__ unsigned long long s_flag[16];
@@ -762,7 +762,7 @@ __device__ unsigned long long radix_select_below(const unsigned long long *g, in
 __global__ __launch_bounds__(kAllThreads) void k_det_segment_all(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
     const float *__restrict__ boxes_ws, int P, int C, int stride, int top_k, float thr, SegOut o) {
-  extern __shared__ unsigned char s_raw[];   // kept so far: keys [stride] | boxes [stride] | areas [stride]
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];   // kept so far: keys [stride] | boxes [stride] | areas [stride]
   __shared__ unsigned long long s_key[kAllChunk];
   __shared__ Box4 s_box[kAllChunk];
   __shared__ float s_area[kAllChunk];
@@ -1386,13 +1386,13 @@ __device__ __forceinline__ int merge_rank(
     const float *__restrict__ boxes_ws, int P, int C, int stride, int wmax, int top_k, int pass,
     int32_t *__restrict__ need, float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
     float *__restrict__ out_scores, int32_t *__restrict__ out_count) {
-  extern __shared__ unsigned char s_raw[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   __shared__ uint32_t r_off[kRankC + 1], r_kc[kRankC];
   __shared__ unsigned long long r_L;
   __shared__ uint32_t r_trunc, r_kth;
   __shared__ int r_m, r_total, r_any;
   const int nslot = (C - 1) * wmax;   // kc <= wmax entries per class (stored at `stride`)
-  if (C > kRankC || static_cast<size_t>(nslot) * 20 > static_cast<size_t>(kRankLds)) return -1;
+  if (C > kRankC || static_cast<size_t>(nslot) * 20 > static_cast<size_t>(kRankLds) || (nslot & 1)) return -1;
   const int b = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
   const int64_t sb0 = static_cast<int64_t>(b) * C;
 #ifdef SBOD_PHASE_CLOCKS
@@ -1539,12 +1539,16 @@ __device__ __forceinline__ int merge_rank(
     const unsigned long long ke = sk[e];
     uint32_t cnt = 0;
     int j = j0;
-    for (; j + 8 <= j1; j += 8) {   // eight independent (broadcast) LDS reads in flight
-      unsigned long long v[8];
+    if ((j & 1) && j < j1) cnt += sk[j++] > ke ? 1u : 0u;
+    // 16-byte broadcast reads (ds_read_b128: 4 LDS cycles per 2 keys, half of ds_read2_b64's),
+    // four in flight; sk is 16-byte aligned (nslot even, see the carve above)
+    const ulonglong2 *sk2 = reinterpret_cast<const ulonglong2 *>(sk);
+    for (; j + 8 <= j1; j += 8) {
+      ulonglong2 v[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = sk[j + u];
+      for (int u = 0; u < 4; ++u) v[u] = sk2[(j >> 1) + u];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) cnt += v[u] > ke ? 1u : 0u;
+      for (int u = 0; u < 4; ++u) cnt += (v[u].x > ke ? 1u : 0u) + (v[u].y > ke ? 1u : 0u);
     }
     for (; j < j1; ++j) cnt += sk[j] > ke ? 1u : 0u;
     if (cnt) atomicAdd(&rk[e], cnt);
@@ -1584,7 +1588,7 @@ __device__ __forceinline__ int merge_body(
     int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
     float *__restrict__ out_scores, int32_t *__restrict__ out_count) {
-  extern __shared__ unsigned char s_raw[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   __shared__ uint32_t s_off[257], s_zoff[257];
   __shared__ uint32_t s_hist[2048];
   __shared__ int s_misc[4];
@@ -1855,7 +1859,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
     int32_t *__restrict__ out_count, int32_t *out_count_host, const unsigned long long *cand,
     uint32_t *cand_count, float thr, SegOut so) {
-  extern __shared__ unsigned char s_raw[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   STAMP_BEGIN();
   const int b = blockIdx.x;
   // the last reader of this image's candidate counters leaves them at zero for the next call
@@ -1900,7 +1904,7 @@ __global__ __launch_bounds__(1024) void k_nms_single(const float *__restrict__ b
                                                      unsigned long long *__restrict__ gkeys,
                                                      int64_t *__restrict__ keep,
                                                      int32_t *__restrict__ count) {
-  extern __shared__ unsigned char s_raw[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   __shared__ uint32_t s_hist[256];
   __shared__ unsigned long long s_st[2];
   __shared__ unsigned long long s_flag[16];
