@@ -516,11 +516,14 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     // them).  Each lane then walks only ITS candidate classes (~1-2 of 20) to emit keys.
     // the raw row stays in LDS: an emitted candidate's probability is recomputed from it with
     // the same operations (bit-identical), so the 20 probabilities are never written back
+    // constant-offset reads (one address, no per-slot index arithmetic): a short last row reads
+    // at most CM - C <= 7 floats past the tile, into the ballot area that follows it in LDS;
+    // only the top 8 slots can be padding (the dispatcher picks CM with C > CM - 8)
     float r[CM];
 #pragma unroll
     for (int k = 0; k < CM; ++k) {
-      const float v = row[k < C ? k : C - 1];   // unconditional reads (no per-slot branches)
-      r[k] = k < C ? v : -__builtin_inff();
+      const float v = row[k];
+      r[k] = (k < CM - 8 || k < C) ? v : -__builtin_inff();
     }
     const bool softmax = a.act == SBOD_ACT_SOFTMAX;
     float m = 0.f, rs = 1.f;
