@@ -436,12 +436,15 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     if constexpr (CM > 0) {
       float r[CM];
       float m = -__builtin_inff(), zmin = __builtin_inff();
+      // constant-offset reads (no per-slot index arithmetic; a short last row reads into the 8
+      // padding floats after the tile); only the top 8 slots can be padding (C > CM - 8)
+      auto in_row = [&](int k) { return k < CM - 8 || k < C; };
 #pragma unroll
       for (int k = 0; k < CM; ++k) {
-        const float x = row[k < C ? k : C - 1];   // unconditional reads (no per-slot branches)
-        r[k] = k < C ? x : -__builtin_inff();
+        const float x = row[k];
+        r[k] = in_row(k) ? x : -__builtin_inff();
         m = fmaxf(m, r[k]);                       // a NaN logit gives a NaN loss either way
-        zmin = (k < C && r[k] < zmin) ? r[k] : zmin;
+        zmin = (in_row(k) && r[k] < zmin) ? r[k] : zmin;
       }
       const float zt = row[c];
       // the exponentials are summed here and recomputed (bit-identically) from the LDS row in
@@ -480,12 +483,12 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
             const float kq = dq * q * scale;
 #pragma unroll
             for (int k = 0; k < CM; ++k)
-              if (k < C) row[k] = loss != loss ? loss : kq * ((k == c ? 1.f : 0.f) - fast_exp(row[k] - m) * inv);
+              if (in_row(k)) row[k] = loss != loss ? loss : kq * ((k == c ? 1.f : 0.f) - fast_exp(row[k] - m) * inv);
           }
         } else if (grad) {
 #pragma unroll
           for (int k = 0; k < CM; ++k)
-            if (k < C) row[k] = 0.f;
+            if (in_row(k)) row[k] = 0.f;
         }
       } else {
         const float ce = -((zt - m) - logf(s));  // cross_entropy = -log_softmax[t]
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
             const float sc = 1.f / n;
 #pragma unroll
             for (int k = 0; k < CM; ++k)
-              if (k < C) row[k] = (expf(row[k] - m) * inv - (k == c ? 1.f : 0.f)) * sc;
+              if (in_row(k)) row[k] = (expf(row[k] - m) * inv - (k == c ? 1.f : 0.f)) * sc;
           }
         } else {
           bool member;
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
           if (grad) {
 #pragma unroll
             for (int k = 0; k < CM; ++k)
-              if (k < C) row[k] = 0.f;
+              if (in_row(k)) row[k] = 0.f;
           }
         }
       }
@@ -924,7 +927,8 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
              npos_total, ovl, threshold, neg_threshold, theta, reg, cls, flags, reg_weight,
              focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool, nullptr};
   dim3 grid((P + kLTile - 1) / kLTile, B);
-  const size_t lds = static_cast<size_t>(kLTile) * C * sizeof(float);
+  // + 8 floats: the register path's constant-offset row reads may run up to 7 past the last row
+  const size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
   {
     KernelTimer kt("k_multibox", s, true);
     a.span = kt.span();
