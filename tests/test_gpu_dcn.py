@@ -129,3 +129,27 @@ def test_module_surface_and_cpu_rejection():
     assert float(m.p_conv.weight.abs().sum()) == 0.0 and float(m.m_conv.weight.abs().sum()) == 0.0
     with pytest.raises(Exception, match='ROCm device'):
         m(torch.randn(1, 4, 5, 5))
+
+
+@pytest.mark.parametrize('which', ['x', 'offset', 'mask', 'weight', 'offset+mask'])
+def test_partial_gradients_match_full_backward(which):
+    """Each subset of requested gradients (the backward skips the dx gather, the dcols rows or the
+    weight MFMA accordingly) equals the same gradients from a full backward."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    B, C, O, H, ks = 2, 48, 64, 12, 3
+    x = torch.randn(B, C, H, H, device=DEV, generator=g)
+    off = torch.randn(B, 2 * ks * ks, H, H, device=DEV, generator=g)
+    ml = torch.randn(B, ks * ks, H, H, device=DEV, generator=g)
+    w = torch.randn(O, C, ks, ks, device=DEV, generator=g) / 20
+    gout = torch.randn(B, O, H, H, device=DEV, generator=g)
+    full = [t.clone().requires_grad_(True) for t in (x, off, ml, w)]
+    core.deform_conv2d(*full, ks, 1, 1).backward(gout)
+    names = ['x', 'offset', 'mask', 'weight']
+    want = set(which.split('+'))
+    part = [t.clone().requires_grad_(n in want) for n, t in zip(names, (x, off, ml, w))]
+    core.deform_conv2d(*part, ks, 1, 1).backward(gout)
+    for n, pf, pp in zip(names, full, part):
+        if n in want:
+            close(pp.grad, pf.grad, 1e-5, 'partial ' + n)
+        else:
+            assert pp.grad is None
