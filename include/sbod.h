@@ -292,7 +292,10 @@ int sbod_nms_f32(const float *boxes, const float *scores, int64_t n, float overl
  *   x [B,C,H,W], offset [B,2k²,Ho,Wo] (p_conv output), mask_logits [B,k²,Ho,Wo] (m_conv
  *   output BEFORE sigmoid, or NULL for modulation=False), weight [O,C,k,k] -> out [B,O,Ho,Wo].
  *   Backward: grad_out -> grad_x, grad_offset, grad_mask_logits, grad_weight (any may be NULL).
- * Workspace: sbod_dcn_workspace_bytes(...). */
+ *   The backward writes dcols rows [B*Ho*Wo][k²][C] and gathers dx per input pixel (no float
+ *   atomics on dx); grad_out and weight must each stay below 2 GiB (buffer-descriptor range).
+ * Workspace: sbod_dcn_workspace_bytes(...) (forward and backward share it; it includes the
+ * backward's dcols rows, B*Ho*Wo*k²*C*4 bytes). */
 size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
 int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logits,
                      const float *weight, int B, int C, int H, int W, int O, int k, int stride,
