@@ -270,10 +270,10 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
   const int m0 = blockIdx.x * kBM, cgb = blockIdx.y * 256, n = blockIdx.z;
   const int HWo = s.Ho * s.Wo;
   const int OT = (s.O + kBOC - 1) / kBOC;
-  // Operand loads are unconditional, through wave-uniform buffer descriptors (32-bit lane offsets):
-  // out-of-range rows read a clamped valid address and are zeroed (dout) or meet a zero dout
-  // (Wb), so no branch makes the compiler wait for the prefetch before the current MFMAs.
-  const int HWo_ = HWo;
+  // Operand loads are unconditional, through wave-uniform buffer descriptors (32-bit lane offsets,
+  // a scalar offset per chunk / row): dout lanes past M read a clamped pixel and rows o >= O read
+  // in-range data or 0 (the descriptor's range check), both zeroed in dstage; Wb rows o >= O meet
+  // a zero dout.  No branch makes the compiler wait for the prefetch before the current MFMAs.
   const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(gout), static_cast<short>(0),
                                                     static_cast<int>(static_cast<int64_t>(s.M) * s.O * 4), 0x00020000);
   const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(wb), static_cast<short>(0),
@@ -284,14 +284,14 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
   for (int i = 0; i < 8; ++i) {
     const int e = tid + kDcnThreads * i;
     const int ol = e >> 6, mm = e & 63, m = min(m0 + mm, s.M - 1);
-    const int b = m / HWo_, pix = m - b * HWo_;
+    const int b = m / HWo, pix = m - b * HWo;
     dok[i] = m0 + mm < s.M;
-    dvoff[i] = ((b * s.O + ol) * HWo_ + pix) * 4;
+    dvoff[i] = ((b * s.O + ol) * HWo + pix) * 4;
   }
   float dstage[8];
   float bcur[2][16], bnext[2][16];
   auto load_dout = [&](int oc) {
-    const int so = oc * kBOC * HWo_ * 4;   // wave-uniform: rows o >= O read finite data or 0 (range check)
+    const int so = oc * kBOC * HWo * 4;   // wave-uniform: rows o >= O read finite data or 0 (range check)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const bool o_ok = oc * kBOC + ((tid + kDcnThreads * i) >> 6) < s.O;
