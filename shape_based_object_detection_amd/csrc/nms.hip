@@ -441,8 +441,10 @@ __device__ __forceinline__ void prep_slots(const DetArgs &a, int b, int C, int t
 }
 
 // CM > 0: rows of C <= CM classes live in CM registers (padding slots hold -inf, so the max, the
-// exponentials and the sum need no per-slot guards); CM == 0: any C, rows in LDS.
-template <int CM>
+// exponentials and the sum need no per-slot guards); CM == 0: any C, rows in LDS.  CE > 0: the
+// class count is the compile-time CE (VOC's 21), so no slot needs a padding select or a k < C
+// test, and only CE exponentials are evaluated.
+template <int CM, int CE>
 __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__restrict__ locs,
                                                         const float *__restrict__ scores) {
   // dynamic LDS: score tile [kDTile][C] f32 | ballots [kDTile/64][C] u64 | slot bases [C] u32,
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   STAMP_BEGIN();
   span_begin(a.span);
   const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
-  const int P = a.P, C = a.C;
+  const int P = a.P, C = CE > 0 ? CE : a.C;
   unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_sc + kDTile * C);
   uint32_t *s_wbf = reinterpret_cast<uint32_t *>(s_balf + (kDTile / 64) * C);   // per-wave slot bases
 #define s_bal(w, c) s_balf[(w) * C + (c)]
@@ -519,54 +521,84 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     // constant-offset reads (one address, no per-slot index arithmetic): a short last row reads
     // at most CM - C <= 7 floats past the tile, into the ballot area that follows it in LDS;
     // only the top 8 slots can be padding (the dispatcher picks CM with C > CM - 8)
-    float r[CM];
+    // KN: the slots that can hold a class (compile-time when CE > 0)
+    constexpr int KN = CE > 0 ? CE : CM;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    float r[KN];
 #pragma unroll
-    for (int k = 0; k < CM; ++k) {
+    for (int k = 0; k < KN; ++k) {
       const float v = row[k];
-      r[k] = (k < CM - 8 || k < C) ? v : -__builtin_inff();
+      r[k] = (CE > 0 || k < CM - 8 || k < C) ? v : -__builtin_inff();
     }
     const bool softmax = a.act == SBOD_ACT_SOFTMAX;
     float m = 0.f, rs = 1.f;
     if (softmax) {
       m = r[0];
 #pragma unroll
-      for (int k = 1; k < CM; ++k) m = fmaxf(m, r[k]);   // NaN rows give NaN probabilities either way
-      float sum = 0.f;
+      for (int k = 1; k < KN; ++k) m = fmaxf(m, r[k]);   // NaN rows give NaN probabilities either way
+      // (x - m) * log2(e) two slots per packed op, hardware exp2, pairwise packed sums
+      const f2 nm2 = {-m, -m}, l2 = {1.4426950408889634f, 1.4426950408889634f};
 #pragma unroll
-      for (int k = 0; k < CM; ++k) {
-        r[k] = fast_exp(r[k] - m);   // padding: exp(-inf) = 0
-        sum += r[k];
+      for (int k = 0; k + 1 < KN; k += 2) {
+        f2 t = {r[k], r[k + 1]};
+        t = (t + nm2) * l2;
+        r[k] = __builtin_amdgcn_exp2f(t.x);   // padding: exp2(-inf) = 0
+        r[k + 1] = __builtin_amdgcn_exp2f(t.y);
       }
-      rs = __builtin_amdgcn_rcpf(sum);
+      if constexpr (KN % 2 == 1) r[KN - 1] = __builtin_amdgcn_exp2f((r[KN - 1] - m) * 1.4426950408889634f);
+      f2 acc2 = {0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < CM; ++k) r[k] = r[k] * rs;
+      for (int k = 0; k + 1 < KN; k += 2) acc2 += f2{r[k], r[k + 1]};
+      float sum = acc2.x + acc2.y;
+      if constexpr (KN % 2 == 1) sum += r[KN - 1];
+      rs = __builtin_amdgcn_rcpf(sum);
+      const f2 rs2 = {rs, rs};
+#pragma unroll
+      for (int k = 0; k + 1 < KN; k += 2) {
+        const f2 t = f2{r[k], r[k + 1]} * rs2;
+        r[k] = t.x;
+        r[k + 1] = t.y;
+      }
+      if constexpr (KN % 2 == 1) r[KN - 1] *= rs;
     } else {
 #pragma unroll
-      for (int k = 0; k < CM; ++k) r[k] = fast_sigmoid(r[k]);
+      for (int k = 0; k < KN; ++k) r[k] = fast_sigmoid(r[k]);
     }
     if (a.dbg_probs && valid) {
 #pragma unroll
-      for (int k = 0; k < CM; ++k)
+      for (int k = 0; k < KN; ++k)
         if (k < C) a.dbg_probs[i * C + k] = r[k];
     }
+    // per class: one compare straight into a wave mask (lanes that may not emit compare against
+    // +inf), kept in scalar registers; this lane's bit shifted into cmask (class k at bit KN-1-k)
+    const float thr = allowed ? a.min_score : __builtin_inff();
     uint32_t cmask = 0;
+    unsigned long long bals[KN];
 #pragma unroll
-    for (int k = 1; k < CM; ++k) {
+    for (int k = 1; k < KN; ++k) {
       if (k < C) {
-        const bool take = allowed && r[k] > a.min_score;
-        const unsigned long long bal = __ballot(take);
-        if (lane == 0) s_bal(wv, k) = bal;
-        cmask |= take ? (1u << k) : 0u;
+        const bool take = r[k] > thr;
+        bals[k] = __builtin_amdgcn_ballot_w64(take);
+        cmask = cmask + cmask + (take ? 1u : 0u);
+      } else {
+        bals[k] = 0ull;
+        cmask = cmask + cmask;
       }
+    }
+    if (lane == 0) {   // one exec switch for all the wave's masks
+#pragma unroll
+      for (int k = 1; k < KN; ++k)
+        if (k < C) s_bal(wv, k) = bals[k];
     }
     SEG_PHASE(2);
     prep_slots(a, b, C, tid, s_balf, s_wbf);
     SEG_PHASE(3);
     while (cmask) {
-      const int c = __builtin_ctz(cmask);
+      const int c = KN - 1 - __builtin_ctz(cmask);
       cmask &= cmask - 1u;
       const unsigned long long bal = s_bal(wv, c);
-      const float pc = softmax ? fast_exp(row[c] - m) * rs : fast_sigmoid(row[c]);
+      // the emitted probability: the same operations as above on the raw LDS row (bit-identical)
+      const float pc = softmax ? __builtin_amdgcn_exp2f((row[c] - m) * 1.4426950408889634f) * rs : fast_sigmoid(row[c]);
       // (plain store: these 8-byte scattered writes must merge into full lines in L2 first —
       // streamed through they cost 1.7x the kernel time)
       const uint32_t slot = s_wb(wv, c) + __popcll(bal & lt);
@@ -2052,11 +2084,12 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     a.span = kt.span();
     const dim3 pg((P + kDTile - 1) / kDTile, B);
     const size_t pl = static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12;
-    if (C <= 8) tlaunch(kt, k_det_prepare<8>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 16) tlaunch(kt, k_det_prepare<16>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 24) tlaunch(kt, k_det_prepare<24>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 32) tlaunch(kt, k_det_prepare<32>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else tlaunch(kt, k_det_prepare<0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
+    if (C <= 8) tlaunch(kt, k_det_prepare<8, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 16) tlaunch(kt, k_det_prepare<16, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C == 21) tlaunch(kt, k_det_prepare<24, 21>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 24) tlaunch(kt, k_det_prepare<24, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else if (C <= 32) tlaunch(kt, k_det_prepare<32, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    else tlaunch(kt, k_det_prepare<0, 0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
                  static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, locs, scores);
   }
   SBOD_LAUNCHED("k_det_prepare");
