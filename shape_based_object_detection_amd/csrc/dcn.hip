@@ -130,6 +130,25 @@ __device__ __forceinline__ void load_vec(const float *p, bool ok, float *v) {
   }
 }
 
+// XCD-aware workgroup order.  The dispatcher deals workgroups to the 8 XCDs round-robin, so
+// consecutive logical tiles (which share corner rows of x, dout pixel rows or a weight slice)
+// would land on 8 different L2s.  Dispatch id L -> logical id: each XCD gets one contiguous
+// range of logical tiles (a bijection for any total).
+struct Tile3 {
+  int x, y, z;
+};
+__device__ __forceinline__ int xcd_logical(int L, int total) {
+  const int q = total >> 3, r = total & 7, x = L & 7, pos = L >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + pos;
+}
+// the logical id decomposed with extents (nx fastest, ny, nz)
+__device__ __forceinline__ Tile3 xcd_tile(int nx, int ny, int nz) {
+  const int L = static_cast<int>(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+  const int lam = xcd_logical(L, nx * ny * nz);
+  const int x = lam % nx, rest = lam / nx;
+  return Tile3{x, rest % ny, rest / ny};
+}
+
 // ----------------------------------------------------------------------------- forward
 // Block: 64 pixels x 256 output channels, 4 waves x (64 channels x 64 pixels) = 2 x 2 MFMA tiles.
 // K'-tiles of 32 channels of one kernel point; blockIdx.z takes a contiguous share of them
@@ -144,11 +163,12 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd(DcnShape s, const fl
                                                             float *__restrict__ out, int atomic_out) {
   __shared__ float s_cols[2][kFKC][kFLD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
-  const int m0 = blockIdx.x * kFM, o0 = blockIdx.y * 256;
+  const Tile3 tl = xcd_tile(gridDim.x, gridDim.y, gridDim.z);   // consecutive pixel tiles share an L2
+  const int m0 = tl.x * kFM, o0 = tl.y * 256;
   const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
   const int CT = (s.C + kFKC - 1) / kFKC, T = s.N * CT;
-  const int t0 = static_cast<int>(static_cast<int64_t>(blockIdx.z) * T / gridDim.z);
-  const int t1 = static_cast<int>(static_cast<int64_t>(blockIdx.z + 1) * T / gridDim.z);
+  const int t0 = static_cast<int>(static_cast<int64_t>(tl.z) * T / gridDim.z);
+  const int t1 = static_cast<int>(static_cast<int64_t>(tl.z + 1) * T / gridDim.z);
   // sampler role: pixel mm, 8 channels starting at 8 * cq
   const int mm = tid & 63, cq = tid >> 6;
   const int ms = m0 + mm;
@@ -267,7 +287,10 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
     DcnShape s, const float *__restrict__ wb, const float *__restrict__ gout, float *__restrict__ dcols) {
   __shared__ float s_dout[2][kBOC][kBLD];     // A operand [o][m]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
-  const int m0 = blockIdx.x * kBM, cgb = blockIdx.y * 256, n = blockIdx.z;
+  // logical order kernel point fastest: the N tiles of one pixel tile (same dout rows) run
+  // back to back on one XCD
+  const Tile3 tl = xcd_tile(gridDim.z, gridDim.x, gridDim.y);
+  const int m0 = tl.y * kBM, cgb = tl.z * 256, n = tl.x;
   const int HWo = s.Ho * s.Wo;
   const int OT = (s.O + kBOC - 1) / kBOC;
   // Operand loads are unconditional, through wave-uniform buffer descriptors (32-bit lane offsets,
@@ -412,7 +435,8 @@ __global__ __launch_bounds__(256) void k_dcn_dx_gather(int C, int ntarget, const
                                                        const DxEnt *__restrict__ ent,
                                                        const float *__restrict__ dcols, float *__restrict__ gxt) {
   const int lane = threadIdx.x & 63;
-  const int tp = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // neighbouring input pixels (overlapping dcols rows) on one XCD
+  const int tp = xcd_logical(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (tp >= ntarget) return;
   const uint32_t e0 = __builtin_amdgcn_readfirstlane(toff[tp]), e1 = __builtin_amdgcn_readfirstlane(toff[tp + 1]);
   for (int c0 = VEC * lane; c0 < C; c0 += 64 * VEC) {
@@ -469,12 +493,13 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
   __shared__ float s_cols[2][kWMs][kWLD];      // B operand [m][c]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
   const int CTw = (s.C + kWC - 1) / kWC;
-  const int n = blockIdx.x / CTw, c0 = (blockIdx.x - n * CTw) * kWC;
-  const int ms0 = blockIdx.y * m_slice, o0 = blockIdx.z * 256;
+  const Tile3 tl = xcd_tile(gridDim.x, gridDim.y, gridDim.z);   // one pixel slice's tiles share an L2
+  const int n = tl.x / CTw, c0 = (tl.x - n * CTw) * kWC;
+  const int ms0 = tl.y * m_slice, o0 = tl.z * 256;
   const int mend = min(ms0 + m_slice, s.M);
   const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
   const int smm = tid >> 3, scg = (tid & 7) * 8;
-  const bool dofs = dcols != nullptr && blockIdx.z == 0;   // offset / mask gradients here
+  const bool dofs = dcols != nullptr && tl.z == 0;   // offset / mask gradients here
   const bool dow = gwp != nullptr;
   float X[4][8], D[8];
   float cg[4] = {0.f, 0.f, 0.f, 0.f}, cm = 0.f;
