@@ -153,15 +153,20 @@ __device__ __forceinline__ Tile3 xcd_tile(int nx, int ny, int nz) {
 // Block: 64 pixels x 256 output channels, 4 waves x (64 channels x 64 pixels) = 2 x 2 MFMA tiles.
 // K'-tiles of 32 channels of one kernel point; blockIdx.z takes a contiguous share of them
 // (split-K for small maps, combined with float atomics).  One tile of gathers is in flight while
-// the previous tile's MFMAs run (double-buffered LDS, one barrier per tile).
+// the previous tile's MFMAs run (double-buffered LDS, one barrier per tile); the weights are
+// single-buffered (loaded after the MFMAs that read them), 3 workgroups per CU.
 constexpr int kFM = 64, kFKC = 32, kFLD = kFM + 2;
 
+#ifndef SBOD_DCN_FWD_WAVES
+#define SBOD_DCN_FWD_WAVES 3
+#endif
 template <int VEC>
-__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd(DcnShape s, const float *__restrict__ xt,
+__global__ __launch_bounds__(kDcnThreads, SBOD_DCN_FWD_WAVES) void k_dcn_fwd(DcnShape s, const float *__restrict__ xt,
                                                             const Coef *__restrict__ coef,
                                                             const float *__restrict__ wf,
                                                             float *__restrict__ out, int atomic_out) {
   __shared__ float s_cols[2][kFKC][kFLD];
+  __shared__ float s_coef[kMaxN][9][kFM];   // per kernel point: idx[4] | g[4] | mask of each pixel
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
   const Tile3 tl = xcd_tile(gridDim.x, gridDim.y, gridDim.z);   // consecutive pixel tiles share an L2
   const int m0 = tl.x * kFM, o0 = tl.y * 256;
@@ -171,15 +176,42 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd(DcnShape s, const fl
   const int t1 = static_cast<int>(static_cast<int64_t>(tl.z + 1) * T / gridDim.z);
   // sampler role: pixel mm, 8 channels starting at 8 * cq
   const int mm = tid & 63, cq = tid >> 6;
-  const int ms = m0 + mm;
-  const bool mvalid = ms < s.M;
-  const int bs = mvalid ? ms / HWo : 0;
-  const float *xb = xt + static_cast<int64_t>(bs) * HW * s.C;
-  int cur_n = -1;
-  int cidx[4] = {-1, -1, -1, -1};
-  float cg[4] = {0.f, 0.f, 0.f, 0.f}, cm = 0.f;
+  // pixels past M sample a clamped pixel: their columns only reach output columns that are never
+  // stored.  Every operand load below is unconditional (clamped addresses, zero selects applied
+  // when the columns are stored), so the loop is straight-line code and the waits the compiler
+  // places before the MFMAs cover exactly the weights they read, not the gathers in flight.
+  const int ms = min(m0 + mm, s.M - 1);
+  const float *xb = xt + static_cast<int64_t>(ms / HWo) * HW * s.C;
+  struct Cf {
+    int idx[4];
+    float g[4], m;
+  };
+  // the block's coefficients (every kernel point of its 64 pixels) staged in LDS once: the
+  // gathers then depend on LDS reads only, never on a global load in flight
+  for (int e = tid; e < s.N * kFM; e += kDcnThreads) {
+    const int n = e / kFM, px = e - n * kFM;
+    const float *c = reinterpret_cast<const float *>(coef + static_cast<int64_t>(min(m0 + px, s.M - 1)) * s.N + n);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) s_coef[n][j][px] = c[j];
+  }
+  __syncthreads();
+  // K'-tile order t = channel chunk * N + kernel point: consecutive tiles sample the same 32
+  // channels at the 3x3 neighbourhood's positions, so their corner lines are still in L2 (the
+  // kernel-point-major order revisited every line only after N chunks' worth of other lines)
+  auto load_coef = [&](int t) {   // idx, g and mask of this pixel's kernel point for tile t
+    const int n = t % s.N;
+    Cf c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      c.idx[q] = __builtin_bit_cast(int, s_coef[n][q][mm]);
+      c.g[q] = s_coef[n][4 + q][mm];
+    }
+    c.m = s_coef[n][8][mm];
+    return c;
+  };
   float X[4][8];
-  float acur[2][16], anext[2][16];
+  bool xok[4][8 / VEC];
+  float acur[2][16];   // one A buffer: the next tile's weights load once the MFMAs have read these
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -188,73 +220,65 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd(DcnShape s, const fl
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  auto gather = [&](int t) {
-    const int n = t / CT, c0 = (t - n * CT) * kFKC + 8 * cq;
-    if (n != cur_n) {
-      cur_n = n;
-      if (mvalid) {
-        const Coef cf = coef[static_cast<int64_t>(ms) * s.N + n];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { cidx[q] = cf.idx[q]; cg[q] = cf.g[q]; }
-        cm = cf.mval;
-      }
-    }
+  auto gather = [&](int t, const Cf &cf) {
+    const int c0 = (t / s.N) * kFKC + 8 * cq;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float *p = xb + static_cast<int64_t>(cidx[q]) * s.C;
+      const float *p = xb + static_cast<int64_t>(max(cf.idx[q], 0)) * s.C;
 #pragma unroll
       for (int v = 0; v < 8; v += VEC) {
         const int c = c0 + v;
-        load_vec<VEC>(p + c, mvalid && cidx[q] >= 0 && c < s.C, &X[q][v]);
+        xok[q][v / VEC] = cf.idx[q] >= 0 && c < s.C;
+        load_vec<VEC>(p + min(c, s.C - VEC), true, &X[q][v]);
       }
     }
   };
-  auto store_cols = [&](int buf) {
+  auto store_cols = [&](int buf, const Cf &cf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 8; ++v) X[q][v] = xok[q][v / VEC] ? X[q][v] : 0.f;
 #pragma unroll
     for (int v = 0; v < 8; ++v)
-      s_cols[buf][8 * cq + v][mm] = combine(cg, cm, X[0][v], X[1][v], X[2][v], X[3][v]);
+      s_cols[buf][8 * cq + v][mm] = combine(cf.g, cf.m, X[0][v], X[1][v], X[2][v], X[3][v]);
   };
-  auto load_a = [&](int t, float (&a)[2][16]) {
-    const int n = t / CT, c0 = (t - n * CT) * kFKC + 16 * h;
+  auto load_a = [&](int t) {   // rows past O are never stored; columns past C meet zero columns
+    const int ct = t / s.N, n = t - ct * s.N, c0 = ct * kFKC + 16 * h;
 #pragma unroll
     for (int ri = 0; ri < 2; ++ri) {
-      const int o = o0 + 64 * wv + 32 * ri + l31;
+      const int o = min(o0 + 64 * wv + 32 * ri + l31, s.O - 1);
       const float *p = wf + static_cast<int64_t>(o) * s.K + static_cast<int64_t>(n) * s.C;
 #pragma unroll
-      for (int v = 0; v < 16; v += VEC) load_vec<VEC>(p + c0 + v, o < s.O && c0 + v < s.C, &a[ri][v]);
+      for (int v = 0; v < 16; v += VEC) load_vec<VEC>(p + min(c0 + v, s.C - VEC), true, &acur[ri][v]);
     }
   };
 
   if (t0 < t1) {
-    gather(t0);
-    store_cols(0);
-    load_a(t0, acur);
-  }
-  __syncthreads();
-  for (int t = t0; t < t1; ++t) {
-    const int buf = (t - t0) & 1;
-    const bool more = t + 1 < t1;
-    if (more) {
-      gather(t + 1);
-      load_a(t + 1, anext);
-    }
-#pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const float b0 = s_cols[buf][16 * h + st][l31];
-      const float b1 = s_cols[buf][16 * h + st][32 + l31];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b1, acc[1][1], 0, 0, 0);
-    }
-    if (more) {
-      store_cols(buf ^ 1);
-#pragma unroll
-      for (int ri = 0; ri < 2; ++ri)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acur[ri][v] = anext[ri][v];
-    }
+    Cf cf = load_coef(t0);
+    gather(t0, cf);
+    store_cols(0, cf);
+    load_a(t0);
     __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+      const int buf = (t - t0) & 1;
+      const int tn = min(t + 1, t1 - 1);   // the last pass re-gathers its own tile into the idle buffer
+      cf = load_coef(tn);
+      gather(tn, cf);
+      __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const float b0 = s_cols[buf][16 * h + st][l31];
+        const float b1 = s_cols[buf][16 * h + st][32 + l31];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b1, acc[1][1], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      load_a(tn);   // L2-resident weights, in flight through the column store and barrier
+      store_cols(buf ^ 1, cf);
+      __syncthreads();
+    }
   }
   // C/D map (gfx950, dtype independent): col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
@@ -485,26 +509,43 @@ __global__ __launch_bounds__(256) void k_dcn_dx_gather(int C, int ntarget, const
 // partials per (pixel, kernel point); output-channel block 0 only).
 constexpr int kWC = 64, kWMs = 32, kWLD = kWC + 2;
 
-template <int VEC, bool AVEC>
-__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
+template <int VEC, bool AVEC, bool DOFS>   // (the scalar-channel form needs more registers: one block per CU)
+__global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weight(
     DcnShape s, const float *__restrict__ xt, const Coef *__restrict__ coef,
     const float *__restrict__ gout, float *__restrict__ gwp, int m_slice,
     const float *__restrict__ dcols, float *__restrict__ goff, float *__restrict__ gmlog) {
   __shared__ float s_cols[2][kWMs][kWLD];      // B operand [m][c]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
-  const int CTw = (s.C + kWC - 1) / kWC;
   const Tile3 tl = xcd_tile(gridDim.x, gridDim.y, gridDim.z);   // one pixel slice's tiles share an L2
-  const int n = tl.x / CTw, c0 = (tl.x - n * CTw) * kWC;
+  // kernel point fastest: the N blocks of one channel block and pixel slice (the same corner
+  // lines, dout rows) run side by side on one XCD
+  const int cb = tl.x / s.N, n = tl.x - cb * s.N, c0 = cb * kWC;
   const int ms0 = tl.y * m_slice, o0 = tl.z * 256;
   const int mend = min(ms0 + m_slice, s.M);
   const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
   const int smm = tid >> 3, scg = (tid & 7) * 8;
-  const bool dofs = dcols != nullptr && tl.z == 0;   // offset / mask gradients here
+  const bool oblk0 = tl.z == 0;   // offset / mask gradients from output-channel block 0 only
   const bool dow = gwp != nullptr;
+  // Every operand load is unconditional (pixels past the slice read a clamped pixel and their
+  // columns are stored as zeros; corners outside the map and channels past C are zeroed at the
+  // store), so the loop is straight-line code: the waits before the MFMAs cover the dout rows
+  // they read, not the next chunk's gathers in flight.
+  struct CfW {
+    int idx[4];
+    float g[4], m, tlx, rbx, tly, rby;
+    int inr;
+  };
+  auto load_cf = [&](int m0) {
+    const float *c = reinterpret_cast<const float *>(coef + static_cast<int64_t>(min(m0 + smm, mend - 1)) * s.N + n);
+    float2 w[7];   // a Coef is 8-byte aligned (56 bytes)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) w[j] = reinterpret_cast<const float2 *>(c)[j];
+    return CfW{{__builtin_bit_cast(int, w[0].x), __builtin_bit_cast(int, w[0].y), __builtin_bit_cast(int, w[1].x),
+                __builtin_bit_cast(int, w[1].y)},
+               {w[2].x, w[2].y, w[3].x, w[3].y}, w[4].x, w[4].y, w[5].x, w[5].y, w[6].x, __builtin_bit_cast(int, w[6].y)};
+  };
   float X[4][8], D[8];
-  float cg[4] = {0.f, 0.f, 0.f, 0.f}, cm = 0.f;
-  float ctlx = 0.f, crbx = 0.f, ctly = 0.f, crby = 0.f;
-  int cinr = 0, cmpix = -1;
+  bool xok[4][8 / VEC];
   float acur[2][16], anext[2][16];
   f32x16 acc[2][2];
 #pragma unroll
@@ -514,119 +555,121 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  auto gather = [&](int m0) {
-    const int m = m0 + smm;
-    const bool ok = m < mend;
-    int idx[4] = {-1, -1, -1, -1};
-    cmpix = -1;
-    if (ok) {
-      const Coef cf = coef[static_cast<int64_t>(m) * s.N + n];
+  auto gather = [&](int m0, const CfW &cf) {
+    const int m = min(m0 + smm, mend - 1);
+    const float *xb = xt + static_cast<int64_t>(m / HWo) * HW * s.C;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) { idx[q] = cf.idx[q]; cg[q] = cf.g[q]; }
-      cm = cf.mval;
-      ctlx = cf.tlx; crbx = cf.rbx; ctly = cf.tly; crby = cf.rby; cinr = cf.inr;
-      cmpix = m;
+    for (int q = 0; q < 4; ++q) {
+      const float *p = xb + static_cast<int64_t>(max(cf.idx[q], 0)) * s.C;
+#pragma unroll
+      for (int v = 0; v < 8; v += VEC) {
+        const int c = c0 + scg + v;
+        xok[q][v / VEC] = cf.idx[q] >= 0 && c < s.C;
+        load_vec<VEC>(p + min(c, s.C - VEC), true, &X[q][v]);
+      }
     }
-    const float *xb = xt + static_cast<int64_t>(ok ? m / HWo : 0) * HW * s.C + c0 + scg;
+    if constexpr (DOFS) {
+      const float *dr = dcols + (static_cast<int64_t>(m) * s.N + n) * s.C;
+#pragma unroll
+      for (int v = 0; v < 8; v += VEC) load_vec<VEC>(dr + min(c0 + scg + v, s.C - VEC), true, &D[v]);
+    }
+  };
+  // live: this chunk's offset / mask partials are added (false for the prefetch past the last)
+  auto store_cols = [&](int buf, const CfW &cf, int m0, bool live) {
+    const bool ok = m0 + smm < mend;
+    const float cm = cf.m;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int v = 0; v < 8; v += VEC)
-        load_vec<VEC>(xb + static_cast<int64_t>(idx[q]) * s.C + v, idx[q] >= 0 && c0 + scg + v < s.C, &X[q][v]);
-    if (dofs) {
-      const float *dr = dcols + (static_cast<int64_t>(ok ? m : 0) * s.N + n) * s.C + c0 + scg;
-#pragma unroll
-      for (int v = 0; v < 8; v += VEC) load_vec<VEC>(dr + v, ok && c0 + scg + v < s.C, &D[v]);
-    }
-  };
-  auto store_cols = [&](int buf) {
+      for (int v = 0; v < 8; ++v) X[q][v] = (ok && xok[q][v / VEC]) ? X[q][v] : 0.f;
     float pm = 0.f, ppx = 0.f, ppy = 0.f;
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
-      const float raw = ((cg[0] * X[0][v] + cg[1] * X[1][v]) + cg[2] * X[2][v]) + cg[3] * X[3][v];
+      const float raw = ((cf.g[0] * X[0][v] + cf.g[1] * X[1][v]) + cf.g[2] * X[2][v]) + cf.g[3] * X[3][v];
       s_cols[buf][smm][scg + v] = raw * cm;   // == combine(): the forward's column value
-      if (dofs) {
-        pm += D[v] * raw;
-        ppx += D[v] * (-(1.f + ctly) * X[0][v] + (1.f - crby) * X[1][v] - (1.f - crby) * X[2][v] + (1.f + ctly) * X[3][v]);
-        ppy += D[v] * (-(1.f + ctlx) * X[0][v] + (1.f - crbx) * X[1][v] + (1.f + ctlx) * X[2][v] - (1.f - crbx) * X[3][v]);
+      if constexpr (DOFS) {
+        const float d = c0 + scg + v < s.C ? D[v] : 0.f;
+        pm += d * raw;
+        ppx += d * (-(1.f + cf.tly) * X[0][v] + (1.f - cf.rby) * X[1][v] - (1.f - cf.rby) * X[2][v] + (1.f + cf.tly) * X[3][v]);
+        ppy += d * (-(1.f + cf.tlx) * X[0][v] + (1.f - cf.rbx) * X[1][v] + (1.f + cf.tlx) * X[2][v] - (1.f - cf.rbx) * X[3][v]);
       }
     }
-    if (dofs) {   // the 8 lanes of this pixel are lanes 8k..8k+7: quad swaps + half-row mirror
-      pm += dpp_f32_or0<0xB1, 0xf>(pm);
-      ppx += dpp_f32_or0<0xB1, 0xf>(ppx);
-      ppy += dpp_f32_or0<0xB1, 0xf>(ppy);
-      pm += dpp_f32_or0<0x4E, 0xf>(pm);
-      ppx += dpp_f32_or0<0x4E, 0xf>(ppx);
-      ppy += dpp_f32_or0<0x4E, 0xf>(ppy);
-      pm += dpp_f32_or0<0x141, 0xf>(pm);
-      ppx += dpp_f32_or0<0x141, 0xf>(ppx);
-      ppy += dpp_f32_or0<0x141, 0xf>(ppy);
-      if ((tid & 7) == 0 && cmpix >= 0) {
-        const int b = cmpix / HWo, pix = cmpix - b * HWo;
-        if (goff) {
-          atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + n) * HWo + pix, (cinr & 1) ? ppx * cm : 0.f);
-          atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + s.N + n) * HWo + pix, (cinr & 2) ? ppy * cm : 0.f);
+    if constexpr (DOFS) {   // the 8 lanes of this pixel are lanes 8k..8k+7: quad swaps + half-row mirror
+      if (live && oblk0) {
+        pm += dpp_f32_or0<0xB1, 0xf>(pm);
+        ppx += dpp_f32_or0<0xB1, 0xf>(ppx);
+        ppy += dpp_f32_or0<0xB1, 0xf>(ppy);
+        pm += dpp_f32_or0<0x4E, 0xf>(pm);
+        ppx += dpp_f32_or0<0x4E, 0xf>(ppx);
+        ppy += dpp_f32_or0<0x4E, 0xf>(ppy);
+        pm += dpp_f32_or0<0x141, 0xf>(pm);
+        ppx += dpp_f32_or0<0x141, 0xf>(ppx);
+        ppy += dpp_f32_or0<0x141, 0xf>(ppy);
+        if ((tid & 7) == 0 && ok) {
+          const int m = m0 + smm, b = m / HWo, pix = m - b * HWo;
+          if (goff) {
+            atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + n) * HWo + pix, (cf.inr & 1) ? ppx * cm : 0.f);
+            atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + s.N + n) * HWo + pix, (cf.inr & 2) ? ppy * cm : 0.f);
+          }
+          if (gmlog) atomicAdd(gmlog + (static_cast<int64_t>(b) * s.N + n) * HWo + pix, pm * cm * (1.f - cm));
         }
-        if (gmlog) atomicAdd(gmlog + (static_cast<int64_t>(b) * s.N + n) * HWo + pix, pm * cm * (1.f - cm));
       }
     }
   };
-  auto load_a = [&](int m0, float (&a)[2][16]) {
+  auto load_a = [&](int m0, float (&a)[2][16]) {   // dout rows; pixels past the slice meet zero columns
     const int mb = m0 + 16 * h;
 #pragma unroll
     for (int ri = 0; ri < 2; ++ri) {
-      const int o = o0 + 64 * wv + 32 * ri + l31;
-      if (AVEC) {
+      const int o = min(o0 + 64 * wv + 32 * ri + l31, s.O - 1);
+      if (AVEC) {   // 32-pixel chunks inside one image, slices of whole chunks: mb + 15 < mend
         const int b = mb / HWo, pix = mb - b * HWo;
         const float *p = gout + (static_cast<int64_t>(b) * s.O + o) * HWo + pix;
 #pragma unroll
-        for (int v = 0; v < 16; v += 4) load_vec<4>(p + v, o < s.O && mb + v < mend, &a[ri][v]);
+        for (int v = 0; v < 16; v += 4) load_vec<4>(p + v, true, &a[ri][v]);
       } else {
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
-          const int m = mb + v;
-          float val = 0.f;
-          if (o < s.O && m < mend) {
-            const int b = m / HWo, pix = m - b * HWo;
-            val = gout[(static_cast<int64_t>(b) * s.O + o) * HWo + pix];
-          }
-          a[ri][v] = val;
+          const int m = min(mb + v, mend - 1);
+          const int b = m / HWo, pix = m - b * HWo;
+          a[ri][v] = gout[(static_cast<int64_t>(b) * s.O + o) * HWo + pix];
         }
       }
     }
   };
 
   if (ms0 < mend) {
-    gather(ms0);
-    store_cols(0);
+    const int nch = (mend - ms0 + kWMs - 1) / kWMs;
+    CfW cf = load_cf(ms0);
+    gather(ms0, cf);
+    store_cols(0, cf, ms0, true);
     load_a(ms0, acur);
-  }
-  __syncthreads();
-  int it = 0;
-  for (int m0 = ms0; m0 < mend; m0 += kWMs, ++it) {
-    const int buf = it & 1;
-    const bool more = m0 + kWMs < mend;
-    if (more) {
-      gather(m0 + kWMs);
-      load_a(m0 + kWMs, anext);
-    }
+    CfW cn = load_cf(ms0 + min(1, nch - 1) * kWMs);   // coefficients one chunk ahead of the gathers
+    __syncthreads();
+    for (int i = 0; i < nch; ++i) {
+      const int buf = i & 1;
+      const int mn = ms0 + min(i + 1, nch - 1) * kWMs;   // the last pass re-gathers its own chunk
+      cf = cn;
+      gather(mn, cf);
+      load_a(mn, anext);
+      cn = load_cf(ms0 + min(i + 2, nch - 1) * kWMs);
+      __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const float b0 = s_cols[buf][16 * h + st][l31];
-      const float b1 = s_cols[buf][16 * h + st][32 + l31];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b1, acc[1][1], 0, 0, 0);
-    }
-    if (more) {
-      store_cols(buf ^ 1);
+      for (int st = 0; st < 16; ++st) {
+        const float b0 = s_cols[buf][16 * h + st][l31];
+        const float b1 = s_cols[buf][16 * h + st][32 + l31];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[0][st], b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b1, acc[1][1], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      store_cols(buf ^ 1, cf, mn, i + 1 < nch);
 #pragma unroll
       for (int ri = 0; ri < 2; ++ri)
 #pragma unroll
         for (int v = 0; v < 16; ++v) acur[ri][v] = anext[ri][v];
+      __syncthreads();
     }
-    __syncthreads();
   }
   if (!dow) return;   // (offset / mask gradients only: the MFMA result is not wanted)
 #pragma unroll
@@ -849,15 +892,19 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
     const float *dc = need_om ? w.dcols : nullptr;
     {
       KernelTimer kt("k_dcn_bwd_weight", hs);
-      if (s.C % 4 == 0 && avec)
-        hipLaunchKernelGGL((k_dcn_bwd_weight<4, true>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp,
-                           m_slice, dc, grad_offset, grad_mask_logits);
-      else if (s.C % 4 == 0)
-        hipLaunchKernelGGL((k_dcn_bwd_weight<4, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp,
-                           m_slice, dc, grad_offset, grad_mask_logits);
-      else
-        hipLaunchKernelGGL((k_dcn_bwd_weight<1, false>), grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp,
-                           m_slice, dc, grad_offset, grad_mask_logits);
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp, m_slice, dc,
+                           grad_offset, grad_mask_logits);
+      };
+      if (dc) {
+        if (s.C % 4 == 0 && avec) go(k_dcn_bwd_weight<4, true, true>);
+        else if (s.C % 4 == 0) go(k_dcn_bwd_weight<4, false, true>);
+        else go(k_dcn_bwd_weight<1, false, true>);
+      } else {
+        if (s.C % 4 == 0 && avec) go(k_dcn_bwd_weight<4, true, false>);
+        else if (s.C % 4 == 0) go(k_dcn_bwd_weight<4, false, false>);
+        else go(k_dcn_bwd_weight<1, false, false>);
+      }
     }
     SBOD_LAUNCHED("k_dcn_bwd_weight");
     if (grad_weight) {
