@@ -166,7 +166,8 @@ __global__ __launch_bounds__(kDcnThreads, SBOD_DCN_FWD_WAVES) void k_dcn_fwd(Dcn
                                                             const float *__restrict__ wf,
                                                             float *__restrict__ out, int atomic_out) {
   __shared__ float s_cols[2][kFKC][kFLD];
-  __shared__ float s_coef[kMaxN][9][kFM];   // per kernel point: idx[4] | g[4] | mask of each pixel
+  extern __shared__ float s_coefd[];        // dynamic [N][9][kFM]: idx[4] | g[4] | mask of each pixel
+  float (*s_coef)[9][kFM] = reinterpret_cast<float (*)[9][kFM]>(s_coefd);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
   const Tile3 tl = xcd_tile(gridDim.x, gridDim.y, gridDim.z);   // consecutive pixel tiles share an L2
   const int m0 = tl.x * kFM, o0 = tl.y * 256;
@@ -810,10 +811,16 @@ int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logi
     return launch_status("hipMemsetAsync(dcn out)");
   const dim3 grid(mt, og, split);
   KernelTimer kt("k_dcn_fwd", hs);
+  const size_t lds = static_cast<size_t>(s.N) * 9 * kFM * 4;   // the block's coefficients
+  if (lds > 48 * 1024) {   // k >= 5: above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
+    const void *f = s.C % 4 == 0 ? reinterpret_cast<const void *>(k_dcn_fwd<4>) : reinterpret_cast<const void *>(k_dcn_fwd<1>);
+    if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess)
+      return launch_status("hipFuncSetAttribute(k_dcn_fwd LDS)");
+  }
   if (s.C % 4 == 0)
-    hipLaunchKernelGGL(k_dcn_fwd<4>, grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
+    hipLaunchKernelGGL(k_dcn_fwd<4>, grid, dim3(kDcnThreads), lds, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_dcn_fwd<1>, grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
+    hipLaunchKernelGGL(k_dcn_fwd<1>, grid, dim3(kDcnThreads), lds, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
   SBOD_LAUNCHED("k_dcn_fwd");
   return SBOD_OK;
 }
