@@ -161,7 +161,7 @@ constexpr int kFM = 64, kFKC = 32, kFLD = kFM + 2;
 #define SBOD_DCN_FWD_WAVES 3
 #endif
 template <int VEC>
-__global__ __launch_bounds__(kDcnThreads, SBOD_DCN_FWD_WAVES) void k_dcn_fwd(DcnShape s, const float *__restrict__ xt,
+__global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_FWD_WAVES : 2) void k_dcn_fwd(DcnShape s, const float *__restrict__ xt,
                                                             const Coef *__restrict__ coef,
                                                             const float *__restrict__ wf,
                                                             float *__restrict__ out, int atomic_out) {
