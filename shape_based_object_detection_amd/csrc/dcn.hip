@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_FWD_WAVES : 2) voi
 // which k_dcn_bwd_weight already samples, so they are reduced there.
 constexpr int kBM = 64, kBOC = 32, kBLD = kBM + 2;
 
-__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
+__global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
     DcnShape s, const float *__restrict__ wb, const float *__restrict__ gout, float *__restrict__ dcols) {
   __shared__ float s_dout[2][kBOC][kBLD];     // A operand [o][m]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
     dvoff[i] = ((b * s.O + ol) * HWo + pix) * 4;
   }
   float dstage[8];
-  float bcur[2][16], bnext[2][16];
+  float bcur[2][16];   // one B buffer: the next chunk's weights load once the MFMAs have read these
   auto load_dout = [&](int oc) {
     const int so = oc * kBOC * HWo * 4;   // wave-uniform: rows o >= O read finite data or 0 (range check)
 #pragma unroll
@@ -386,7 +386,6 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
     const bool more = oc + 1 < OT;
     const int ocn = more ? oc + 1 : oc;
     load_dout(ocn);
-    load_b(ocn, bnext);
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       a0[st] = s_dout[buf][16 * h + st][l31];
@@ -401,11 +400,8 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data(
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[st], bcur[1][st], acc[1][1], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
+    load_b(ocn, bcur);   // L2-resident weights, in flight through the dout store and barrier
     if (more) store_dout(buf ^ 1);
-#pragma unroll
-    for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-      for (int st = 0; st < 16; ++st) bcur[ci][st] = bnext[ci][st];
     __syncthreads();
   }
   // epilogue: row m = 32 ri + (r&3) + 8 (r>>2) + 4 h, column c = cgb + 64 wv + 32 ci + l31
