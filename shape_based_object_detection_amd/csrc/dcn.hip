@@ -460,31 +460,40 @@ __global__ __launch_bounds__(256) void k_dcn_dx_gather(int C, int ntarget, const
   const int tp = xcd_logical(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (tp >= ntarget) return;
   const uint32_t e0 = __builtin_amdgcn_readfirstlane(toff[tp]), e1 = __builtin_amdgcn_readfirstlane(toff[tp + 1]);
-  for (int c0 = VEC * lane; c0 < C; c0 += 64 * VEC) {
+  for (int cb = 0; cb < C; cb += 64 * VEC) {   // uniform trip count: every lane loads entries
+    const int c0 = min(cb + VEC * lane, C - VEC);   // lanes past C read a valid column, store nothing
     float acc[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
-    uint32_t e = e0;
-    for (; e + 4 <= e1; e += 4) {   // four rows in flight
-      DxEnt d[4];
-      float x[4][VEC];
+    // entries 64 at a time, one per lane (one coalesced load), broadcast by readlane; eight dcols
+    // rows in flight; rows summed in entry order
+    for (uint32_t eb = e0; eb < e1; eb += 64) {
+      const int ne = static_cast<int>(min(e1 - eb, 64u));
+      const DxEnt mine = lane < ne ? ent[eb + lane] : DxEnt{0u, 0.f};
+      int k = 0;
+      for (; k + 8 <= ne; k += 8) {
+        float x[8][VEC], w[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        d[u] = ent[e + u];
-        load_vec<VEC>(dcols + static_cast<int64_t>(d[u].row) * C + c0, true, x[u]);
+        for (int u = 0; u < 8; ++u) {
+          const uint32_t row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mine.row), k + u));
+          w[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mine.w), k + u));
+          load_vec<VEC>(dcols + static_cast<int64_t>(row) * C + c0, true, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[v] += w[u] * x[u][v];
       }
+      for (; k < ne; ++k) {
+        const uint32_t row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mine.row), k));
+        const float w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mine.w), k));
+        float x[VEC];
+        load_vec<VEC>(dcols + static_cast<int64_t>(row) * C + c0, true, x);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) acc[v] += d[u].w * x[u][v];
+        for (int v = 0; v < VEC; ++v) acc[v] += w * x[v];
+      }
     }
-    for (; e < e1; ++e) {
-      const DxEnt d = ent[e];
-      float x[VEC];
-      load_vec<VEC>(dcols + static_cast<int64_t>(d.row) * C + c0, true, x);
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) acc[v] += d.w * x[v];
-    }
+    if (cb + VEC * lane >= C) continue;
     float *dst = gxt + static_cast<int64_t>(tp) * C + c0;
     if (VEC == 4)
       *reinterpret_cast<float4 *>(dst) = make_float4(acc[0], acc[1], acc[VEC > 2 ? 2 : 0], acc[VEC > 3 ? 3 : 0]);
