@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument('--eager', action='store_true', help='no hipGraph: launch every call each step')
     ap.add_argument('--one-stream', action='store_true',
                     help='graph mode: one graph per step (criterion and detect in stream order)')
+    ap.add_argument('--priority', choices=('none', 'detect', 'criterion'), default='criterion',
+                    help='graph mode: which of the two streams gets the high HIP stream priority')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-dcn', action='store_true')
     ap.add_argument('--cpu-detect-images', type=int, default=2)
@@ -192,7 +194,7 @@ def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
 class Step:
     """Criterion forward+backward and detect on one batch; eager or captured in a hipGraph."""
 
-    def __init__(self, dev, B, rank, world, graph, two_streams=True):
+    def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none'):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -210,12 +212,13 @@ class Step:
         # the warm-up runs on the capture stream, so every workspace the captured calls use
         # (cached per stream in core.workspace) already exists: nothing large is allocated
         # under capture
-        self.cap_stream = torch.cuda.Stream(dev)
+        # (priority: the stream whose graph gets the high HIP stream priority, if any)
+        self.cap_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'criterion' else 0)
         # graph mode: the criterion and detect are two graphs replayed on two streams, so their
         # kernels (several latency-bound, few workgroups) run concurrently on the GPU; a
         # fork/join INSIDE one graph costs ~30 us per edge on this runtime
         # (scripts/probe_graph_launch.py), two graphs on two streams need no edge at all
-        self.det_stream = torch.cuda.Stream(dev)
+        self.det_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'detect' else 0)
         self.two = two_streams
         self.graph = None
         self.use_graph = graph
@@ -440,7 +443,7 @@ def main():
     torch.cuda.set_device(dev)
     L.lib()
     B = a.batch
-    st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream)
+    st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing)
     with torch.no_grad():
@@ -544,7 +547,7 @@ def main():
         'step_algorithmic_bytes': step_bytes,
         'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        'graph': st.use_graph,
+        'graph': st.use_graph, 'stream_priority': a.priority,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }
