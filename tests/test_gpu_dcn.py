@@ -79,6 +79,7 @@ def _oracle_case(B, C, O, H, W, ks, pad, stride, modulation, off_scale, seed):
     (2, 7, 5, 8, 6, 3, 0, 1, True, 1.5),       # no zero padding
     (1, 6, 3, 9, 7, 3, 2, 1, False, 1.0),      # wider padding, no modulation
     (1, 4, 7, 8, 8, 5, 2, 1, True, 1.0),       # kernel 5
+    (1, 8, 16, 9, 9, 7, 3, 1, True, 1.0),      # kernel 7 (the forward's coefficient LDS > 64 KB)
     (1, 3, 4, 6, 6, 2, 1, 1, True, 0.7),       # even kernel
     (2, 6, 5, 7, 7, 3, 1, 1, True, 8.0),       # offsets far outside: border clamp everywhere
     (1, 64, 96, 13, 11, 3, 1, 1, True, 1.0),   # K, M, O not multiples of the tiles
