@@ -24,6 +24,9 @@ namespace sbod {
 SBOD_STAMP_DECL
 
 constexpr int kDTile = 256;
+#ifndef SBOD_PREP_GLDS
+#define SBOD_PREP_GLDS 1
+#endif
 __device__ const uint8_t kOneByte = 1;
 constexpr int kSegThreads = 256;
 constexpr int kMaxWindow = 4096;   // LDS-resident window (keys + boxes + areas + flags)
@@ -473,7 +476,27 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   const Box4 pr = a.box_type == SBOD_BOX_OFFSET ? ld4(a.priors + 4 * static_cast<int64_t>(valid ? p : p0))
                                                 : Box4{0.f, 0.f, 0.f, 0.f};
   const uint8_t posv = *(a.pos != nullptr ? a.pos + ic : &kOneByte);   // branch-free: no early wait
+#if SBOD_PREP_GLDS
+  if (CM > 0 && (reinterpret_cast<uintptr_t>(scores + rbase * C) & 15) == 0) {
+    // LDS-DMA: each wave-instruction copies 64 x 16 B of the tile straight into LDS (lane-linear,
+    // no VGPR round trip, no LDS write instructions); the tail floats go the ordinary way
+    const float4 *src4 = reinterpret_cast<const float4 *>(scores + rbase * C);
+    const int n = np * C, n4 = n >> 2, wv0 = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < (CM > 0 ? (CM + 3) / 4 : 1); ++k) {
+      const int q0 = k * kDTile + 64 * wv0;   // the wave's first float4 (uniform)
+      if (q0 + lane < n4)
+        __builtin_amdgcn_global_load_lds(src4 + q0 + lane,
+                                         (__attribute__((address_space(3))) void *)(reinterpret_cast<float4 *>(s_sc) + q0),
+                                         16, 0, 0);
+    }
+    for (int e = (n4 << 2) + tid; e < n; e += kDTile) s_sc[e] = scores[rbase * C + e];
+  } else {
+    tile_load_f32<(CM > 0 ? (CM + 3) / 4 : 8)>(s_sc, scores + rbase * C, np * C);
+  }
+#else
   tile_load_f32<(CM > 0 ? (CM + 3) / 4 : 8)>(s_sc, scores + rbase * C, np * C);
+#endif
   __syncthreads();
   SEG_PHASE(1);
   float *row = s_sc + tid * C;
