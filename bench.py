@@ -11,10 +11,16 @@ One step = one pass of the hot path over one batch of SSD512 synthetic input res
   3. detect on the same batch (softmax, offset decode + clamp, per-class NMS at IoU 0.45,
      min_score 0.01, top_k 200 — models.utils.detect's work) up to its per-image lists, which
      need one device->host sync.
-Steps 2-3 are captured once into a hipGraph (torch.cuda.graph over the same eager calls, one
-stream) and replayed every step.  Every kernel still runs every step; the graph removes the
-per-launch host work.  ``--eager`` runs the same calls without the graph; the line also carries
-the eager step time (measured before the capture).
+Steps 2-3 are captured into hipGraphs (criterion and detect, two streams) and replayed every
+step.  Every kernel still runs every step; the graph removes the per-launch host work.  ``--eager``
+runs the same calls without the graph; the line also carries the eager step time.
+
+Inputs come from HBM, not from the 256 MiB Infinity Cache (MI355X_MICROARCH.md, "Infinity
+Cache": FETCH_SIZE and kernel time both count its hits): the bench holds ``--batches`` (default
+6) distinct seeded SSD512 batches — each with its own ground truth, locs/scores and detect
+scores, and its own captured graphs and gradient buffers — and step k runs batch k mod 6.  One
+step touches ~100 MB, a full rotation ~600 MB, so every replay reads lines last touched 5 steps
+(~500 MB) earlier.
 
 Data parallel (``--gpus N``): one process per GPU.  Without WORLD_SIZE in the environment this
 script starts the N rank processes itself (subprocesses, before any GPU call); under
@@ -49,7 +55,6 @@ N_CLASSES = 21
 ARCH = 'SSD512'
 SSD512_PARAMS = 26450959   # SSD512 parameter count -> fp32 gradient elements
 BUCKET_MB = 25             # DDP's default bucket size
-TIMING_EVERY = 10          # one step in 10 carries the dominant kernel's timing
 
 
 class Cfg(dict):
@@ -69,18 +74,29 @@ def parse(argv=None):
                     help='graph mode: which of the two streams gets the high HIP stream priority')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-dcn', action='store_true')
-    ap.add_argument('--cpu-detect-images', type=int, default=2)
+    ap.add_argument('--batches', type=int, default=6,
+                    help='distinct resident batches rotated step by step (HBM, not cache, reads)')
+    ap.add_argument('--timing-steps', type=int, default=12,
+                    help='eager steps whose every kernel dispatch carries HIP events')
+    ap.add_argument('--no-c2', action='store_true', help='skip the config C2 bf16 B=16 figure')
     return ap.parse_args(argv)
 
 
-def make_batch(B, seed, dev):
-    P = prior_table(ARCH).shape[0]
-    boxes, labels = synth.make_gt(B, seed=seed, n_classes=N_CLASSES)
-    locs, scores = synth.make_preds(B, P, N_CLASSES, seed=seed)
-    det_scores = scores.clone()
-    det_scores[:, :, 0] += 6.0            # detection workload: +6 background logit (§8(d))
-    return ([b.to(dev) for b in boxes], [l.to(dev) for l in labels], locs.to(dev), scores.to(dev),
-            det_scores.to(dev))
+class Batch:
+    """One resident synthetic batch (SURVEY §8(d) recipe): per-image GT lists on the device,
+    locs/scores leaves (grad-enabled) in ``dtype``, and the detection workload's scores."""
+
+    def __init__(self, B, seed, dev, dtype=torch.float32):
+        P = prior_table(ARCH).shape[0]
+        boxes, labels = synth.make_gt(B, seed=seed, n_classes=N_CLASSES)
+        locs, scores = synth.make_preds(B, P, N_CLASSES, seed=seed)
+        det_scores = scores.clone()
+        det_scores[:, :, 0] += 6.0            # detection workload: +6 background logit (§8(d))
+        self.boxes = [b.to(dev) for b in boxes]
+        self.labels = [l.to(dev) for l in labels]
+        self.locs = locs.to(dev, dtype).requires_grad_(True)
+        self.scores = scores.to(dev, dtype).requires_grad_(True)
+        self.det_scores = det_scores.to(dev, dtype)
 
 
 def criterion_bytes(B, P, C):
@@ -123,21 +139,23 @@ def pmc_traffic(kernel):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(B, det_images, threads_all):
-    """The oracle (CPU restatement of the reference, pinned by tests/golden) on host cores: warm
-    median of MultiBoxLoss512 (DIoU+focal) fwd+bwd over the SAME B-image workload, plus detect on
-    a sample of `det_images` images (numpy greedy NMS, torchvision semantics), at all host threads
-    (capped at 16, the box's CPU share) and at 1 thread.  kind = 'port'."""
+def cpu_baseline(B, threads_all, det_images_one=8):
+    """The oracle (CPU restatement of the reference, pinned by tests/golden) on host cores, over
+    the SAME B-image workload as the GPU step: warm median of MultiBoxLoss512 (DIoU+focal)
+    fwd+bwd on the whole batch, plus detect (softmax, offset decode, numpy greedy NMS with
+    torchvision semantics, top-k) on every one of the B images, at all host threads (capped at
+    16, the box's CPU share).  The 1-thread figure times the criterion the same way and detect on
+    ``det_images_one`` images (the NMS is single-threaded numpy either way).  kind = 'port'."""
     from oracle import loss_ref as LR
     from oracle import match_ref as M
     Pn = prior_table(ARCH)
     P = torch.from_numpy(Pn)
     boxes, labels = synth.make_gt(B, seed=0, n_classes=N_CLASSES)
     locs, scores = synth.make_preds(B, Pn.shape[0], N_CLASSES, seed=0)
-    det = scores[:det_images].clone()
+    det = scores.clone()
     det[:, :, 0] += 6.0
     out = {}
-    for threads in (threads_all, 1):
+    for threads, n_det in ((threads_all, B), (1, min(det_images_one, B))):
         torch.set_num_threads(threads)
         crit = []
         for _ in range(3):      # first run warms the allocator / thread pool; median of the rest
@@ -147,21 +165,22 @@ def cpu_baseline(B, det_images, threads_all):
             crit.append(time.perf_counter() - t0)
         t_crit = sorted(crit[1:])[len(crit[1:]) // 2]
         t0 = time.perf_counter()
-        probs = torch.softmax(det, 2).numpy()
-        bx = M.decode_boxes(locs[:det_images].numpy(), Pn, 'offset')
+        probs = torch.softmax(det[:n_det], 2).numpy()
+        bx = M.decode_boxes(locs[:n_det].numpy(), Pn, 'offset')
         M.detect(probs, bx, 0.01, 0.45, 200)
         t_det = time.perf_counter() - t0
-        per_img = t_crit / B + t_det / det_images
-        out[threads] = (1.0 / per_img, t_crit, t_det)
+        per_img = t_crit / B + t_det / n_det
+        out[threads] = (1.0 / per_img, t_crit, t_det, n_det)
     torch.set_num_threads(threads_all)
-    v_all, c_all, d_all = out[threads_all]
-    v_one, c_one, d_one = out[1]
+    v_all, c_all, d_all, n_all = out[threads_all]
+    v_one, c_one, d_one, n_one = out[1]
     return {'value': round(v_all, 3), 'unit': 'images/s', 'cores': threads_all, 'kind': 'port',
             'sample': ('oracle MultiBoxLoss512 (DIoU+focal) fwd+bwd on the %d-image batch, warm median '
-                       'of 2: %.3f s; oracle detect on %d images: %.2f s; images/s = 1 / (criterion '
-                       's/img + detect s/img), %d host threads' % (B, c_all, det_images, d_all, threads_all)),
+                       'of 2: %.3f s; oracle detect on all %d images of it: %.2f s (%.3f s/image); '
+                       'images/s = 1 / (criterion s/img + detect s/img), %d host threads'
+                       % (B, c_all, n_all, d_all, d_all / n_all, threads_all)),
             'one_thread': {'value': round(v_one, 3), 'cores': 1, 'criterion_s': round(c_one, 4),
-                           'detect_s': round(d_one, 3)}}
+                           'detect_s': round(d_one, 3), 'detect_images': n_one}}
 
 
 # ----------------------------------------------------------------------------- DCN (config C4)
@@ -192,9 +211,15 @@ def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
 
 # ----------------------------------------------------------------------------- the step
 class Step:
-    """Criterion forward+backward and detect on one batch; eager or captured in a hipGraph."""
+    """Criterion forward+backward and detect on one batch; eager or captured in hipGraphs.
 
-    def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none'):
+    ``n_batches`` resident batches are rotated (step k uses batch k mod n): in graph mode each
+    batch has its own pair of graphs (criterion on ``cap_stream``, detect on ``det_stream``)
+    that own its gradients and detections, so consecutive steps never share an input or output
+    buffer and the two-deep pipeline (submit step k, then collect step k-1) needs no copies."""
+
+    def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
+                 dtype=torch.float32):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -203,93 +228,102 @@ class Step:
                        cls_loss='focal', focal_type='softmax', model={'box_type': 'offset'})
         self.crit = CR.MultiBoxLoss512(priors_cxcy=self.priors, config=self.cfg)
         self.crit.distributed = world > 1
-        self.boxes, self.labels, locs0, scores0, self.det_scores = make_batch(B, 1000 * rank, dev)
-        self.locs = locs0.clone().requires_grad_(True)
-        self.scores = scores0.clone().requires_grad_(True)
-        cap = max(int(b.shape[0]) for b in self.boxes)
+        self.batches = [Batch(B, 1000 * rank + 100 * i, dev, dtype) for i in range(max(1, n_batches))]
+        cap = max(int(b.shape[0]) for bt in self.batches for b in bt.boxes)
         self.capacity = max(16, (cap + 15) // 16 * 16)
         self.stage = core.GtStaging(B, self.capacity, dev)
-        # the warm-up runs on the capture stream, so every workspace the captured calls use
+        # the warm-up runs on the capture streams, so every workspace the captured calls use
         # (cached per stream in core.workspace) already exists: nothing large is allocated
-        # under capture
-        # (priority: the stream whose graph gets the high HIP stream priority, if any)
+        # under capture.  Graph mode: the criterion and detect are two graphs replayed on two
+        # streams, so their kernels (several latency-bound, few workgroups) run concurrently;
+        # a fork/join INSIDE one graph costs ~30 us per edge on this runtime
+        # (scripts/probe_graph_launch.py), two graphs on two streams need no edge at all.
         self.cap_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'criterion' else 0)
-        # graph mode: the criterion and detect are two graphs replayed on two streams, so their
-        # kernels (several latency-bound, few workgroups) run concurrently on the GPU; a
-        # fork/join INSIDE one graph costs ~30 us per edge on this runtime
-        # (scripts/probe_graph_launch.py), two graphs on two streams need no edge at all
         self.det_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'detect' else 0)
         self.two = two_streams
         self.graph = None
         self.use_graph = graph
         self.capture_error = None
         self.fast = None
+        self.k = 0
+        self.pending = None
+        self.host_submit = self.host_collect = 0.0
         # the read-only unit upstream gradient: no ones-fill and no scale launch in the step
         self.one = core.unit_grad(dev)
 
-    def body(self, gt, capture=False):
-        """The step's device work, in stream order on the current stream: criterion forward,
-        detect (kernels queued ahead of the backward, lists collected later), backward.  One
-        stream on purpose: a fork/join inside a graph costs ~30 us per edge on this runtime
-        (scripts/probe_graph_launch.py), more than the parallel branch would save."""
-        loss = self.crit(self.locs, self.scores, gt, None)
-        h = core.detect(self.locs.detach(), self.det_scores, 0.01, 0.45, 200, self.priors,
-                        box_type='offset', act='softmax', async_=True, capture=capture)
+    def _next_batch(self):
+        bt = self.batches[self.k % len(self.batches)]
+        self.k += 1
+        return bt
+
+    def detect(self, bt, capture):
+        return core.detect(bt.locs.detach(), bt.det_scores, 0.01, 0.45, 200, self.priors,
+                           box_type='offset', act='softmax', async_=True, capture=capture)
+
+    def body(self, bt, gt):
+        """One stream, in stream order: criterion forward, detect (lists collected later),
+        backward."""
+        loss = self.crit(bt.locs, bt.scores, gt, None)
+        h = self.detect(bt, False)
         loss.backward(self.one)
         return loss, h
 
     def launch_eager(self):
-        self.locs.grad = None
-        self.scores.grad = None
-        gt = self.stage.stage(self.boxes, self.labels)
-        return self.body(gt)
+        bt = self._next_batch()
+        bt.locs.grad = None
+        bt.scores.grad = None
+        gt = self.stage.stage(bt.boxes, bt.labels)
+        return self.body(bt, gt)
 
     def eager(self):
         loss, h = self.launch_eager()
         return loss, h.wait()
 
     def eager_split(self):
-        """The two-stream form eagerly (warms both capture streams' workspaces): GT packing,
-        criterion forward and backward on cap_stream, detect on det_stream."""
-        self.locs.grad = None
-        self.scores.grad = None
+        """The two-stream form eagerly (also warms both capture streams' workspaces): GT
+        packing, criterion forward and backward on cap_stream, detect on det_stream."""
+        bt = self._next_batch()
+        bt.locs.grad = None
+        bt.scores.grad = None
+        self.cap_stream.wait_stream(torch.cuda.current_stream(self.dev))
+        self.det_stream.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(self.cap_stream):
-            gt = self.stage.stage(self.boxes, self.labels)
-            loss = self.crit(self.locs, self.scores, gt, None)
+            gt = self.stage.stage(bt.boxes, bt.labels)
+            loss = self.crit(bt.locs, bt.scores, gt, None)
         with torch.cuda.stream(self.det_stream):
-            h = self.detect(False)
+            h = self.detect(bt, False)
         with torch.cuda.stream(self.cap_stream):
             loss.backward(self.one)
-        return loss, h.wait()
+        out = loss, h.wait()
+        torch.cuda.current_stream(self.dev).wait_stream(self.cap_stream)
+        return out
 
-    def detect(self, capture):
-        return core.detect(self.locs.detach(), self.det_scores, 0.01, 0.45, 200, self.priors,
-                           box_type='offset', act='softmax', async_=True, capture=capture)
-
-    def capture(self, n=2, after_first=None):
-        """Capture body() into ``n`` hipGraphs (the usual torch pattern: warm-up already done on
-        the capture stream; gradients set to None so the captured backward owns them).  Each
-        graph owns its outputs (loss, gradients, detections, pinned counts), so step k+1 can run
-        while the host collects step k's detections (``pipelined``)."""
-        gt = self.stage.stage(self.boxes, self.labels)
+    def capture(self, after_first=None):
+        """Capture one graph pair per resident batch (the usual torch pattern: warm-up already
+        done on the capture streams; gradients set to None so the captured backward owns
+        them).  ``after_first`` runs after the first batch's capture."""
+        gt = self.stage.stage(self.batches[0].boxes, self.batches[0].labels)
+        n = len(self.batches)
         core.reserve_count_slots(self.dev, self.B, n)
         torch.cuda.synchronize()
         self.slots = []
-        for _ in range(n):
-            self.locs.grad = None
-            self.scores.grad = None
+        for bt in self.batches:
+            bt.locs.grad = None
+            bt.scores.grad = None
             if self.two:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga, stream=self.cap_stream):
-                    loss = self.crit(self.locs, self.scores, gt, None)
+                    loss = self.crit(bt.locs, bt.scores, gt, None)
                     loss.backward(self.one)
                 with torch.cuda.graph(gb, stream=self.det_stream):
-                    h = self.detect(True)
+                    h = self.detect(bt, True)
                 self.slots.append((ga, gb, loss, h))
             else:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=self.cap_stream):
-                    loss, h = self.body(gt, capture=True)
+                    loss = self.crit(bt.locs, bt.scores, gt, None)
+                    h = self.detect(bt, True)
+                    loss.backward(self.one)
                 self.slots.append((g, None, loss, h))
             if after_first is not None and len(self.slots) == 1:
                 after_first()
@@ -310,18 +344,19 @@ class Step:
 
     def launch_replay(self):
         i = self.k % len(self.slots)
+        bt = self._next_batch()
         ga, gb, loss, h = self.slots[i]
-        self.k += 1
         if self.fast is not None:
             launches, ev, ev_stream = self.fast[i]
-            if self.stage.stage_and_replay(self.boxes, self.labels, launches, ev, ev_stream) is not None:
+            if self.stage.stage_and_replay(bt.boxes, bt.labels, launches, ev, ev_stream) is not None:
                 return loss, h.rearmed()
         if gb is None:
-            self.stage.stage(self.boxes, self.labels)
-            ga.replay()
-            return loss, h.replayed()
+            with torch.cuda.stream(self.cap_stream):
+                self.stage.stage(bt.boxes, bt.labels)
+                ga.replay()
+                return loss, h.replayed(self.cap_stream)
         with torch.cuda.stream(self.cap_stream):
-            self.stage.stage(self.boxes, self.labels)
+            self.stage.stage(bt.boxes, bt.labels)
             ga.replay()
         with torch.cuda.stream(self.det_stream):
             gb.replay()
@@ -332,7 +367,7 @@ class Step:
         return loss, h.wait()
 
     def pipelined(self):
-        """One step, pipelined two deep: launch step k (GT packing + graph replay), then collect
+        """One step, pipelined two deep: launch step k (GT packing + graph replays), then collect
         step k-1's per-image detection lists (its host sync overlaps step k on the GPU)."""
         t0 = time.perf_counter()
         nxt = self.launch_replay()
@@ -352,11 +387,32 @@ class Step:
             return prev[0], prev[1].wait()
         return None
 
-    def launch(self):
-        return self.launch_replay() if self.graph is not None else self.launch_eager()
-
     def __call__(self):
         return self.replay() if self.graph is not None else self.eager()
+
+
+def c2_figure(dev, steps, warmup, B=16, n_batches=12):
+    """Config C2 (SSD512 batch=16 bf16 on 1 GPU): the same captured step with bf16 locs / scores
+    (and bf16 gradients) for the criterion, and the detect on the bf16 activations (widened to
+    fp32 inside the graph, as detect's fp32 kernels take them).  ``n_batches`` resident batches
+    (~23 MB touched per step) keep the rotation above the Infinity Cache.  Algorithmic bytes of
+    the criterion at 2 B/element: SURVEY §8(d) (16.56 MB at B=16)."""
+    st = Step(dev, B, 0, 1, graph=True, n_batches=n_batches, dtype=torch.bfloat16)
+    for _ in range(max(warmup - 1, 1)):
+        st.eager_split()
+    torch.cuda.synchronize()
+    st.capture()
+    for _ in range(len(st.slots) + 1):
+        st.replay()
+    el = timed(st.pipelined, steps, None, dev, finish=st.drain)
+    ms = el / steps * 1e3
+    crit_b = B * st.P * 2 * (4 + N_CLASSES) * 2 + 16 * st.P
+    del st
+    torch.cuda.synchronize()
+    return {'config': 'C2 SSD512 batch=%d bf16: MultiBoxLoss512(DIoU+focal) fwd+bwd in bf16 + detect '
+                      '(bf16 activations widened to fp32), captured, %d resident batches' % (B, n_batches),
+            'ms_per_step': round(ms, 4), 'images_per_s': round(B / (ms * 1e-3), 1),
+            'criterion_algorithmic_bytes': crit_b, 'steps': steps}
 
 
 def timed(fn, steps, dist, dev, per_step=None, finish=None):
@@ -443,53 +499,58 @@ def main():
     torch.cuda.set_device(dev)
     L.lib()
     B = a.batch
-    st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority)
+    st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
+              n_batches=a.batches)
     P = st.P
-    # workload constants for the algorithmic byte counts (computed before any timing)
+    # workload constants for the algorithmic byte counts (computed before any timing; the
+    # candidate count is averaged over the resident batches)
     with torch.no_grad():
-        n_cand = int((torch.softmax(st.det_scores, 2)[:, :, 1:] > 0.01).sum().item())
+        n_cand = sum(int((torch.softmax(bt.det_scores, 2)[:, :, 1:] > 0.01).sum().item())
+                     for bt in st.batches) // len(st.batches)
     wl = {'B': B, 'P': P, 'C': N_CLASSES, 'n_cand': n_cand}
 
-    # warm-up on the capture stream (lazy init of autograd / allocator state, and the per-stream
-    # workspaces the captured calls will use)
-    side = st.cap_stream
-    side.wait_stream(torch.cuda.current_stream(dev))
-    st.det_stream.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(side):
-        for _ in range(max(a.warmup - 1, 1)):
-            if st.use_graph and st.two:
-                st.eager_split()
-            else:
-                st.eager()
+    # warm-up on the capture streams (lazy init of autograd / allocator state, and the
+    # per-stream workspaces the captured calls will use)
+    for _ in range(max(a.warmup - 1, 1)):
+        st.eager_split()
     torch.cuda.synchronize()
-    # one more eager step with every instrumented kernel carrying HIP events on its dispatch:
-    # the per-kernel table, and the dominant HBM-bound kernel that is timed live below
-    torch.cuda.synchronize()
+
+    # Kernel durations: eager two-stream steps over the rotating batches with HIP events attached
+    # to EVERY instrumented dispatch on its own launch stream (hipExtLaunchKernel start/stop
+    # events: the runtime stamps the dispatch's begin and end, as rocprofv3's kernel trace does).
+    # The dominant HBM-bound kernel's average over these launches is the roofline's duration.
     L.timing_enable('*')
-    st.eager()
+    for _ in range(max(a.timing_steps, 10)):
+        st.eager_split()
     torch.cuda.synchronize()
-    kernel_us = {}
+    kernel_us, kernel_n = {}, {}
     for k in ALL_KERNELS:
         n, ms = L.timing_query(k)
         if n:
-            kernel_us[k] = round(ms * 1e3, 1)
-    dominant = max(HBM_KERNELS, key=lambda k: kernel_us.get(k, 0.0))
+            kernel_us[k] = round(ms * 1e3 / n * (n / max(a.timing_steps, 10)), 2)   # per step
+            kernel_n[k] = n
     L.timing_enable(None)
+    dominant = max(HBM_KERNELS, key=lambda k: kernel_us.get(k, 0.0))
+    L.timing_enable(dominant)
+    for _ in range(max(a.timing_steps, 10)):
+        st.eager_split()
+    torch.cuda.synchronize()
+    n_dom, ms_dom = L.timing_query(dominant)
+    L.timing_enable(None)
+    dom_avg_s = ms_dom / n_dom * 1e-3 if n_dom else float('nan')
 
     eager_ms = None
     if st.use_graph:        # the same step without the graph, for the host-overhead comparison
         n_e = min(a.steps, 20)
         eager_ms = timed(st.eager, n_e, dist, dev) / n_e * 1e3
 
-    samples = []
+    spans = []
     if st.use_graph:
-        # the dominant kernel is captured with a device span record it overwrites itself on every
-        # replay (first workgroup start -> last workgroup end, stores acknowledged); one replay
-        # in TIMING_EVERY is read back afterwards (a small host-synchronous copy)
+        # every batch's graph carries a device span record for the dominant kernel (first
+        # workgroup start -> last workgroup end, s_memrealtime), read after the timed region
         L.timing_enable(dominant)
         try:
-            # only the first graph carries the span record (steps 0, 2, 4, ... replay it)
-            st.capture(after_first=lambda: L.timing_enable(None))
+            st.capture()
         except Exception as ex:   # noqa: BLE001 — fall back to eager launches, say so in the line
             st.graph = None
             st.use_graph = False
@@ -497,30 +558,22 @@ def main():
             torch.cuda.synchronize()
         L.timing_enable(None)
     if st.use_graph:
-        for _ in range(3):
-            st()
-        count = [0]
-
-        def graph_step():
-            k = count[0]
-            count[0] += 1
-            out = st.pipelined()
-            if k % TIMING_EVERY == 1:   # step k-1 (graph 0) is complete, graph 1 is running
-                n, ms = L.timing_query(dominant)
-                if n:
-                    samples.append(ms / n)
-            return out
+        for _ in range(len(st.slots) + 1):
+            st.replay()
         st.host_submit = st.host_collect = 0.0
-        elapsed = timed(graph_step, a.steps, dist, dev, finish=st.drain)
+        elapsed = timed(st.pipelined, a.steps, dist, dev, finish=st.drain)
         host_submit, host_collect = st.host_submit, st.host_collect
+        # the in-graph span of the dominant kernel (a host-synchronous read, so outside the
+        # timed region): each batch's graph keeps the record of its latest replay, so after
+        # every full rotation the query returns len(slots) distinct launches
+        for _ in range(max(2, -(-12 // len(st.slots)))):
+            for _ in range(len(st.slots)):
+                st.replay()
+            torch.cuda.synchronize()
+            n, ms = L.timing_query(dominant)
+            spans += [ms / n] * n if n else []
     else:
-        L.call('sbod_timing_every', TIMING_EVERY)
-        L.timing_enable(dominant)
         elapsed = timed(st, a.steps, dist, dev)
-        n, ms = L.timing_query(dominant)
-        samples = [ms / n] * n if n else []
-        L.timing_enable(None)
-        L.call('sbod_timing_every', 1)
     ms_step = elapsed / a.steps * 1e3
 
     dp = grad_allreduce_figure(st.replay if st.use_graph else st.eager, a, dist, dev, world) if dist else None
@@ -551,30 +604,44 @@ def main():
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }
-    avg_s = (sum(samples) / len(samples) * 1e-3) if samples else float('nan')
     algo = ALGO_BYTES[dominant](wl)
-    achieved = algo / avg_s / 1e9
+    achieved = algo / dom_avg_s / 1e9
     line['roofline'] = {
         'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(dominant),
-        'kernel': dominant, 'launches_timed': len(samples), 'avg_us': round(avg_s * 1e6, 2),
-        'timing': ('device span stamped by the kernel in the graph (first workgroup start to last '
-                   'workgroup end, s_memrealtime), one replay in %d' % TIMING_EVERY
-                   if st.use_graph else 'HIP events on the dispatch, one launch in %d' % TIMING_EVERY),
+        'kernel': dominant, 'launches_timed': n_dom, 'avg_us': round(dom_avg_s * 1e6, 2),
+        'timing': ('HIP start/stop events attached to each dispatch (hipExtLaunchKernel) on its '
+                   'launch stream, %d eager two-stream steps rotating %d HBM-resident batches'
+                   % (max(a.timing_steps, 10), len(st.batches))),
         'algorithmic_bytes_per_launch': algo,
     }
-    if st.use_graph:
-        line['roofline']['span_clock_hz'] = L.lib().sbod_timing_clock_hz()
+    if spans:
+        sp = sum(spans) / len(spans)
+        line['roofline']['graph_span'] = {
+            'avg_us': round(sp * 1e3, 2), 'samples': len(spans),
+            'frac': round(algo / (sp * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            'timing': 'in the replayed graph: first workgroup start to last workgroup end '
+                      '(s_memrealtime), excludes the dispatch ramp and the end-of-kernel release',
+            'clock_hz': L.lib().sbod_timing_clock_hz()}
     line['kernel_us_per_step'] = kernel_us
+    line['kernel_launches_timed'] = kernel_n
+    line['resident_batches'] = len(st.batches)
     if st.use_graph:   # host time per step: GT packing + replays, and collecting the lists
         line['host_us_per_step'] = {'submit': round(host_submit / a.steps * 1e6, 1),
                                     'collect_incl_wait': round(host_collect / a.steps * 1e6, 1)}
     if dp is not None:
         line['dp_train_step_with_grad_allreduce'] = dp
+    if not a.no_c2 and world == 1:
+        line['c2_bf16'] = c2_figure(dev, a.steps, a.warmup)
     if not a.no_dcn:
-        line['dcn'] = dcn_figure(dev)
+        maps = [dcn_figure(dev, H=h, iters=5 if h >= 32 else 20) for h in (64, 32, 16, 8)]
+        tot_ms = sum(m['ms'] for m in maps)
+        tot_tf = sum(3 * 2.0 * 16 * h * h * 256 * 256 * 9 for h in (64, 32, 16, 8)) / tot_ms / 1e9
+        line['dcn'] = dict(maps[0], maps={str(h): m for h, m in zip((64, 32, 16, 8), maps)},
+                           c4_all_maps={'ms': round(tot_ms, 3), 'tflops': round(tot_tf, 2),
+                                        'mfma_frac': round(tot_tf / F32_MFMA_PEAK_TFS, 4)})
     if not a.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(B, a.cpu_detect_images, min(os.cpu_count() or 1, 16))
+        line['cpu_baseline'] = cpu_baseline(B, min(os.cpu_count() or 1, 16))
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -7,13 +7,14 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-run}; shift
 LIBD=$PWD/shape_based_object_detection_amd/lib
+VARD=$PWD/variants
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_dcn.py -q -x --timeout 120 --timeout-method thread \
     > gpurun_out/dcntests_$TAG.log 2>&1 || { echo "EXIT tests"; exit 1; }
 run() { echo "$1" >> gpurun_out/dcnab_$TAG.json; SBOD_LIB=$1 timeout -k 10 120 python scripts/dcn_bench.py --sizes 64 \
     >> gpurun_out/dcnab_$TAG.json 2>> gpurun_out/dcnab_$TAG.err; }
 for round in 1 2; do
-  for v in "$@"; do run $LIBD/libsbod_hip_$v.so || { echo "EXIT ab"; exit 1; }; done
+  for v in "$@"; do run $VARD/libsbod_hip_$v.so || { echo "EXIT ab"; exit 1; }; done
   run $LIBD/libsbod_hip.so || { echo "EXIT ab"; exit 1; }
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dprof_$TAG -o run --output-format csv -- \

@@ -102,6 +102,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise SbodError('libsbod_hip.so not found at %s — build it with '
                             '`python -m shape_based_object_detection_amd.build`' % LIB_PATH)
+        check_stamp()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             try:
@@ -114,6 +115,20 @@ def lib():
         _lib = L
         _load_fast()
     return _lib
+
+
+def check_stamp():
+    """Refuse a library that was not built from the sources in this tree: build.py records the
+    sha256 of the sources, flags and arch in lib/build_stamp.json, and it must match what the
+    tree holds now.  (An explicit SBOD_LIB — a diagnostic or A/B variant — is not checked.)"""
+    if 'SBOD_LIB' in os.environ:
+        return
+    from . import build as B
+    have, want = B.read_stamp(), B.source_digest()
+    if have != want:
+        raise SbodError('libsbod_hip.so in %s was built from other sources (stamp %s, tree %s): '
+                        'rebuild with `python -m shape_based_object_detection_amd.build`'
+                        % (os.path.dirname(LIB_PATH), (have or 'missing')[:12], want[:12]))
 
 
 def _load_fast():

@@ -14,6 +14,7 @@ call on the host, which is most of the hot path's step time at SSD512 B=32).
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import json
 import os
 import re
@@ -44,11 +45,60 @@ def _deps():
     return glob.glob(os.path.join(CSRC, '*.h')) + glob.glob(os.path.join(INCLUDE, '*.h'))
 
 
-def _stale(target, sources):
-    if not os.path.exists(target):
+STAMP = os.path.join(PKG, 'lib', 'build_stamp.json')
+
+
+def _digest(paths, extra=()):
+    """sha256 over the CONTENT of ``paths`` (+ ``extra`` strings): staleness is decided by what the
+    sources say, never by file times (a checkout or a copy to the GPU box changes mtimes, not
+    content)."""
+    h = hashlib.sha256()
+    for p in sorted(paths):
+        h.update(os.path.relpath(p, REPO).encode() + b'\0')
+        with open(p, 'rb') as f:
+            h.update(f.read())
+        h.update(b'\0')
+    for e in extra:
+        h.update(str(e).encode() + b'\0')
+    return h.hexdigest()
+
+
+def source_files():
+    """Every file the built libraries are made from."""
+    return (sorted(glob.glob(os.path.join(CSRC, '*.hip'))) + [HOSTPACK_SRC] + _deps()
+            + [os.path.join(PKG, '_lib.py')])
+
+
+def source_digest():
+    """Digest of the sources, the compile flags and the target arch: ``lib/build_stamp.json``
+    records it after a successful build, and ``_lib.lib()`` refuses a library whose stamp differs
+    (the box must run exactly the committed sources)."""
+    return _digest(source_files(), [ARCH] + CXXFLAGS)
+
+
+def read_stamp():
+    try:
+        with open(STAMP) as f:
+            return json.load(f).get('digest')
+    except (OSError, ValueError):
+        return None
+
+
+def _key_path(target):
+    return target + '.sha256'
+
+
+def _stale(target, key):
+    """True unless ``target`` exists and was built from inputs whose digest is ``key``."""
+    if not os.path.exists(target) or not os.path.exists(_key_path(target)):
         return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(s) > t for s in sources)
+    with open(_key_path(target)) as f:
+        return f.read().strip() != key
+
+
+def _mark(target, key):
+    with open(_key_path(target), 'w') as f:
+        f.write(key + '\n')
 
 
 _RES_RE = re.compile(r'remark: +(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|'
@@ -70,13 +120,15 @@ def _resource_usage(stderr):
 def _compile(src, force):
     obj = os.path.join(OBJDIR, os.path.basename(src) + '.o')
     res = obj + '.resources.json'
-    if force or _stale(obj, [src] + _deps()) or not os.path.exists(res):
+    key = _digest([src] + _deps(), [ARCH] + CXXFLAGS)
+    if force or _stale(obj, key) or not os.path.exists(res):
         cmd = [hipcc()] + CXXFLAGS + ['-Rpass-analysis=kernel-resource-usage', '-c', src, '-o', obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError('hipcc failed for %s:\n%s\n%s' % (src, ' '.join(cmd), r.stderr))
         with open(res, 'w') as f:
             json.dump(_resource_usage(r.stderr), f, indent=1, sort_keys=True)
+        _mark(obj, key)
     return obj
 
 
@@ -93,15 +145,20 @@ def build(force=False, jobs=8, verbose=True):
             usage.update(json.load(f))
     with open(RESOURCES, 'w') as f:     # kernel resource table (tests assert no scratch use)
         json.dump(usage, f, indent=1, sort_keys=True)
-    if force or _stale(LIB, objs):
+    lib_key = _digest([o + '.sha256' for o in objs], [ARCH])
+    if force or _stale(LIB, lib_key):
         cmd = [hipcc(), '-shared', '-fPIC', '--offload-arch=' + ARCH, '-o', LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError('link failed:\n%s\n%s' % (' '.join(cmd), r.stderr))
+        _mark(LIB, lib_key)
         if verbose:
             print('built', LIB)
     build_fastcall(force=force, verbose=verbose)
     build_hostpack(force=force, verbose=verbose)
+    with open(STAMP, 'w') as f:
+        json.dump({'digest': source_digest(), 'arch': ARCH,
+                   'sources': [os.path.relpath(p, REPO) for p in source_files()]}, f, indent=1)
     return LIB
 
 
@@ -171,7 +228,8 @@ def build_fastcall(force=False, verbose=True):
     if old != src:
         with open(FASTCALL_SRC, 'w') as f:
             f.write(src)
-    if force or old != src or _stale(FASTCALL_LIB, [FASTCALL_SRC, LIB] + _deps()):
+    key = _digest([FASTCALL_SRC, _key_path(LIB)] + _deps())
+    if force or _stale(FASTCALL_LIB, key):
         cc = shutil.which('gcc') or 'cc'
         cmd = [cc, '-O2', '-shared', '-fPIC', '-Wall', '-Werror', '-I', sysconfig.get_paths()['include'],
                '-I', INCLUDE, FASTCALL_SRC, '-o', FASTCALL_LIB, '-L', os.path.dirname(LIB), '-lsbod_hip',
@@ -179,6 +237,7 @@ def build_fastcall(force=False, verbose=True):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError('fastcall build failed:\n%s\n%s' % (' '.join(cmd), r.stderr))
+        _mark(FASTCALL_LIB, key)
         if verbose:
             print('built', FASTCALL_LIB)
     return FASTCALL_LIB
@@ -194,7 +253,8 @@ def build_hostpack(force=False, verbose=True):
     import sysconfig
     import torch
     tdir = os.path.dirname(torch.__file__)
-    if force or _stale(HOSTPACK_LIB, [HOSTPACK_SRC, LIB] + _deps()):
+    key = _digest([HOSTPACK_SRC, _key_path(LIB)] + _deps(), [torch.__version__])
+    if force or _stale(HOSTPACK_LIB, key):
         cxx = shutil.which('g++') or 'c++'
         abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
         tlib = os.path.join(tdir, 'lib')
@@ -209,6 +269,7 @@ def build_hostpack(force=False, verbose=True):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError('hostpack build failed:\n%s\n%s' % (' '.join(cmd), r.stderr))
+        _mark(HOSTPACK_LIB, key)
         if verbose:
             print('built', HOSTPACK_LIB)
     return HOSTPACK_LIB

@@ -466,7 +466,7 @@ class DetectHandle:
     it again (event behind the replay, fresh result lists)."""
 
     __slots__ = ('_args', '_out', '_cnt_host', '_event', '_full', '_res', '_window', '_launch',
-                 '_slot_key', '_persistent')
+                 '_slot_key', '_persistent', '_stream')
 
     def __init__(self, args, out, cnt_host, event, full, window, persistent=False):
         self._args, self._out, self._cnt_host, self._event = args, out, cnt_host, event
@@ -497,15 +497,20 @@ class DetectHandle:
         if not self._persistent:
             _COUNT_SLOTS.setdefault(self._slot_key, []).append((self._cnt_host, self._event))
         if min(counts) < 0:   # rare: some image needs a wider candidate window (exactness)
-            _detect_launch(*self._launch_args(4096))
-            counts = cnt.cpu().tolist()
-            if min(counts) < 0:
-                # a class whose survivors a 4,096-candidate window cannot bound (thousands of
-                # near-duplicates): chunked greedy NMS over all of its candidates
-                _detect_launch(*self._launch_args(-1))
+            # The retry reuses the launch's workspace (cached per launch stream), so it runs on
+            # THAT stream: a later detect already queued there (pipelined graph replays share
+            # the workspace) finishes first and leaves the counters zero, and the retry cannot
+            # overlap it.  cnt.cpu() then waits for the retry in that stream's order.
+            with torch.cuda.stream(self._stream):
+                _detect_launch(*self._launch_args(4096))
                 counts = cnt.cpu().tolist()
                 if min(counts) < 0:
-                    raise L.SbodError('detect: internal error, the exhaustive pass left an image undecided')
+                    # a class whose survivors a 4,096-candidate window cannot bound (thousands of
+                    # near-duplicates): chunked greedy NMS over all of its candidates
+                    _detect_launch(*self._launch_args(-1))
+                    counts = cnt.cpu().tolist()
+            if min(counts) < 0:
+                raise L.SbodError('detect: internal error, the exhaustive pass left an image undecided')
         if in_place and lc is not locs:
             locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
         if min(counts) == top_k:     # every image full (the usual eval case)
@@ -565,6 +570,9 @@ def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overl
     out_b, out_l, out_s, cnt = out
     need = L.lib().sbod_detect_counter_bytes(B, C)
     flags = _zeroed_flag(ws, need, L.DETECT_COUNTERS_ZEROED, 'detect')
+    # a call that fails part-way can leave its counters non-zero (k_det_prepare has added to
+    # them, k_det_merge never ran): the workspace counts as clean again only after a success
+    _CLEAN.pop(ws.data_ptr(), None)
     L.call('sbod_detect_f32', L.ptr(lc), L.ptr(sc), B, P, C, L.ptr(pri), L.ptr(pm), L.BOX[box_type],
            L.ACT[act], float(min_score), float(max_overlap), int(top_k), fn, int(window), flags,
            L.ptr(out_b), L.ptr(out_l), L.ptr(out_s), L.ptr(cnt), L.ptr(cnt_host), L.ptr(dbg[0]),
@@ -627,6 +635,7 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
                      cnt_host, ev, full, window, persistent=capture)
     h._launch = launch
     h._slot_key = (dev, B)
+    h._stream = torch.cuda.current_stream(dev)   # the stream whose workspace the launch used
     return h if (async_ or capture) else h.wait()
 
 

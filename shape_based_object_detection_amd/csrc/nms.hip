@@ -2096,6 +2096,11 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   const size_t tools_fast = static_cast<size_t>(kMatrixMax) * 25 + 16 + static_cast<size_t>(kMatrixMax) * (kMatrixMax / 64) * 8;
   const size_t merge_lds = head + static_cast<size_t>(kMergeStage) * 4 +
                            (final_nms >= 0.f ? (tools_general > tools_fast ? tools_general : tools_fast) : 0);
+  // every argument / LDS check comes before the first launch: k_det_prepare adds to the
+  // candidate counters that only k_det_merge clears again, so a call must not stop in between
+  const size_t all_lds = static_cast<size_t>(w2) * (8 + 16 + 4);
+  SBOD_REQUIRE(!exhaustive || ((w2 >= top_k || w2 >= P) && all_lds <= 64 * 1024),
+               "sbod_detect_f32: exhaustive mode supports top_k <= 2047");
   hipStream_t s = as_stream(stream);
   if ((flags & SBOD_DETECT_COUNTERS_ZEROED) == 0 &&
       hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4, s) != hipSuccess)
@@ -2118,11 +2123,8 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
   if (exhaustive) {
-    const size_t al = static_cast<size_t>(w2) * (8 + 16 + 4);
-    SBOD_REQUIRE((w2 >= top_k || w2 >= P) && al <= 64 * 1024,
-                 "sbod_detect_f32: exhaustive mode supports top_k <= 2047");
     KernelTimer kt("k_det_segment", s, true);
-    tlaunch(kt, k_det_segment_all, dim3(C - 1, B), dim3(kAllThreads), al, s, ws.cand, ws.count, ws.boxes, P, C,
+    tlaunch(kt, k_det_segment_all, dim3(C - 1, B), dim3(kAllThreads), all_lds, s, ws.cand, ws.count, ws.boxes, P, C,
             w2, top_k, max_overlap, so);
   } else {
     KernelTimer kt("k_det_segment", s, true);

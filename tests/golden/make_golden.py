@@ -618,19 +618,89 @@ def gen_map(R):
     save('map.npz', d)
 
 
+def gen_transforms(R):
+    """dataset/transforms.py:292-383 (``transform``) run by the reference itself on small PIL
+    images.  torchvision's functional ops are absent: the stub ``FT`` module gets PIL/torch
+    versions of hflip / resize / to_tensor / to_pil_image / normalize (test harness, pixel values
+    not pinned) and RECORDERS for the four colour ops (identity on the image, logging the op name
+    and factor).  Pinned: output boxes and labels (the reference's own box arithmetic, incl.
+    random_crop's find_jaccard_overlap), the colour-op call sequence, and the number of draws
+    taken from ``random`` (the next ``random.random()`` after each call)."""
+    import random
+    from PIL import Image
+    FT = R.transforms.FT
+    calls = []
+    names = ['adjust_brightness', 'adjust_contrast', 'adjust_saturation', 'adjust_hue']
+
+    def recorder(name):
+        def f(img, factor):
+            calls.append((names.index(name), factor))
+            return img
+        f.__name__ = sys.intern(name)
+        return f
+    FT.adjust_brightness, FT.adjust_contrast, FT.adjust_saturation, FT.adjust_hue = \
+        [recorder(n) for n in names]
+    FT.to_tensor = lambda pic: torch.from_numpy(
+        np.asarray(pic, dtype=np.uint8).astype(np.float32) / 255.0).permute(2, 0, 1).contiguous()
+    FT.to_pil_image = lambda t: Image.fromarray(
+        t.mul(255).byte().permute(1, 2, 0).contiguous().numpy(), mode='RGB')
+    FT.hflip = lambda img: img.transpose(Image.FLIP_LEFT_RIGHT)
+    FT.resize = lambda img, dims: img.resize((dims[1], dims[0]), Image.BILINEAR)
+    FT.normalize = lambda t, mean, std: (t - torch.tensor(mean).view(3, 1, 1)) / torch.tensor(std).view(3, 1, 1)
+
+    d = {}
+    cases = []
+    for k in range(40):
+        split = 'TRAIN' if k < 36 else ('TEST' if k < 38 else 'VAL')
+        ops = [['expand', 'random_crop'], ['random_crop'], ['expand'], []][k % 4]
+        cases.append((k, split, ops))
+    rs = np.random.RandomState(11)
+    for k, split, ops in cases:
+        h, w = int(rs.randint(24, 64)), int(rs.randint(24, 64))
+        g = int(rs.randint(1, 7))
+        x1 = rs.uniform(0, w - 6, g)
+        y1 = rs.uniform(0, h - 6, g)
+        x2 = np.minimum(x1 + rs.uniform(2, w / 2, g), w - 1)
+        y2 = np.minimum(y1 + rs.uniform(2, h / 2, g), h - 1)
+        boxes = torch.tensor(np.stack([x1, y1, x2, y2], 1), dtype=torch.float32)
+        labels = torch.tensor(rs.randint(1, 21, g), dtype=torch.int64)
+        img = Image.fromarray(rs.randint(0, 256, (h, w, 3), dtype=np.uint8), mode='RGB')
+        cfg = Cfg(model={'operation_list': ops, 'return_percent_coords': k % 5 != 4})
+        pre = 't%d_' % k
+        d[pre + 'in_boxes'] = f32(boxes)
+        d[pre + 'in_labels'] = i64(labels)
+        d[pre + 'image'] = np.asarray(img, dtype=np.uint8)
+        d[pre + 'meta'] = np.array([k, ['TRAIN', 'TEST', 'VAL'].index(split), k % 4, int(k % 5 != 4),
+                                    32, 40], dtype=np.int64)
+        calls.clear()
+        random.seed(1000 + k)
+        out_img, out_b, out_l = R.transforms.transform(img, boxes.clone(), labels.clone(), split=split,
+                                                       resize_dim=(32, 40), config=cfg)
+        d[pre + 'next_random'] = np.float64(random.random())
+        d[pre + 'out_boxes'] = f32(out_b)
+        d[pre + 'out_labels'] = i64(out_l)
+        d[pre + 'out_shape'] = np.array(out_img.shape, dtype=np.int64)
+        d[pre + 'calls'] = np.array([c[0] for c in calls], dtype=np.int64)
+        d[pre + 'factors'] = np.array([c[1] for c in calls], dtype=np.float64)
+    d['n_cases'] = np.int64(len(cases))
+    d['op_lists'] = np.array(['expand,random_crop', 'random_crop', 'expand', ''])
+    save('transforms.npz', d)
+
+
 def main(only=None):
     """Regenerate every fixture, or only the named generators (e.g. ``make_golden.py map``)."""
     torch.set_num_threads(8)
     R = load_reference()
     gens = ['jaccard', 'match', 'iou_utils_match', 'codecs', 'losses', 'criteria', 'nms', 'detect',
-            'dcn', 'map']
+            'dcn', 'map', 'transforms']
     todo = set(only or gens)
-    priors = gen_priors(R) if (only is None or todo - {'losses', 'nms', 'dcn', 'map'}) else None
+    no_priors = {'losses', 'nms', 'dcn', 'map', 'transforms'}
+    priors = gen_priors(R) if (only is None or todo - no_priors) else None
     for name in gens:
         if name not in todo:
             continue
         fn = globals()['gen_' + name]
-        if name in ('losses', 'nms', 'dcn', 'map'):
+        if name in no_priors:
             fn(R)
         else:
             fn(R, priors)

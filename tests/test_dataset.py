@@ -9,6 +9,7 @@ import torch
 from torch.utils.data import DataLoader
 
 from shape_based_object_detection_amd.dataset import Datasets as D
+from shape_based_object_detection_amd.dataset import transforms as T
 
 
 def _cfg(ops=()):
@@ -54,12 +55,12 @@ def test_train_augmentation_in_worker_processes(tmp_path):
 
 def test_random_crop_keeps_centred_objects():
     import random
-    rng = random.Random(7)
+    random.seed(7)
     img = torch.rand(3, 200, 300)
     boxes = torch.tensor([[10., 10., 60., 80.], [100., 50., 250., 190.], [150., 20., 180., 40.]])
     labels = torch.tensor([3, 7, 9])
     for _ in range(20):
-        im, b, l = D.random_crop(img, boxes, labels, rng)
+        im, b, l = T.random_crop(img, boxes, labels)
         assert im.shape[0] == 3 and b.shape[0] == l.shape[0]
         assert (b >= 0).all()
         assert (b[:, 2] <= im.shape[2]).all() and (b[:, 3] <= im.shape[1]).all()
@@ -69,10 +70,50 @@ def test_flip_and_expand_boxes():
     from PIL import Image
     im = Image.fromarray(np.zeros((50, 80, 3), np.uint8))
     boxes = torch.tensor([[10., 5., 30., 25.]])
-    _, fb = D.flip(im, boxes)
+    _, fb = T.flip(im, boxes.clone())
     assert fb.tolist() == [[80 - 30 - 1, 5., 80 - 10 - 1, 25.]]
     import random
-    t, eb = D.expand(torch.rand(3, 50, 80), boxes, D.IMAGENET_MEAN, random.Random(1))
+    random.seed(1)
+    t, eb = T.expand(torch.rand(3, 50, 80), boxes, T.IMAGENET_MEAN)
     assert t.shape[1] >= 50 and t.shape[2] >= 80
     d = eb - boxes
     assert d[0, 0] == d[0, 2] and d[0, 1] == d[0, 3]
+
+
+def test_traffic_dataset_concatenates_folders(tmp_path):
+    """Datasets.py:167-256: a space-separated folder list, folders without the split skipped,
+    objects under 'boxes' with an 'image_id'."""
+    a = D.write_synthetic_voc(str(tmp_path / 'a'), 3, size=(120, 160), split='TRAIN', seed=1)
+    b = D.write_synthetic_voc(str(tmp_path / 'b'), 2, size=(120, 160), split='TRAIN', seed=2)
+    c = str(tmp_path / 'c')          # no TRAIN split here
+    os.makedirs(c)
+    for folder, base in ((a, 0), (b, 100)):
+        path = os.path.join(folder, 'TRAIN_objects.json')
+        with open(path) as f:
+            objs = json.load(f)
+        objs = [{'boxes': o['bbox'], 'labels': o['labels'], 'difficulties': o['difficulties'],
+                 'image_id': base + i} for i, o in enumerate(objs)]
+        with open(path, 'w') as f:
+            json.dump(objs, f)
+    ds = D.TrafficDataset(' '.join([a, c, b]), 'train', (64, 64), _cfg())
+    assert len(ds) == 5
+    dl = DataLoader(ds, batch_size=5, shuffle=False, collate_fn=ds.collate_fn)
+    images, boxes, labels, ids, diffs = next(iter(dl))
+    assert images.shape == (5, 3, 64, 64)
+    assert ids == [0, 1, 2, 100, 101]
+    assert all(bb.shape[0] == ll.shape[0] for bb, ll in zip(boxes, labels))
+
+
+def test_decimate_and_resize_keep():
+    from PIL import Image
+    t = torch.arange(4 * 6 * 8, dtype=torch.float32).view(4, 6, 8)
+    d = T.decimate(t, [None, 3, 2])
+    assert d.shape == (4, 2, 4) and torch.equal(d, t[:, ::3, ::2])
+    im = Image.fromarray(np.zeros((40, 100, 3), np.uint8))      # landscape (W > H)
+    boxes = torch.tensor([[10., 5., 30., 25.]])
+    # transforms.py:271-277 as written: for W > H, dims (h, w) with h < w are swapped, so both
+    # orders give an output of height 300 and width 200
+    for dims in ((300, 200), (200, 300)):
+        out, nb = T.resize_keep(im, boxes.clone(), dims)
+        assert out.size == (200, 300)
+        assert torch.equal(nb, boxes / torch.tensor([100., 40., 100., 40.]))
