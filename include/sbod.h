@@ -79,6 +79,11 @@ int sbod_memcpy_d2h_async(void *dst_host, const void *src_dev, size_t bytes, voi
 int sbod_graph_launch(void *graph_exec, void *stream);
 int sbod_event_record(void *event, void *stream);
 
+/* Stream ordering for work handed between streams (no host sync): everything queued on
+ * `on_stream` so far completes before anything queued on `waiting_stream` after this call.
+ * A no-op when both are the same stream. */
+int sbod_stream_wait(void *waiting_stream, void *on_stream);
+
 /* ---------------------------------------------------------------- f1: ground-truth packing
  * Replaces the per-step GT handling of every criterion: the collate_fn list-of-tensors batch
  * (dataset/Datasets.py:58-86), moved to the device image by image (train_anchor.py:266-268) and
@@ -294,9 +299,12 @@ int sbod_nms_f32(const float *boxes, const float *scores, int64_t n, float overl
  *   Backward: grad_out -> grad_x, grad_offset, grad_mask_logits, grad_weight (any may be NULL).
  *   The backward writes dcols rows [B*Ho*Wo][k²][C] and gathers dx per input pixel (no float
  *   atomics on dx); grad_out and weight must each stay below 2 GiB (buffer-descriptor range).
- * Workspace: sbod_dcn_workspace_bytes(...) (forward and backward share it; it includes the
- * backward's dcols rows, B*Ho*Wo*k²*C*4 bytes). */
+ * Workspace: sbod_dcn_workspace_bytes(...) for the backward (it includes the dcols rows,
+ * B*Ho*Wo*k²*C*4 bytes); the forward needs only sbod_dcn_fwd_workspace_bytes(...) (coefficients,
+ * channels-last x and the transposed weights — a prefix of the backward's layout, so one
+ * workspace sized for the backward serves both). */
 size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
+size_t sbod_dcn_fwd_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
 int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logits,
                      const float *weight, int B, int C, int H, int W, int O, int k, int stride,
                      int pad, float *out, void *workspace, size_t workspace_bytes, void *stream);

@@ -59,8 +59,10 @@ SIGNATURES = {
     'sbod_memcpy_d2h_async': (I32, [P, P, SZ, P]),
     'sbod_graph_launch': (I32, [P, P]),
     'sbod_event_record': (I32, [P, P]),
+    'sbod_stream_wait': (I32, [P, P]),
     'sbod_gt_pack': (I32, [P, P, P, I32, I64, P, P, P, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
+    'sbod_dcn_fwd_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
     'sbod_dcn_fwd_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),
     'sbod_dcn_bwd_f32': (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, P,
                                P, SZ, P]),

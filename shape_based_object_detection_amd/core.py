@@ -179,14 +179,21 @@ class GtStaging:
         stream, then every (graph exec, stream) of ``launches`` (from ``graph_launches``), then
         ``event`` (a raw hipEvent_t, 0 for none) recorded on ``event_stream`` — all in C++
         (_sbodhost.stage_and_replay).  Returns the GtPack, or None when the batch or the build
-        needs the Python path (nothing was launched then)."""
+        needs the Python path (nothing was launched then).
+
+        Ordering: the lists may have been produced on the CURRENT stream (e.g. a non_blocking
+        ``.to(device)``).  The packing stream waits for it first, and the current stream waits
+        for the packing launch afterwards (not for the graphs), so the pack never reads a copy
+        in flight and the caching allocator cannot recycle the lists' memory under it."""
         ext = L.host_ext
         if (ext is None or type(boxes) is not list or type(labels) is not list or not launches
                 or len(boxes) != self.batch or not boxes[0].is_cuda):
             return None
-        r = ext.stage_and_replay(boxes, labels, self.boxes.shape[0], self.capacity, self.device.index or 0,
+        dev = self.device.index or 0
+        r = ext.stage_and_replay(boxes, labels, self.boxes.shape[0], self.capacity, dev,
                                  self.boxes.data_ptr(), self.labels.data_ptr(), self.offsets.data_ptr(),
-                                 launches[0][1], allow_empty, launches, event or None, event_stream or None)
+                                 launches[0][1], allow_empty, launches, event or None, event_stream or None,
+                                 L._raw_stream(dev) or None)
         if r is None:
             return None
         if type(r) is int:
@@ -413,25 +420,38 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
     return loss, holder[0]
 
 
+_POOL_SIZES_OK = set()   # (group, world, B*P) whose equality over the ranks was verified
+
+
 def allgather_pool(group=None):
     """The data-parallel exchange of MultiBoxLoss300's global mining pool (SSD300.py:580-588):
     every rank's [B*P] pool gathered rank-major over RCCL (B*P*4 bytes per rank; equal B on every
     rank, as a DistributedSampler with drop_last gives).  Returns ``f(pool) -> (pool_all,
-    local_off)`` for ``fused_criterion(exchange=...)``."""
+    local_off)`` for ``fused_criterion(exchange=...)``.
+
+    The first eager call at a given pool size checks that every rank holds the same B*P (one
+    tiny MAX all-reduce of (n, -n) and a host read), so unequal shards fail loudly on every rank
+    instead of desynchronising the gather.  Later calls at a verified size — and calls under
+    hipGraph capture, whose replays keep the captured shapes — enqueue the gather alone, so a
+    data-parallel SSD300 step is capturable (an unverified size under capture raises: run the
+    step eagerly once first, as any capture warm-up does)."""
     import torch.distributed as dist
 
     def exchange(pool):
         world, rank = dist.get_world_size(group), dist.get_rank(group)
-        # every rank must contribute the same B*P (a DistributedSampler with drop_last): checked
-        # with one tiny MAX all-reduce of (n, -n), so unequal shards fail loudly on every rank
-        # instead of desynchronising the gather
         n = pool.numel()
-        chk = torch.tensor([n, -n], dtype=torch.int64, device=pool.device)
-        dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=group)
-        hi, lo = chk.tolist()
-        if hi != -lo:
-            raise RuntimeError('sbod global mining: ranks hold unequal batches (B*P between %d and %d); '
-                               'use equal per-rank batches (drop_last=True)' % (-lo, hi))
+        key = (id(group) if group is not None else None, world, n)
+        if key not in _POOL_SIZES_OK:
+            if pool.is_cuda and torch.cuda.is_current_stream_capturing():
+                raise L.SbodError('sbod global mining under hipGraph capture: the per-rank pool size '
+                                  '%d was never verified; run the criterion eagerly once first' % n)
+            chk = torch.tensor([n, -n], dtype=torch.int64, device=pool.device)
+            dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=group)
+            hi, lo = chk.tolist()
+            if hi != -lo:
+                raise RuntimeError('sbod global mining: ranks hold unequal batches (B*P between %d and %d); '
+                                   'use equal per-rank batches (drop_last=True)' % (-lo, hi))
+            _POOL_SIZES_OK.add(key)
         out = torch.empty(world * n, dtype=pool.dtype, device=pool.device)
         if dist.get_backend(group) == 'gloo':     # gloo has no all_gather_into_tensor
             parts = [torch.empty_like(pool) for _ in range(world)]
@@ -443,13 +463,15 @@ def allgather_pool(group=None):
     return exchange
 
 
-def allreduce_npos(n_pos, group=None):
+def allreduce_npos(n_pos, group=None, force=False):
     """Data parallel: the global positive count (one 4-byte SUM all-reduce over RCCL, enqueued on
-    the current stream — no host sync).  Every rank then normalises by the global count, so the
-    per-rank gradients are exactly the global-batch gradient's slices."""
+    the current stream — no host sync, so it is captured into a hipGraph with the criterion).
+    Every rank then normalises by the global count, so the per-rank gradients are exactly the
+    global-batch gradient's slices.  A one-rank group skips the collective unless
+    ``force`` (tests exercise the captured collective on one GPU that way)."""
     import torch.distributed as dist
     tot = n_pos[-1:].clone()
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_available() and dist.is_initialized() and (force or dist.get_world_size(group) > 1):
         dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
     return tot
 
@@ -784,7 +806,9 @@ class _DeformConv(torch.autograd.Function):
         if tuple(weight.shape) != (O, C, ks, ks):
             raise ValueError('DeformConv2d: weight shape %s' % (tuple(weight.shape),))
         out = torch.empty(B, O, Ho, Wo, dtype=torch.float32, device=x.device)
-        nb = L.lib().sbod_dcn_workspace_bytes(B, C, H, W, O, ks, stride, padding)
+        # forward-only size (no dcols rows): an eval forward does not pay the backward's buffers;
+        # the backward grows the same cached workspace when it runs
+        nb = L.lib().sbod_dcn_fwd_workspace_bytes(B, C, H, W, O, ks, stride, padding)
         ws = workspace(nb, x.device, 'dcn')
         L.call('sbod_dcn_fwd_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight),
                B, C, H, W, O, ks, stride, padding, L.ptr(out), L.ptr(ws), nb, L.stream_of(x))

@@ -260,6 +260,23 @@ int sbod_event_record(void *event, void *stream) {
   return SBOD_OK;
 }
 
+int sbod_stream_wait(void *waiting_stream, void *on_stream) {
+  if (waiting_stream == on_stream) return SBOD_OK;
+  // one event per host thread and device: hipStreamWaitEvent binds to the record current at the
+  // time of the call, so re-recording the same event for the next wait is safe
+  thread_local hipEvent_t ev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return sbod::launch_status("sbod_stream_wait");
+  if (ev[dev] == nullptr && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) {
+    ev[dev] = nullptr;
+    return sbod::launch_status("sbod_stream_wait(create)");
+  }
+  if (hipEventRecord(ev[dev], sbod::as_stream(on_stream)) != hipSuccess ||
+      hipStreamWaitEvent(sbod::as_stream(waiting_stream), ev[dev], 0) != hipSuccess)
+    return sbod::launch_status("sbod_stream_wait");
+  return SBOD_OK;
+}
+
 int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, void *stream) {
   SBOD_REQUIRE(n >= 0 && scale != nullptr, "sbod_scale_inplace: bad arguments");
   if (n == 0) return SBOD_OK;

@@ -725,7 +725,9 @@ size_t dcn_scan_bytes(int64_t n) {
   return b;
 }
 
-size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w) {
+// The forward needs only coef, xt and wt (a prefix of the layout); the backward's buffers
+// follow, so a forward-only caller sizes its workspace with sbod_dcn_fwd_workspace_bytes.
+size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w, bool fwd_only = false) {
   char *p = static_cast<char *>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) { char *r = p ? p + off : nullptr; off += align_up(bytes); return r; };
@@ -733,11 +735,15 @@ size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w) {
   const size_t wbytes = static_cast<size_t>(s.O) * s.K * 4;
   const size_t rows = static_cast<size_t>(s.M) * s.N;
   const size_t npix = static_cast<size_t>(s.B) * s.H * s.W;
-  DcnWs t;
+  DcnWs t{};
   t.coef = reinterpret_cast<Coef *>(take(rows * sizeof(Coef)));
   t.xt = reinterpret_cast<float *>(take(xbytes));
-  t.gxt = reinterpret_cast<float *>(take(xbytes));
   t.wt = reinterpret_cast<float *>(take(wbytes));
+  if (fwd_only) {
+    if (w) *w = t;
+    return off;
+  }
+  t.gxt = reinterpret_cast<float *>(take(xbytes));
   t.gwp = reinterpret_cast<float *>(take(wbytes));
   t.dcols = reinterpret_cast<float *>(take(rows * s.C * 4));
   t.tcount = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
@@ -763,6 +769,10 @@ size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int st
   return dcn_carve(make_shape(B, C, H, W, O, k, stride, pad), nullptr, nullptr);
 }
 
+size_t sbod_dcn_fwd_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
+  return dcn_carve(make_shape(B, C, H, W, O, k, stride, pad), nullptr, nullptr, true);
+}
+
 static int dcn_check(const DcnShape &s, const float *x, const float *offset, const float *weight) {
   SBOD_REQUIRE(x && offset && weight && s.B > 0 && s.C > 0 && s.H > 0 && s.W > 0 && s.O > 0 &&
                    s.k > 0 && s.stride > 0 && s.pad >= 0,
@@ -776,13 +786,13 @@ static int dcn_check(const DcnShape &s, const float *x, const float *offset, con
 
 static int dcn_prepare(const DcnShape &s, const float *x, const float *offset, const float *mask_logits,
                        void *workspace, size_t workspace_bytes, DcnWs *w, hipStream_t hs, const char *who,
-                       bool count_targets) {
-  const size_t need = dcn_carve(s, nullptr, nullptr);
+                       bool count_targets, bool fwd_only) {
+  const size_t need = dcn_carve(s, nullptr, nullptr, fwd_only);
   if (workspace == nullptr || workspace_bytes < need) {
     set_error("%s: workspace %zu < %zu", who, workspace_bytes, need);
     return SBOD_E_WORKSPACE;
   }
-  dcn_carve(s, workspace, w);
+  dcn_carve(s, workspace, w, fwd_only);
   const int64_t nc = static_cast<int64_t>(s.M) * s.N;
   if (count_targets &&
       hipMemsetAsync(w->tcount, 0, (static_cast<size_t>(s.B) * s.H * s.W + 1) * 4, hs) != hipSuccess)
@@ -804,7 +814,7 @@ int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logi
   SBOD_REQUIRE(out != nullptr, "sbod_dcn_fwd_f32: out is NULL");
   hipStream_t hs = as_stream(stream);
   DcnWs w;
-  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_fwd_f32", false);
+  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_fwd_f32", false, true);
   if (st != SBOD_OK) return st;
   launch_transpose(weight, w.wt, s.O, s.C, s.N, hs);   // W [O][C][N] -> Wf [O][N][C]
   SBOD_LAUNCHED("k_transpose(w)");
@@ -842,7 +852,7 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
   hipStream_t hs = as_stream(stream);
   DcnWs w;
   st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_bwd_f32",
-                   grad_x != nullptr);
+                   grad_x != nullptr, false);
   if (st != SBOD_OK) return st;
   if (!mask_logits) grad_mask_logits = nullptr;
   const int npix = B * H * W;

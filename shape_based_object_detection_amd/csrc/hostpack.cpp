@@ -30,7 +30,7 @@ namespace {
 // batch needs the Python path (nothing launched), or a negative sbod status.
 int pack_lists(PyObject *boxes, PyObject *labels, long long capacity, long long per_image,
                int want_dev, void *ob, void *ol, void *oo, void *stream, int allow_empty,
-               std::vector<int32_t> &cnt) {
+               std::vector<int32_t> &cnt, void *src_stream) {
   if (!PyList_Check(boxes) || !PyList_Check(labels)) return 0;
   const Py_ssize_t B = PyList_GET_SIZE(boxes);
   if (B != PyList_GET_SIZE(labels) || B == 0) return 0;
@@ -59,6 +59,10 @@ int pack_lists(PyObject *boxes, PyObject *labels, long long capacity, long long 
     total += g;
   }
   if (total > capacity) return 0;
+  if (src_stream != stream) {   // fork: the pack waits for the stream that produced the GT
+    const int sw = sbod_stream_wait(stream, src_stream);
+    if (sw != SBOD_OK) return sw;
+  }
   const int st = sbod_gt_pack(bp.data(), lp.data(), cnt.data(), static_cast<int>(B), capacity,
                               static_cast<float *>(ob), static_cast<int64_t *>(ol),
                               static_cast<int32_t *>(oo), stream);
@@ -87,21 +91,28 @@ PyObject *pack_device_lists(PyObject *, PyObject *const *a, Py_ssize_t n) {
   const int allow_empty = PyObject_IsTrue(a[9]);
   if (PyErr_Occurred()) return nullptr;
   std::vector<int32_t> cnt;
-  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, cnt);
+  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, cnt,
+                           stream);
   if (r == 0) Py_RETURN_NONE;
   if (r < 0) return PyLong_FromLong(r);
   return counts_list(cnt);
 }
 
 // stage_and_replay(boxes, labels, capacity, per_image_cap, device, out_boxes, out_labels,
-//                  out_offsets, stream, allow_empty, launches, event, event_stream)
+//                  out_offsets, stream, allow_empty, launches, event, event_stream, src_stream)
 //   pack_device_lists' packing on `stream`, then every (graph_exec, stream) pair of `launches`
 //   (a tuple) launched in order (sbod_graph_launch), then `event` (hipEvent_t or None) recorded
 //   on `event_stream`: one call submits a captured step.  Returns as pack_device_lists; None
 //   means nothing was launched.
+//   Ordering contract: the GT tensors were produced on `src_stream` (the caller's current
+//   stream, e.g. by a non_blocking .to(device)).  When the packing stream differs, it first
+//   waits for `src_stream`, and `src_stream` then waits for the packing launch (not for the
+//   graphs): the pack never reads a copy that has not landed, and the caching allocator —
+//   which hands a freed block out again only to work on its allocation stream — cannot give
+//   the source memory to later work on `src_stream` before the pack has read it.
 PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
-  if (n != 13) {
-    PyErr_SetString(PyExc_TypeError, "stage_and_replay: expected 13 arguments");
+  if (n != 14) {
+    PyErr_SetString(PyExc_TypeError, "stage_and_replay: expected 14 arguments");
     return nullptr;
   }
   const long long capacity = PyLong_AsLongLong(a[2]);
@@ -113,6 +124,7 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
   PyObject *launches = a[10];
   void *event = opt_ptr(a[11]);
   void *ev_stream = opt_ptr(a[12]);
+  void *src_stream = opt_ptr(a[13]);
   if (PyErr_Occurred()) return nullptr;
   if (!PyTuple_Check(launches)) {
     PyErr_SetString(PyExc_TypeError, "stage_and_replay: launches must be a tuple of (exec, stream)");
@@ -131,9 +143,14 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
   }
   if (PyErr_Occurred()) return nullptr;
   std::vector<int32_t> cnt;
-  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, cnt);
+  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, cnt,
+                           src_stream);
   if (r == 0) Py_RETURN_NONE;
   if (r < 0) return PyLong_FromLong(r);
+  if (src_stream != stream) {
+    const int sj = sbod_stream_wait(src_stream, stream);   // join: after the pack only
+    if (sj != SBOD_OK) return PyLong_FromLong(sj);
+  }
   for (Py_ssize_t i = 0; i < nl; ++i) {
     const int s2 = sbod_graph_launch(ex[i], st[i]);
     if (s2 != SBOD_OK) return PyLong_FromLong(s2);

@@ -50,6 +50,7 @@ class _AnchorCriterion(nn.Module):
         self.distributed = False
         self.process_group = None
         self.grad_reduction = 'mean'
+        self.force_collectives = False   # run the collectives even in a one-rank group (tests)
         self.last_components = None
 
     def increase_threshold(self, increment=0.1):
@@ -89,7 +90,8 @@ class _AnchorCriterion(nn.Module):
         assert n_priors == predicted_locs.size(1) == predicted_scores.size(1)
         gt = core.pack_gt(boxes, labels)
         obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold)
-        tot = core.allreduce_npos(npos, self.process_group) if self.distributed else npos[B:]
+        tot = (core.allreduce_npos(npos, self.process_group, self.force_collectives)
+               if self.distributed else npos[B:])
         spec = self._spec()
         # SSD300's CE mines over the whole batch: data-parallel, the pools are exchanged
         exchange = (core.allgather_pool(self.process_group)
@@ -147,6 +149,7 @@ class RefineDetLoss(nn.Module):
         self.distributed = False
         self.process_group = None
         self.grad_reduction = 'mean'
+        self.force_collectives = False
         self.last_components = None
 
     def increase_threshold(self, increment=0.05):
@@ -156,7 +159,8 @@ class RefineDetLoss(nn.Module):
             self.threshold += increment
 
     def _tot(self, npos, B):
-        return core.allreduce_npos(npos, self.process_group) if self.distributed else npos[B:]
+        return (core.allreduce_npos(npos, self.process_group, self.force_collectives)
+                if self.distributed else npos[B:])
 
     def compute_arm_loss(self, arm_locs, arm_scores, boxes, labels):
         """Binary anchor-refinement loss vs the fixed priors (RefineDet512.py:730-820)."""

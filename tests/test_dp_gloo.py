@@ -155,9 +155,9 @@ def _worker_criterion_class(rank, world, port, kind, reg, cls, out_q):
 
         real_ar, real_ag = core.allreduce_npos, core.allgather_pool
 
-        def allreduce_npos(npos, group=None):
+        def allreduce_npos(npos, group=None, force=False):
             calls.append('allreduce_npos')
-            return real_ar(npos, group)
+            return real_ar(npos, group, force)
 
         def allgather_pool(group=None):
             calls.append('allgather_pool')

@@ -1,0 +1,104 @@
+"""Config C5 (FCOS-R50 800x1333, batch 64 data-parallel over 8 GPUs) at its shapes.
+
+The reference's ``FCOSLoss`` is broken (models/FCOSDet.py:147,174,410,441 crash before any loss
+is computed), so FCOSLoss itself is "parity unpinned".  Its live pieces are
+pinned here at C5's shapes against the oracle (a torch-fp32 restatement of Loss.py, itself
+pinned to the reference's golden vectors in test_oracle_golden.py):
+
+* ``SigmoidFocalLoss`` (operators/Loss.py:41-80) on one rank's shard: 8 images x 22,300
+  locations (strides 8..128 on 800x1333: 100x167 + 50x84 + 25x42 + 13x21 + 7x11) x 81 classes,
+  normalised by (positives + batch) as FCOSLoss does (FCOSDet.py:527-529);
+* ``IouLoss`` (Loss.py:164-200) on the shard's positives, 'Diou' with centerness weights (the
+  FCOSLoss call, FCOSDet.py:537) and 'Giou' / 'Iou' with the 'mean' reduction;
+* the batch-64-over-8 split: the eight shards' focal sums over the GLOBAL normaliser add up to
+  the full batch-64 loss, and every shard's logit gradient is the full batch's gradient rows.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import loss_ref as LR
+from shape_based_object_detection_amd.operators import Loss as LS
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+LOCS = 100 * 167 + 50 * 84 + 25 * 42 + 13 * 21 + 7 * 11      # 22,300 locations per image
+C = 81
+B_RANK, WORLD = 8, 8
+
+
+class _Cfg:
+    device = DEV
+
+
+def _shard(seed, B=B_RANK, pos_frac=0.015):
+    g = torch.Generator().manual_seed(seed)
+    rows = B * LOCS
+    logits = torch.randn(rows, C, generator=g)
+    labels = torch.zeros(rows, dtype=torch.int64)
+    pos = torch.rand(rows, generator=g) < pos_frac
+    labels[pos] = torch.randint(1, C, (int(pos.sum()),), generator=g)
+    n = int(pos.sum())
+    xy = torch.rand(n, 2, generator=g) * 0.7
+    wh = torch.rand(n, 2, generator=g) * 0.25 + 0.02
+    tgt = torch.cat([xy, xy + wh], 1)
+    pred = tgt + torch.randn(n, 4, generator=g) * 0.02
+    ctr = torch.rand(n, generator=g) * 0.9 + 0.05             # centerness targets in (0, 1)
+    return logits, labels, pos, pred, tgt, ctr
+
+
+def test_c5_sigmoid_focal_shard_vs_oracle():
+    logits, labels, pos, _, _, _ = _shard(5)
+    norm = float(int(pos.sum()) + B_RANK)
+    z = logits.to(DEV).requires_grad_(True)
+    loss = LS.SigmoidFocalLoss(2.0, 0.25, _Cfg())(z, labels.to(DEV).int()) / norm
+    loss.backward()
+    zr = logits.clone().requires_grad_(True)
+    ref = LR.focal_sigmoid(zr, labels, gamma=2.0, alpha=0.25) / norm
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
+    # per-element gradients: each comes from one row's closed form, no reduction in between
+    np.testing.assert_allclose(z.grad.cpu().numpy(), zr.grad.numpy(), rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize('kind', ['Diou', 'Giou', 'Iou'])
+def test_c5_iou_loss_on_shard_positives(kind):
+    _, _, _, pred, tgt, ctr = _shard(6)
+    p = pred.to(DEV).requires_grad_(True)
+    w = ctr.to(DEV) if kind == 'Diou' else None           # FCOSDet.py:537 weights the Diou loss
+    loss = LS.IouLoss(pred_mode='Corner', reduce='mean', losstype=kind)(p, tgt.to(DEV), weights=w)
+    loss.backward()
+    pr = pred.clone().requires_grad_(True)
+    ref = LR.iou_loss(kind.lower(), pr, tgt, weights=ctr if kind == 'Diou' else None)
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
+    np.testing.assert_allclose(p.grad.cpu().numpy(), pr.grad.numpy(), rtol=1e-3, atol=1e-9)
+
+
+def test_c5_batch64_over_8_shards_equals_full_batch():
+    """DP mechanics of C5: per-rank focal sums over the global normaliser (positives of all 64
+    images + 64) add up to the single-device batch-64 loss; per-rank gradients are the rows of
+    the full batch's gradient (the same per-element closed form)."""
+    shards = [_shard(100 + r) for r in range(WORLD)]
+    n_pos = sum(int(s[2].sum()) for s in shards)
+    norm = float(n_pos + B_RANK * WORLD)
+    crit = LS.SigmoidFocalLoss(2.0, 0.25, _Cfg())
+    parts, grads = [], []
+    for logits, labels, _, _, _, _ in shards:
+        z = logits.to(DEV).requires_grad_(True)
+        l = crit(z, labels.to(DEV).int()) / norm
+        l.backward()
+        parts.append(l.detach().double())
+        grads.append(z.grad)
+    full_z = torch.cat([s[0] for s in shards]).to(DEV).requires_grad_(True)
+    full = crit(full_z, torch.cat([s[1] for s in shards]).to(DEV).int()) / norm
+    full.backward()
+    np.testing.assert_allclose(float(sum(parts)), full.item(), rtol=1e-5)
+    torch.testing.assert_close(torch.cat(grads), full_z.grad, rtol=0, atol=0)
+    # two of the shards against the oracle as well (the whole batch on the CPU oracle is slow)
+    for r in (0, WORLD - 1):
+        zr = shards[r][0].clone().requires_grad_(True)
+        ref = LR.focal_sigmoid(zr, shards[r][1], gamma=2.0, alpha=0.25) / norm
+        ref.backward()
+        np.testing.assert_allclose(parts[r].item(), ref.item(), rtol=1e-4)
+        np.testing.assert_allclose(grads[r].cpu().numpy(), zr.grad.numpy(), rtol=1e-4, atol=1e-9)
