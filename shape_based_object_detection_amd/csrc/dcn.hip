@@ -692,18 +692,31 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
     }
 }
 
+// A shape whose sizes are non-positive, out of range or overflow 32-bit indexing comes back with
+// every field 0 (shape_ok() false): no division by a zero stride, no signed overflow in the
+// products, and the size queries return 0 for it.
 DcnShape make_shape(int B, int C, int H, int W, int O, int k, int stride, int pad) {
-  DcnShape s;
+  DcnShape s{};
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || O <= 0 || k <= 0 || k > 7 || stride <= 0 || pad < 0 ||
+      H > (1 << 30) || W > (1 << 30) || pad > (1 << 20))
+    return s;
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;   // p_conv: 3x3, padding 1
+  const int64_t M = static_cast<int64_t>(B) * Ho * Wo, K = static_cast<int64_t>(C) * k * k;
+  if (M * k * k >= (1ll << 31) || K * O >= (1ll << 31) || static_cast<int64_t>(C) * H * W >= (1ll << 31) ||
+      static_cast<int64_t>(B) * C * H * W >= (1ll << 40))
+    return s;
   s.B = B; s.C = C; s.H = H; s.W = W; s.O = O; s.k = k; s.N = k * k;
   s.stride = stride; s.pad = pad;
-  s.Ho = (H - 1) / stride + 1;   // p_conv: 3x3, padding 1, stride `stride`
-  s.Wo = (W - 1) / stride + 1;
+  s.Ho = static_cast<int>(Ho);
+  s.Wo = static_cast<int>(Wo);
   s.Hp = H + 2 * pad;
   s.Wp = W + 2 * pad;
-  s.M = B * s.Ho * s.Wo;
-  s.K = C * s.N;
+  s.M = static_cast<int>(M);
+  s.K = static_cast<int>(K);
   return s;
 }
+
+inline bool shape_ok(const DcnShape &s) { return s.B > 0; }
 
 struct DcnWs {
   Coef *coef;
@@ -766,17 +779,19 @@ using namespace sbod;
 extern "C" {
 
 size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
-  return dcn_carve(make_shape(B, C, H, W, O, k, stride, pad), nullptr, nullptr);
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  return shape_ok(s) ? dcn_carve(s, nullptr, nullptr) : 0;
 }
 
 size_t sbod_dcn_fwd_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
-  return dcn_carve(make_shape(B, C, H, W, O, k, stride, pad), nullptr, nullptr, true);
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  return shape_ok(s) ? dcn_carve(s, nullptr, nullptr, true) : 0;
 }
 
 static int dcn_check(const DcnShape &s, const float *x, const float *offset, const float *weight) {
-  SBOD_REQUIRE(x && offset && weight && s.B > 0 && s.C > 0 && s.H > 0 && s.W > 0 && s.O > 0 &&
-                   s.k > 0 && s.stride > 0 && s.pad >= 0,
-               "sbod_dcn: bad arguments");
+  SBOD_REQUIRE(x && offset && weight && shape_ok(s),
+               "sbod_dcn: bad arguments (NULL tensor, or sizes non-positive, kernel_size > 7 or "
+               "beyond 32-bit indexing)");
   SBOD_REQUIRE(s.N <= kMaxN, "sbod_dcn: kernel_size %d > 7 unsupported", s.k);
   SBOD_REQUIRE(static_cast<int64_t>(s.M) * s.N < (1ll << 31) && static_cast<int64_t>(s.C) * s.H * s.W < (1ll << 31) &&
                    static_cast<int64_t>(s.O) * s.K < (1ll << 31) && s.H < 65536 * 64 && s.W < 65536,
