@@ -59,7 +59,10 @@ def _digest(paths, extra=()):
             h.update(f.read())
         h.update(b'\0')
     for e in extra:
-        h.update(str(e).encode() + b'\0')
+        e = str(e)
+        if os.path.isabs(e):   # include paths: the tree moves (the GPU box runs it elsewhere)
+            e = os.path.relpath(e, REPO)
+        h.update(e.encode() + b'\0')
     return h.hexdigest()
 
 
