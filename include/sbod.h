@@ -144,7 +144,9 @@ int sbod_match_expand_f32(const float *gt_boxes, const int64_t *gt_labels,
 
 /* iou_utils.match / match_ious (iou_utils.py:236-321): plain jaccard vs point_form(priors),
  * best-prior fill 2.0, UNFILTERED j, conf = labels + 1.  Writes loc_t[idx] / conf_t[idx]
- * rows (caller passes the row pointers).  encode != 0 -> encode(variances) else raw matches. */
+ * rows (caller passes the row pointers).  encode != 0 -> encode(variances) else raw matches.
+ * Workspace: sbod_match_ssd_workspace_bytes(G, P) (0 for non-positive sizes). */
+size_t sbod_match_ssd_workspace_bytes(int G, int P);
 int sbod_match_ssd_f32(const float *truths, const int64_t *labels, int G,
                        const float *priors_cxcy, int P, float threshold, float var0, float var1,
                        int encode, float *loc_t_row, int64_t *conf_t_row, void *workspace,

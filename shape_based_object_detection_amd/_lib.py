@@ -30,6 +30,7 @@ SIGNATURES = {
     'sbod_match_workspace_bytes_p': (SZ, [I32, I32, I32]),
     'sbod_match_f32': (I32, [P, P, P, I32, I32, P, P, P, I32, F32, F32, I32, P, P, P, P, SZ, P]),
     'sbod_match_expand_f32': (I32, [P, P, P, I32, P, P, P, P, I32, F32, F32, I32, P, P, P, P, P]),
+    'sbod_match_ssd_workspace_bytes': (SZ, [I32, I32]),
     'sbod_match_ssd_f32': (I32, [P, P, I32, P, I32, F32, F32, F32, I32, P, P, P, SZ, P]),
     'sbod_codec_f32': (I32, [I32, P, P, I64, I64, F32, F32, P, P]),
     'sbod_loss_workspace_bytes': (SZ, [I32, I32]),

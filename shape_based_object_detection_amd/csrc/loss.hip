@@ -847,13 +847,12 @@ struct LossWs {
 };
 LossWs carve(void *w, int B, int P) {
   const size_t nblk = static_cast<size_t>(B) * ((P + kLTile - 1) / kLTile);
-  char *c = static_cast<char *>(w);
   LossWs r;
-  r.partials = reinterpret_cast<float *>(c);
+  r.partials = ws_at<float>(w, 0);
   size_t o = align_up(nblk * 2 * sizeof(float));
-  r.pool = reinterpret_cast<float *>(c + o);
+  r.pool = ws_at<float>(w, o);
   o += align_up(static_cast<size_t>(B) * P * sizeof(float));
-  r.hnm = reinterpret_cast<float *>(c + o);
+  r.hnm = ws_at<float>(w, o);
   o += align_up((B + 1) * sizeof(float));
   r.bytes = o;
   return r;

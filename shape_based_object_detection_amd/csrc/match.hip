@@ -622,12 +622,11 @@ struct MatchWs {
 };
 MatchWs carve_match(void *w, int B, int Gmax, int P) {
   const size_t ntile = (P + kMThreads - 1) / kMThreads;
-  char *c = static_cast<char *>(w);
   MatchWs r;
   size_t o = 0;
-  r.rec = reinterpret_cast<MRec *>(c + o);
+  r.rec = ws_at<MRec>(w, o);
   o += align_up(static_cast<size_t>(B) * ntile * Gmax * sizeof(MRec));
-  r.tcount = reinterpret_cast<int32_t *>(c + o);
+  r.tcount = ws_at<int32_t>(w, o);
   o += align_up(static_cast<size_t>(B) * ntile * 4);
   r.bytes = o;
   return r;
@@ -726,6 +725,12 @@ int sbod_match_expand_f32(const float *gt_boxes, const int64_t *gt_labels,
   return SBOD_OK;
 }
 
+size_t sbod_match_ssd_workspace_bytes(int G, int P) {
+  // per object: the best prior key (8 B); per prior: best object and its overlap (4 + 4 B)
+  if (G <= 0 || P <= 0) return 0;
+  return align_up(G * 8ull) + align_up(P * 4ull) * 2;
+}
+
 int sbod_match_ssd_f32(const float *truths, const int64_t *labels, int G,
                        const float *priors_cxcy, int P, float threshold, float var0, float var1,
                        int encode, float *loc_t_row, int64_t *conf_t_row, void *workspace,
@@ -733,7 +738,7 @@ int sbod_match_ssd_f32(const float *truths, const int64_t *labels, int G,
   SBOD_REQUIRE(G > 0 && P > 0 && truths && labels && priors_cxcy && loc_t_row && conf_t_row,
                "sbod_match_ssd_f32: bad arguments (G=%d P=%d)", G, P);
   SBOD_REQUIRE(G <= 4096, "sbod_match_ssd_f32: G %d > 4096 unsupported", G);
-  const size_t need = align_up(G * 8ull) + align_up(P * 4ull) * 2;
+  const size_t need = sbod_match_ssd_workspace_bytes(G, P);
   if (workspace_bytes < need) {
     set_error("sbod_match_ssd_f32: workspace %zu < %zu", workspace_bytes, need);
     return SBOD_E_WORKSPACE;

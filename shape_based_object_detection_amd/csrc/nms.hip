@@ -2020,26 +2020,25 @@ struct DetWs {
   size_t bytes;
 };
 DetWs carve_det(void *w, int B, int P, int C, int window) {
-  char *c = static_cast<char *>(w);
   DetWs r;
   size_t o = 0;
   // the candidate counters first: their place depends on B * C only (sbod_detect_f32's
   // SBOD_DETECT_COUNTERS_ZEROED contract)
-  r.count = reinterpret_cast<uint32_t *>(c + o);
+  r.count = ws_at<uint32_t>(w, o);
   o += align_up(static_cast<size_t>(B) * C * 4);
-  r.boxes = reinterpret_cast<float *>(c + o);
+  r.boxes = ws_at<float>(w, o);
   o += align_up(static_cast<size_t>(B) * P * 16);
-  r.cand = reinterpret_cast<unsigned long long *>(c + o);
+  r.cand = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * C * P * 8);
-  r.kept = reinterpret_cast<unsigned long long *>(c + o);
+  r.kept = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * C * window * 8);
-  r.kc = reinterpret_cast<uint32_t *>(c + o);
+  r.kc = ws_at<uint32_t>(w, o);
   o += align_up(static_cast<size_t>(B) * C * 4);
-  r.lastkey = reinterpret_cast<unsigned long long *>(c + o);
+  r.lastkey = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * C * 8);
-  r.scratch = reinterpret_cast<unsigned long long *>(c + o);
+  r.scratch = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * C * window * 8);
-  r.need = reinterpret_cast<int32_t *>(c + o);
+  r.need = ws_at<int32_t>(w, o);
   o += align_up(static_cast<size_t>(B) * 4);
   r.bytes = o;
   return r;

@@ -128,6 +128,13 @@ inline void tlaunch(const KernelTimer &kt, void (*kernel)(KArgs...), dim3 grid, 
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
+// Address `off` bytes into a caller workspace, or nullptr in a size-only query (base == nullptr):
+// the carve functions never do pointer arithmetic on a null base.
+template <typename T>
+inline T *ws_at(void *base, size_t off) {
+  return base ? reinterpret_cast<T *>(static_cast<char *>(base) + off) : nullptr;
+}
+
 inline int next_pow2_host(int x) {
   int p = 1;
   while (p < x) p <<= 1;

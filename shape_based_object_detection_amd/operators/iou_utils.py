@@ -83,8 +83,8 @@ def _match(threshold, truths, priors, variances, labels, loc_t, conf_t, idx, enc
     lb = labels.to(torch.int64).contiguous()
     pri = priors.float().contiguous()
     G, P = tr.shape[0], pri.shape[0]
-    nb = 2 * (8 * G + 256) + 8 * P + 512
-    ws = core.workspace(nb, tr.device)
+    nb = L.lib().sbod_match_ssd_workspace_bytes(G, P)
+    ws = core.workspace(nb, tr.device, 'match_ssd')
     L.call('sbod_match_ssd_f32', L.ptr(tr), L.ptr(lb), G, L.ptr(pri), P, float(threshold),
            float(variances[0]), float(variances[1]), int(encode), L.ptr(loc_t[idx]),
            L.ptr(conf_t[idx]), L.ptr(ws), nb, L.stream_of(tr))
