@@ -14,6 +14,6 @@ export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
   echo "# $(date -u +%FT%TZ) host ASan+UBSan: $RT"
   echo "# libsbod_hip.so (-Xarch_host sanitizers), _sbodhost.so, _sbodcall.so from variants/asan"
   LD_PRELOAD="$RT${LD_PRELOAD:+:$LD_PRELOAD}" SBOD_LIB=$PWD/variants/asan/libsbod_hip.so \
-    timeout -k 10 900 python -m pytest -p no:cacheprovider tests/test_cpu_host.py tests/test_host_malformed.py \
+    timeout -k 10 900 python -m pytest -p no:cacheprovider -s tests/test_cpu_host.py tests/test_host_malformed.py \
     tests/test_host_path.py -q 2>&1
 } | tee "$LOG"
