@@ -843,6 +843,7 @@ using namespace sbod;
 namespace {
 struct LossWs {
   float *partials, *pool, *hnm;
+  size_t pool_off;   // byte offset of `pool` (sbod_loss_pool_offset)
   size_t bytes;
 };
 LossWs carve(void *w, int B, int P) {
@@ -851,6 +852,7 @@ LossWs carve(void *w, int B, int P) {
   r.partials = ws_at<float>(w, 0);
   size_t o = align_up(nblk * 2 * sizeof(float));
   r.pool = ws_at<float>(w, o);
+  r.pool_off = o;
   o += align_up(static_cast<size_t>(B) * P * sizeof(float));
   r.hnm = ws_at<float>(w, o);
   o += align_up((B + 1) * sizeof(float));
@@ -963,8 +965,7 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
 }
 
 size_t sbod_loss_pool_offset(int B, int P) {
-  LossWs ws = carve(nullptr, B, P);
-  return static_cast<size_t>(reinterpret_cast<uintptr_t>(ws.pool));
+  return carve(nullptr, B, P).pool_off;
 }
 
 int sbod_multibox_mine_global(const void *scores, int dtype, int B, int P, int C,

@@ -22,3 +22,29 @@ def load_golden(name):
 @pytest.fixture(scope='session')
 def golden():
     return load_golden
+
+
+# Tolerance probe (SBOD_TOL_PROBE=<path.jsonl>): every np.testing.assert_allclose records, per
+# call site, the smallest rtol that passes with the asserted atol — used once on the GPU box to
+# tighten the gradient tolerances to what the kernels actually meet.
+if os.environ.get('SBOD_TOL_PROBE'):
+    import inspect
+    import json
+
+    _orig_allclose = np.testing.assert_allclose
+
+    def _probe_allclose(actual, desired, rtol=1e-7, atol=0, **kw):
+        a = np.asarray(actual, dtype=np.float64)
+        d = np.broadcast_to(np.asarray(desired, dtype=np.float64), a.shape)
+        err = np.abs(a - d)
+        with np.errstate(divide='ignore', invalid='ignore'):
+            need = np.where(err > atol, (err - atol) / np.abs(d), 0.0)
+        need = float(np.nanmax(need)) if need.size else 0.0
+        fr = inspect.stack()[1]
+        with open(os.environ['SBOD_TOL_PROBE'], 'a') as f:
+            f.write(json.dumps({'site': '%s:%d' % (os.path.basename(fr.filename), fr.lineno),
+                                'rtol': rtol, 'atol': atol, 'rtol_needed': need,
+                                'max_abs_err': float(err.max()) if err.size else 0.0}) + '\n')
+        return _orig_allclose(actual, desired, rtol=rtol, atol=atol, **kw)
+
+    np.testing.assert_allclose = _probe_allclose

@@ -159,3 +159,17 @@ def test_model_entry_registry():
         MD.model_entry(Cfg(model={'arch': 'RETINA50'}, n_classes=21, device='cpu'))
     with pytest.raises(NotImplementedError):
         MD.model_entry(Cfg(model={'arch': 'FCOS50'}, n_classes=21, device='cpu'))
+
+
+def test_workspace_layout_queries():
+    """Size / offset queries answer from the layout alone (no workspace): the mining pool sits
+    past the per-block partials and inside the loss workspace; the detect counters lead theirs."""
+    lib = L.lib()
+    for B, P in ((8, 8732), (32, 10248), (1, 7)):
+        off, nb = lib.sbod_loss_pool_offset(B, P), lib.sbod_loss_workspace_bytes(B, P)
+        assert 0 < off and off + 4 * B * P <= nb
+    assert lib.sbod_detect_counter_bytes(32, 21) <= lib.sbod_detect_workspace_bytes(32, 10248, 21)
+    assert lib.sbod_match_ssd_workspace_bytes(5, 8732) >= 5 * 8 + 8732 * 8
+    assert lib.sbod_match_ssd_workspace_bytes(0, 8732) == 0
+    assert 0 < lib.sbod_dcn_fwd_workspace_bytes(2, 8, 9, 9, 8, 3, 1, 1) < lib.sbod_dcn_workspace_bytes(2, 8, 9, 9, 8, 3, 1, 1)
+    assert lib.sbod_dcn_workspace_bytes(2, 8, 9, 9, 8, 3, 0, 1) == 0      # stride 0: invalid, no SIGFPE
