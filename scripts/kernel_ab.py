@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel device time (HIP events via sbod_timing_*) of the bench step's kernels, GPU-bound
-(criterion fwd+bwd + detect back to back, 200 iterations).  Select the library with SBOD_LIB to
+(criterion fwd+bwd + detect back to back, 200 iterations over 6 HBM-resident batches).  Select the library with SBOD_LIB to
 A/B two builds on one box:  SBOD_LIB=.../libsbod_hip_old.so python scripts/kernel_ab.py"""
 import json
 import os
@@ -18,16 +18,18 @@ dev = torch.device('cuda')
 pri = torch.from_numpy(prior_table('SSD512')).to(dev)
 cfg = bench.Cfg(reg_weights=1.0, device=dev, n_classes=21, reg_loss='diou', cls_loss='focal')
 crit = CR.MultiBoxLoss512(priors_cxcy=pri, config=cfg)
-boxes, labels, locs0, scores0, det = bench.make_batch(32, 0, dev)
-locs = locs0.clone().requires_grad_(True)
-scores = scores0.clone().requires_grad_(True)
+# six resident batches rotated step by step, as bench.py does: every launch reads from HBM
+batches = [bench.Batch(32, 100 * i, dev) for i in range(6)]
+k = [0]
 
 
 def step():
-    locs.grad = None
-    scores.grad = None
-    crit(locs, scores, boxes, labels).backward()
-    core.detect(locs.detach(), det, 0.01, 0.45, 200, pri)
+    bt = batches[k[0] % len(batches)]
+    k[0] += 1
+    bt.locs.grad = None
+    bt.scores.grad = None
+    crit(bt.locs, bt.scores, bt.boxes, bt.labels).backward()
+    core.detect(bt.locs.detach(), bt.det_scores, 0.01, 0.45, 200, pri)
 
 
 for _ in range(20):

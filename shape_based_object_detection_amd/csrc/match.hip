@@ -59,16 +59,19 @@ struct Anchor {
 };
 
 template <bool kOdm>
-__device__ __forceinline__ Anchor load_anchor(const float *anchors, const float *priors, int b,
-                                              int P, int p) {
-  Box4 a;
-  if constexpr (kOdm) {
-    a = decode_tenfive_xy(ld4(anchors + 4 * (static_cast<int64_t>(b) * P + p)), ld4(priors + 4 * p));
-  } else {
-    a = ld4(anchors + 4 * static_cast<int64_t>(p));
-  }
+__device__ __forceinline__ Anchor make_anchor(Box4 raw, Box4 prior) {
+  Box4 a = raw;
+  if constexpr (kOdm) a = decode_tenfive_xy(raw, prior);
   float ax = a.c - a.a, ay = a.d - a.b;
   return Anchor{a.a, a.b, a.c, a.d, ax * ay, (ax < kIouEps) && (ay < kIouEps)};
+}
+
+template <bool kOdm>
+__device__ __forceinline__ Anchor load_anchor(const float *anchors, const float *priors, int b,
+                                              int P, int p) {
+  if constexpr (kOdm)
+    return make_anchor<true>(ld4(anchors + 4 * (static_cast<int64_t>(b) * P + p)), ld4(priors + 4 * p));
+  return make_anchor<false>(ld4(anchors + 4 * static_cast<int64_t>(p)), Box4{0.f, 0.f, 0.f, 0.f});
 }
 
 // Matching in two launches.
@@ -130,13 +133,14 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile(
     float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
     MRec *__restrict__ rec, int32_t *__restrict__ tcount, int32_t *__restrict__ npos, int B,
     SpanRing *span) {
-  // dynamic LDS: [4 * Gmax labels]
+  // dynamic LDS: [4 * max(Gmax, kMThreads) labels]
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   __shared__ __attribute__((aligned(16))) uint32_t s_ord[kGc][kMThreads];  // per object, per prior: ord
   __shared__ uint32_t s_ev[kMThreads / 64];                                 // per wave: objects evaluated
   __shared__ int32_t s_fo[kMThreads];                                       // final (obj, ovl) per prior
   __shared__ float s_fv[kMThreads];
   __shared__ int s_red[16];
+  __shared__ float4 s_gt[kMThreads];   // this chunk's GT boxes: slot j < 16 = object gc + j
   STAMP_BEGIN();
   span_begin(span);
   PHASE_DECL;
@@ -148,10 +152,22 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile(
   const int tbase = blockIdx.x * kMThreads;
   const int p = tbase + tid;
   const bool valid = p < P;
-  const Anchor a = load_anchor<kOdm>(anchors, priors, b, P, min(p, P - 1));
+  // ONE memory round trip before the object loop: the anchor, the first chunk's GT boxes and the
+  // labels are loaded together (unconditional, clamped) and committed to LDS by unconditional
+  // stores before the first barrier, so no load sits under a branch where the compiler would
+  // sink it behind the anchor's wait; the object loop then reads the boxes from LDS instead of a
+  // scalar load round trip per group of objects.  An image without objects reads element 0 (the
+  // GT buffers hold at least one); s_lab has room for max(Gmax, kMThreads) labels.
+  const int pc = min(p, P - 1);
+  const Box4 araw = ld4(kOdm ? anchors + 4 * (static_cast<int64_t>(b) * P + pc) : anchors + 4 * static_cast<int64_t>(pc));
+  const Box4 apri = kOdm ? ld4(priors + 4 * pc) : Box4{0.f, 0.f, 0.f, 0.f};
   const int g0 = ld_i32_uniform(off + b), G = ld_i32_uniform(off + b + 1) - g0;
-  // labels are needed only after the object loop (the chunk barrier orders them)
-  for (int i = tid; i < G; i += kMThreads) s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
+  const Box4 gt0 = ld4(gt + 4 * static_cast<int64_t>(G > 0 ? g0 + min(tid & (kGc - 1), G - 1) : 0));
+  const int32_t lab0 = static_cast<int32_t>(labels[G > 0 ? g0 + min(tid, G - 1) : 0]);
+  const Anchor a = make_anchor<kOdm>(araw, apri);
+  s_gt[tid] = make_float4(gt0.a, gt0.b, gt0.c, gt0.d);
+  s_lab[tid] = lab0;
+  for (int i = tid + kMThreads; i < G; i += kMThreads) s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
   // the wave's prior bounding box as monotone integer keys, so each object's "does any prior of
   // this wave overlap it" test runs on the scalar unit: an object outside the box has
   // iw <= 0 or ih <= 0 for every prior of the wave (overlap 0 or -1, never a key, never a new
@@ -167,11 +183,22 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile(
   MRec *rrow = rec + (static_cast<int64_t>(b) * ntile + blockIdx.x) * Gmax;
   for (int gc = 0; gc < G; gc += kGc) {
     const int gn = min(G - gc, kGc);
+    if (gc > 0) {   // later chunks: their boxes into LDS (the previous chunk's end barrier is behind)
+      const Box4 bx = ld4(gt + 4 * static_cast<int64_t>(g0 + gc + min(tid & (kGc - 1), gn - 1)));
+      s_gt[tid] = make_float4(bx.a, bx.b, bx.c, bx.d);
+    }
+    __syncthreads();
     uint32_t ev = 0u;   // objects of this chunk evaluated by this wave (wave-uniform)
     for (int j0 = 0; j0 < gn; j0 += 4) {
-      Box4 t[4];   // uniform loads: scalar registers, four objects in flight
+      Box4 t[4];   // LDS broadcast reads made scalar: the wave-box test runs on the scalar unit
 #pragma unroll
-      for (int u = 0; u < 4; ++u) t[u] = ld4_uniform(gt + 4 * static_cast<int64_t>(g0 + gc + min(j0 + u, gn - 1)));
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = s_gt[min(j0 + u, gn - 1)];
+        t[u] = Box4{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
+                    __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y))),
+                    __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z))),
+                    __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w)))};
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int j = j0 + u;
@@ -681,7 +708,8 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
   do {                                                                                          \
     {                                                                                           \
       KernelTimer kt("k_match_tile", s, true);                                                  \
-      tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads), static_cast<size_t>(Gmax) * 4, s, \
+      tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads),                                \
+              static_cast<size_t>(Gmax > kMThreads ? Gmax : kMThreads) * 4, s,                      \
               gt_boxes, gt_labels, gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, \
               theta, obj, ovl, w.rec, w.tcount, n_pos, B, kt.span());                           \
     }                                                                                           \

@@ -472,10 +472,17 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   const int64_t i = rbase + tid;
   // this prior's loc / prior / mask loads go out with the score tile's (one memory round trip)
   const int64_t ic = valid ? i : rbase;
+  // Every prologue load is unconditional and lands in a plain register: a load under a branch
+  // (or a select of two loaded values) makes the wait-count insertion at the join wait for it
+  // BEFORE the score tile below is even issued — one whole memory round trip on every
+  // workgroup's critical path.  Absent priors / positive mask read a valid dummy address (this
+  // row's locs) and are ignored by the uses.
   const Box4 l = ld4(locs + 4 * ic);
-  const Box4 pr = a.box_type == SBOD_BOX_OFFSET ? ld4(a.priors + 4 * static_cast<int64_t>(valid ? p : p0))
-                                                : Box4{0.f, 0.f, 0.f, 0.f};
-  const uint8_t posv = *(a.pos != nullptr ? a.pos + ic : &kOneByte);   // branch-free: no early wait
+  const float *pp = a.box_type == SBOD_BOX_OFFSET ? a.priors + 4 * static_cast<int64_t>(valid ? p : p0) : locs + 4 * ic;
+  const Box4 pr = ld4(pp);
+  const auto *posp = (const __attribute__((address_space(1))) uint8_t *)(
+      a.pos != nullptr ? a.pos + ic : reinterpret_cast<const uint8_t *>(locs + 4 * ic));
+  const uint8_t posraw = *posp;
 #if SBOD_PREP_GLDS
   if (CM > 0 && (reinterpret_cast<uintptr_t>(scores + rbase * C) & 15) == 0) {
     // LDS-DMA: each wave-instruction copies 64 x 16 B of the tile straight into LDS (lane-linear,
@@ -531,7 +538,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
       }
     }
   }
-  const bool allowed = valid && posv != 0;
+  const bool allowed = valid && (a.pos == nullptr || posraw != 0);
   const int wv = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
   if constexpr (CM > 0) {
