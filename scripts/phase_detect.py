@@ -19,16 +19,14 @@ class Cfg(dict):
 dev = torch.device('cuda')
 Pn = prior_table('SSD512')
 pri = torch.from_numpy(Pn).to(dev)
-boxes, labels = synth.make_gt(32, seed=0)
-locs, scores = synth.make_preds(32, Pn.shape[0], 21, seed=0)
-det = scores.clone()
-det[:, :, 0] += 6.0
-locs, scores, det = locs.to(dev), scores.to(dev), det.to(dev)
+import bench  # noqa: E402
+batches = [bench.Batch(32, 100 * i, dev) for i in range(6)]   # rotated: inputs come from HBM
 crit = CR.MultiBoxLoss512(priors_cxcy=pri, config=Cfg(reg_weights=1.0, device=dev, n_classes=21,
                                                        reg_loss='diou', cls_loss='focal'))
-lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
-for _ in range(2):
-    crit(lo, sc, [b.to(dev) for b in boxes], [l.to(dev) for l in labels]).backward()
-    core.detect(locs, det, 0.01, 0.45, 200, pri)
-torch.cuda.synchronize()
+for i in range(8):      # the last iterations' lines are the steady state
+    bt = batches[i % 6]
+    print('== iteration %d' % i, flush=True)
+    crit(bt.locs, bt.scores, bt.boxes, bt.labels).backward()
+    core.detect(bt.locs.detach(), bt.det_scores, 0.01, 0.45, 200, pri)
+    torch.cuda.synchronize()
 print('done', flush=True)

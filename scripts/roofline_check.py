@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Cross-check a bench line's roofline against the rocprofv3 kernel trace of the same command.
+
+    python scripts/roofline_check.py gpurun_out/bench_TAG.json gpurun_out/prof_TAG/run_kernel_trace.csv \
+        [profiles/r3_roofline_check_TAG.json]
+
+For every HBM-bound kernel of the bench's ALGO_BYTES table, the dispatches of the bench
+workload (grid = B x ceil(P/256) workgroups of 256 threads, so the C2 bf16 step and other
+shapes in the same run are excluded) are averaged from the trace (End - Start, ns: the
+dispatch-level time rocprofv3 reports).  Written: per kernel, the rocprof average, the bench's
+event-timed average (kernel_us_per_step), algorithmic bytes per launch, the HBM fraction from
+each, and their relative difference; plus the headline kernel's line frac vs the rocprof frac.
+"""
+import csv
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def main(bench_json, trace_csv, out=None):
+    import bench as BM
+    line = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    cfg = line['config']
+    B, P, C = cfg.get('global_batch', 32) // line['n_gpus'], cfg['n_priors'], cfg['n_classes']
+    rl = line['roofline']
+    algo = {k: f({'B': B, 'P': P, 'C': C, 'n_cand': 0}) for k, f in BM.ALGO_BYTES.items()}
+    # k_det_prepare's candidate-key bytes depend on the workload's count: take them from the line
+    if rl['kernel'] == 'k_det_prepare':
+        algo['k_det_prepare'] = rl['algorithmic_bytes_per_launch']
+    else:
+        algo['k_det_prepare'] = line['step_algorithmic_bytes'] - BM.criterion_bytes(B, P, C)
+    grid_x = 256 * ((P + 255) // 256)
+    durs = {k: [] for k in algo}
+    with open(trace_csv) as f:
+        for r in csv.DictReader(f):
+            name = r['Kernel_Name']
+            for k in algo:
+                if (k + '<') in name or (k + '(') in name:
+                    if 'unsigned short' in name:      # the bf16 (C2) instantiation
+                        continue
+                    if int(r['Grid_Size_X']) == grid_x and int(r['Grid_Size_Y']) == B:
+                        durs[k].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+    res = {'bench': os.path.basename(bench_json), 'trace': os.path.basename(trace_csv),
+           'workload': {'B': B, 'P': P, 'C': C}, 'peak_GBps': BM.HBM_PEAK_GBS, 'kernels': {}}
+    for k, d in durs.items():
+        if not d:
+            continue
+        us = sum(d) / len(d) / 1e3
+        bus = line.get('kernel_us_per_step', {}).get(k)
+        e = {'dispatches': len(d), 'rocprof_avg_us': round(us, 3), 'bench_event_avg_us': bus,
+             'algorithmic_bytes': algo[k], 'frac_rocprof': round(algo[k] / (us * 1e-6) / 1e9 / BM.HBM_PEAK_GBS, 4)}
+        if bus:
+            e['frac_bench'] = round(algo[k] / (bus * 1e-6) / 1e9 / BM.HBM_PEAK_GBS, 4)
+            e['rel_diff'] = round(bus / us - 1.0, 4)
+        res['kernels'][k] = e
+    hk = rl['kernel']
+    if hk in res['kernels']:
+        fr = res['kernels'][hk]['frac_rocprof']
+        res['headline'] = {'kernel': hk, 'line_frac': rl['frac'], 'line_avg_us': rl['avg_us'],
+                           'rocprof_frac': fr, 'rel_diff': round(rl['frac'] / fr - 1.0, 4),
+                           'within_5pct': abs(rl['frac'] / fr - 1.0) <= 0.05}
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if out:
+        with open(out, 'w') as f:
+            f.write(txt + '\n')
+
+
+if __name__ == '__main__':
+    main(*sys.argv[1:4])

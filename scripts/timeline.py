@@ -29,24 +29,23 @@ def main():
     Pn = prior_table('SSD512')
     P = Pn.shape[0]
     pri = torch.from_numpy(Pn).to(dev)
-    boxes, labels = synth.make_gt(B, seed=0)
-    locs, scores = synth.make_preds(B, P, C, seed=0)
-    det = scores.clone()
-    det[:, :, 0] += 6.0
-    bx, lb = [b.to(dev) for b in boxes], [l.to(dev) for l in labels]
-    locs, scores, det = locs.to(dev), scores.to(dev), det.to(dev)
+    import bench
+    batches = [bench.Batch(B, 100 * i, dev) for i in range(6)]   # rotated: inputs come from HBM
     cfg = Cfg(reg_weights=1.0, device=dev, n_classes=C, reg_loss='diou', cls_loss='focal')
     crit = CR.MultiBoxLoss512(priors_cxcy=pri, config=cfg)
-    lo = locs.clone().requires_grad_(True)
-    sc = scores.clone().requires_grad_(True)
+    k = [0, 0]
 
     def crit_step():
-        lo.grad = None
-        sc.grad = None
-        crit(lo, sc, bx, lb).backward()
+        bt = batches[k[0] % 6]
+        k[0] += 1
+        bt.locs.grad = None
+        bt.scores.grad = None
+        crit(bt.locs, bt.scores, bt.boxes, bt.labels).backward()
 
     def det_step():
-        core.detect(locs, det, 0.01, 0.45, 200, pri)
+        bt = batches[k[1] % 6]
+        k[1] += 1
+        core.detect(bt.locs.detach(), bt.det_scores, 0.01, 0.45, 200, pri)
 
     lib = L.lib()
     kernels = [('match', 5, 'k_match_tile', crit_step, B * ((P + 255) // 256)),

@@ -623,18 +623,25 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     SEG_PHASE(2);
     prep_slots(a, b, C, tid, s_balf, s_wbf);
     SEG_PHASE(3);
-    while (cmask) {
-      const int c = KN - 1 - __builtin_ctz(cmask);
-      cmask &= cmask - 1u;
-      const unsigned long long bal = s_bal(wv, c);
-      // the emitted probability: the same operations as above on the raw LDS row (bit-identical)
-      const float pc = softmax ? __builtin_amdgcn_exp2f((row[c] - m) * 1.4426950408889634f) * rs : fast_sigmoid(row[c]);
-      // (plain store: these 8-byte scattered writes must merge into full lines in L2 first —
-      // streamed through they cost 1.7x the kernel time)
-      const uint32_t slot = s_wb(wv, c) + __popcll(bal & lt);
-      if (slot < static_cast<uint32_t>(P))   // always, with counters zero on entry (memory-safe otherwise)
-        a.cand[(static_cast<int64_t>(b) * C + c) * P + slot] = make_key(pc, static_cast<uint32_t>(p));
+    // Emission, one class at a time in a uniform loop: the wave's mask for the class is in
+    // scalar registers (bals), its slot base one LDS word made scalar, and the emitting lanes'
+    // probability is r[k] itself (computed once above, still in registers) — no divergent
+    // per-lane loop over candidate classes and no LDS row re-read per candidate (phase clocks:
+    // this phase was ~6K of ~16K cycles per workgroup in the per-lane form).
+    // (plain stores: these 8-byte scattered writes must merge into full lines in L2 first —
+    // streamed through they cost 1.7x the kernel time)
+    unsigned long long *cb = a.cand + static_cast<int64_t>(b) * C * P;
+#pragma unroll
+    for (int k = 1; k < KN; ++k) {
+      if (k < C && bals[k] != 0ull) {
+        const uint32_t base = __builtin_amdgcn_readfirstlane(s_wb(wv, k));
+        const uint32_t slot = base + __popcll(bals[k] & lt);
+        // slot < P always with counters zero on entry (memory-safe otherwise)
+        if (((bals[k] >> lane) & 1ull) && slot < static_cast<uint32_t>(P))
+          cb[static_cast<int64_t>(k) * P + slot] = make_key(r[k], static_cast<uint32_t>(p));
+      }
     }
+    (void)cmask;
   } else {
     SEG_PHASE(2);
     for (int c = 1; c < C; ++c) {

@@ -102,5 +102,5 @@ def test_c4_refinedet_full_size_vs_oracle():
     ref.backward()
     np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
     for name, t, r in zip(('arm_locs', 'arm_scores', 'odm_locs', 'odm_scores'), ts, rs):
-        np.testing.assert_allclose(t.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-3, atol=1e-8,
+        np.testing.assert_allclose(t.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-4, atol=1e-8,
                                    err_msg=name)

@@ -52,5 +52,5 @@ def test_c1_ssd300_voc_batch_step(tmp_path, reg, cls):
     ref = LR.criterion('ssd300', P, rl, rs, boxes, labels, oreg, cls)
     ref.backward()
     np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
-    np.testing.assert_allclose(lo.grad.cpu().numpy(), rl.grad.numpy(), rtol=1e-3, atol=1e-8)
-    np.testing.assert_allclose(sc.grad.cpu().numpy(), rs.grad.numpy(), rtol=1e-3, atol=1e-8)
+    np.testing.assert_allclose(lo.grad.cpu().numpy(), rl.grad.numpy(), rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(sc.grad.cpu().numpy(), rs.grad.numpy(), rtol=1e-4, atol=1e-8)

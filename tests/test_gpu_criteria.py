@@ -57,13 +57,13 @@ def test_criteria_golden(name):
     loss, gl, gs = _run(kind, P, locs, scores, boxes, labels, reg, cls, C)
     np.testing.assert_allclose(loss, d['loss'], rtol=RTOL)
     if 'grad_locs' in d.files:
-        np.testing.assert_allclose(gl, d['grad_locs'], rtol=1e-3, atol=1e-7)
-        np.testing.assert_allclose(gs, d['grad_scores'], rtol=1e-3, atol=1e-7)
+        np.testing.assert_allclose(gl, d['grad_locs'], rtol=1e-4, atol=1e-7)
+        np.testing.assert_allclose(gs, d['grad_scores'], rtol=1e-4, atol=1e-7)
     else:
         np.testing.assert_allclose(gl.reshape(-1, 4)[d['grad_locs_rows']], d['grad_locs_at_rows'],
-                                   rtol=1e-3, atol=1e-8)
+                                   rtol=1e-4, atol=1e-8)
         np.testing.assert_allclose(gs.reshape(-1, C)[d['grad_scores_rows']], d['grad_scores_at_rows'],
-                                   rtol=1e-3, atol=1e-8)
+                                   rtol=1e-4, atol=1e-8)
         np.testing.assert_allclose(np.abs(gl).astype(np.float64).sum(), d['grad_locs_abssum'], rtol=1e-4)
         np.testing.assert_allclose(np.abs(gs).astype(np.float64).sum(), d['grad_scores_abssum'], rtol=1e-4)
 
@@ -82,8 +82,8 @@ def test_criteria_vs_oracle_full(kind, arch, B, reg, cls):
     ref = LR.criterion(kind, P, lo, sc, boxes, labels, reg, cls)
     ref.backward()
     np.testing.assert_allclose(loss, ref.item(), rtol=RTOL)
-    np.testing.assert_allclose(gl, lo.grad.numpy(), rtol=1e-3, atol=1e-8)
-    np.testing.assert_allclose(gs, sc.grad.numpy(), rtol=1e-3, atol=1e-8)
+    np.testing.assert_allclose(gl, lo.grad.numpy(), rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(gs, sc.grad.numpy(), rtol=1e-4, atol=1e-8)
 
 
 def test_refinedet_golden():
@@ -98,7 +98,7 @@ def test_refinedet_golden():
     loss.backward()
     np.testing.assert_allclose(loss.item(), d['loss'], rtol=RTOL)
     for n, t in zip(['arm_locs', 'arm_scores', 'odm_locs', 'odm_scores'], ts):
-        np.testing.assert_allclose(t.grad.cpu().numpy(), d[n + '_grad'], rtol=1e-3, atol=1e-7)
+        np.testing.assert_allclose(t.grad.cpu().numpy(), d[n + '_grad'], rtol=1e-4, atol=1e-7)
 
 
 def test_grad_scale_and_determinism():

@@ -56,8 +56,8 @@ def _criterion(arch, B, reg, cls, seed):
     ref = LR.criterion('retina', P, rl, rs, boxes, labels, reg, cls)
     ref.backward()
     np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
-    np.testing.assert_allclose(lo.grad.cpu().numpy(), rl.grad.numpy(), rtol=1e-3, atol=1e-8)
-    np.testing.assert_allclose(sc.grad.cpu().numpy(), rs.grad.numpy(), rtol=1e-3, atol=1e-8)
+    np.testing.assert_allclose(lo.grad.cpu().numpy(), rl.grad.numpy(), rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(sc.grad.cpu().numpy(), rs.grad.numpy(), rtol=1e-4, atol=1e-8)
 
 
 @pytest.mark.parametrize('reg,cls', [('diou', 'focal'), ('smoothl1', 'ce')])
