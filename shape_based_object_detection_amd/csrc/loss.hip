@@ -447,12 +447,26 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
         zmin = (in_row(k) && r[k] < zmin) ? r[k] : zmin;
       }
       const float zt = row[c];
-      // the exponentials are summed here and recomputed (bit-identically) from the LDS row in
-      // the gradient loops, so r[] is dead before the loss math (no spills around powf)
       float s = 0.f;
+      // focal: the exponentials stay in registers for the gradient (computed once), packed
+      // fp32 for the elementwise steps — this pass is VALU-issue-bound (a v_exp costs 8 cycles
+      // of a wave's issue, a plain or packed op 4), every wave of the round computing at once
+      typedef float f2 __attribute__((ext_vector_type(2)));
       if constexpr (CLS == SBOD_CLS_FOCAL) {
+        // the exponentials replace the logits in the LDS row (the gradient pass reads them back:
+        // LDS operations instead of a second v_exp per class, and no register array live across
+        // the loss math's powf / logf)
+        const f2 nm2 = {-m, -m}, l2 = {1.4426950408889634f, 1.4426950408889634f};
+        f2 acc2 = {0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < CM; ++k) s += fast_exp(r[k] - m);   // padding: exp(-inf) = 0
+        for (int k = 0; k < CM; k += 2) {   // CM is a multiple of 8
+          const f2 t = (f2{r[k], r[k + 1]} + nm2) * l2;
+          const f2 ex = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};   // padding: 0
+          acc2 += ex;
+          if (in_row(k)) row[k] = ex.x;
+          if (in_row(k + 1)) row[k + 1] = ex.y;
+        }
+        s = acc2.x + acc2.y;
       } else {
         // CE feeds the hard-negative selection (a ranking): the accurate exp keeps its values
         // within an ulp of the reference's so near-ties at the top-k boundary do not move
@@ -476,14 +490,32 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
             dq = a.afg * (-a.gamma * powg1(om, a.gamma) * -lq - powg(om, a.gamma) / q);
           }
           // 0 * log 0 in the reference when any class probability is exactly 0: decided on the
-          // smallest logit with the accurate exp (underflow is monotone in the logit)
-          if (!(expf(zmin - m) * inv > 0.f)) loss = __builtin_nanf("");
+          // smallest logit with the accurate exp (underflow is monotone in the logit).  Above
+          // -80 no probability can underflow (exp >= 1.8e-35, 1 / sum >= 1 / C), so the accurate
+          // exp runs only in rows that come near it (a branch the wave skips when no lane does).
+          const float zd = zmin - m;
+          bool nanrow = false;
+          if (zd < -80.f) nanrow = !(expf(zd) * inv > 0.f);
+          if (nanrow) loss = __builtin_nanf("");
           conf_l += loss;
           if (grad) {
-            const float kq = dq * q * scale;
+            if (loss != loss) {
 #pragma unroll
-            for (int k = 0; k < CM; ++k)
-              if (in_row(k)) row[k] = loss != loss ? loss : kq * ((k == c ? 1.f : 0.f) - fast_exp(row[k] - m) * inv);
+              for (int k = 0; k < CM; ++k)
+                if (in_row(k)) row[k] = loss;
+            } else {
+              // kq * (onehot - p), p = e * inv (the same values the loss used), two classes per op
+              const float kq = dq * q * scale;
+              const f2 inv2 = {inv, inv}, kq2 = {kq, kq};
+#pragma unroll
+              for (int k = 0; k < CM; k += 2) {
+                const f2 pp = f2{in_row(k) ? row[k] : 0.f, in_row(k + 1) ? row[k + 1] : 0.f} * inv2;
+                const f2 oh = {k == c ? 1.f : 0.f, k + 1 == c ? 1.f : 0.f};
+                const f2 g = (oh - pp) * kq2;
+                if (in_row(k)) row[k] = g.x;
+                if (in_row(k + 1)) row[k + 1] = g.y;
+              }
+            }
           }
         } else if (grad) {
 #pragma unroll
