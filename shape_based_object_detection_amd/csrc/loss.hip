@@ -327,11 +327,13 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
                                                      T *__restrict__ glocs, T *__restrict__ gsc) {
   extern __shared__ float s_sc[];
   __shared__ float s_red[16];
+  __shared__ int2 s_plist[kLTile];        // positive rows: wave w's at [64 w, 64 w + count)
+  __shared__ int s_wcnt[kLTile / 64];
   STAMP_BEGIN();
   span_begin(a.span);
   PHASE_DECL;
   SEG_PHASE(0);
-  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x;
+  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int P = a.P, C = a.C;
   const int np = min(kLTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
@@ -369,39 +371,66 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   const float n = static_cast<float>(*a.npos_total);
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
   const bool grad = gsc != nullptr;
-  __syncthreads();
-  SEG_PHASE(1);
-  float conf_l = 0.f, loc_l = 0.f;
+  // The row's class decision before the barrier, so the tile's positive rows can be listed.
+  int c = 0;
+  bool negrow = false, easy = false, pos = false;
   if (valid) {
-    const int p = p0 + tid;
-    const int64_t i = ic;
-    int c = v < a.thr ? 0 : static_cast<int>(labg);
+    c = v < a.thr ? 0 : static_cast<int>(labg);
     if (a.flags & SBOD_MATCH_BINARY) c = c > 0 ? 1 : 0;
-    const bool negrow = v < a.nthr;
-    bool easy = false;
+    negrow = v < a.nthr;
     if (odm) {  // RefineDet512.py:894-899
-      const float z0 = a.arm_scores[2 * i], z1 = a.arm_scores[2 * i + 1];
+      const float z0 = a.arm_scores[2 * ic], z1 = a.arm_scores[2 * ic + 1];
       const float m = fmaxf(z0, z1);
       const float e0 = expf(z0 - m), e1 = expf(z1 - m);
       easy = e1 / (e0 + e1) < a.theta;
     }
-    const bool pos = c > 0 && !easy;
-    // ---------------- box regression (first: its prologue loads die before the class row is live)
-    float gl[4] = {0.f, 0.f, 0.f, 0.f};
-    if (pos) {   // lc, pri_cxcy, tb were loaded in the prologue
+    pos = c > 0 && !easy;
+  }
+  {   // each wave lists its positive rows (tile row, object) in its own 64 slots
+    const unsigned long long bal = __ballot(pos);
+    if (pos) s_plist[64 * wv + __popcll(bal & ((1ull << lane) - 1ull))] = make_int2(tid, objv);
+    if (lane == 0) s_wcnt[wv] = __popcll(bal);
+  }
+  __syncthreads();
+  SEG_PHASE(1);
+  float conf_l = 0.f, loc_l = 0.f;
+  // ---------------- box regression, compacted: positives are ~1-3 % of the rows, yet with one
+  // per wave the whole wave would run the DIoU / encode path (a dozen IEEE divisions, exps).
+  // The tile's positives are packed 64 per chunk and chunk k runs on wave k % 4 (usually one
+  // chunk): it re-reads its rows' loc / prior / GT box (L2 hits) and writes their gradient
+  // rows; every other row's gradient row is the zero written below by its own thread.
+  {
+    const int n0 = s_wcnt[0], n1 = s_wcnt[1], n2 = s_wcnt[2], n3 = s_wcnt[3];
+    const int total = n0 + n1 + n2 + n3;
+    for (int e0 = 64 * wv; e0 < total; e0 += kLTile) {
+      const int e = e0 + lane;
+      if (e >= total) break;
+      // entry e of the concatenation of the four waves' lists
+      const int ww = e < n0 ? 0 : (e < n0 + n1 ? 1 : (e < n0 + n1 + n2 ? 2 : 3));
+      const int r0 = e - (ww == 0 ? 0 : (ww == 1 ? n0 : (ww == 2 ? n0 + n1 : n0 + n1 + n2)));
+      const int2 pe = s_plist[64 * ww + r0];
+      const int64_t i = rbase + pe.x;
+      Box4 l;
+      if constexpr (sizeof(T) == 4)
+        l = ld4(reinterpret_cast<const float *>(locs) + 4 * i);
+      else
+        l = Box4{ldf(locs + 4 * i), ldf(locs + 4 * i + 1), ldf(locs + 4 * i + 2), ldf(locs + 4 * i + 3)};
+      const Box4 pc = ld4(a.priors + 4 * static_cast<int64_t>(p0 + pe.x));
+      const Box4 t = ld4(a.gt + 4 * static_cast<int64_t>(offb + pe.y));
+      float gl[4] = {0.f, 0.f, 0.f, 0.f};
       if (a.reg == SBOD_REG_DIOU) {  // SSD512.py:579-581: IouLoss(Diou) on decoded boxes
-        const Box4 d = decode_tenfive_xy(lc, pri_cxcy);
-        const OvOut r = aligned_overlap(SBOD_OV_DIOU, d, tb, grad);
+        const Box4 d = decode_tenfive_xy(l, pc);
+        const OvOut r = aligned_overlap(SBOD_OV_DIOU, d, t, grad);
         loc_l += 1.f - r.v;
         if (grad) {
           const float s = -a.reg_weight / n;
           const float gb[4] = {r.g[0] * s, r.g[1] * s, r.g[2] * s, r.g[3] * s};
-          decode_backward(gb, lc, pri_cxcy, gl);
+          decode_backward(gb, l, pc, gl);
         }
       } else {  // smooth-L1 (Loss.py:213-217) or L1 on encoded targets
-        const Box4 pr = odm ? xy_to_cxcy(decode_tenfive_xy(ld4(a.arm_locs + 4 * i), pri_cxcy)) : pri_cxcy;
-        const Box4 e = encode_tenfive(xy_to_cxcy(tb), pr);
-        const float lv[4] = {lc.a, lc.b, lc.c, lc.d}, ev[4] = {e.a, e.b, e.c, e.d};
+        const Box4 pr = odm ? xy_to_cxcy(decode_tenfive_xy(ld4(a.arm_locs + 4 * i), pc)) : pc;
+        const Box4 en = encode_tenfive(xy_to_cxcy(t), pr);
+        const float lv[4] = {l.a, l.b, l.c, l.d}, ev[4] = {en.a, en.b, en.c, en.d};
         const bool l1 = a.reg == SBOD_REG_L1;
         const float beta = 1.f / 9.f;
         const float s = l1 ? a.reg_weight / (4.f * n) : a.reg_weight / n;
@@ -422,13 +451,24 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
           }
         }
       }
+      if (glocs) {
+        if constexpr (sizeof(T) == 4) {
+          st4_nt(reinterpret_cast<float *>(glocs) + 4 * i, Box4{gl[0], gl[1], gl[2], gl[3]});
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
+        }
+      }
     }
-    if (glocs) {
+  }
+  if (valid) {
+    const int64_t i = ic;
+    if (glocs && !pos) {
       if constexpr (sizeof(T) == 4) {
-        st4_nt(reinterpret_cast<float *>(glocs) + 4 * i, Box4{gl[0], gl[1], gl[2], gl[3]});
+        st4_nt(reinterpret_cast<float *>(glocs) + 4 * i, Box4{0.f, 0.f, 0.f, 0.f});
       } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
+        for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, 0.f);
       }
     }
     // ---------------- classification
