@@ -93,13 +93,19 @@ def test_against_oracle(B, C, O, H, W, ks, pad, stride, mod, off_scale):
     _oracle_case(B, C, O, H, W, ks, pad, stride, mod, off_scale, seed=B * 1000 + C * 10 + ks)
 
 
-def test_full_channel_case_against_oracle():
+def test_c4_dcn_full_channels_vs_oracle():
     # C4 channel count (256 -> 256) at a spatial size the CPU oracle finishes in seconds
     _oracle_case(2, 256, 256, 16, 16, 3, 1, 1, True, 1.0, seed=4)
 
 
+def test_c4_dcn_b16_8x8_full_shape_vs_oracle():
+    # C4's smallest map at its full shape (B=16, 256 -> 256, 3x3, 8x8) with random offsets and
+    # modulation, forward and all four gradients against the oracle
+    _oracle_case(16, 256, 256, 8, 8, 3, 1, 1, True, 1.0, seed=88)
+
+
 @pytest.mark.parametrize('H,stride', [(64, 1), (32, 1), (16, 2), (8, 1)])
-def test_zero_offset_equals_conv_at_full_size(H, stride):
+def test_c4_dcn_zero_offset_equals_conv_at_full_size(H, stride):
     """Size-independent property at BASELINE C4 sizes (B=16, 256->256): with zero offsets and no
     modulation every sample lands on an integer grid point, so DeformConv2d(k=3, pad=1, stride)
     is exactly conv2d(x, W, stride, padding=1); gradients w.r.t. x and W must agree too."""
