@@ -70,8 +70,10 @@ def parse(argv=None):
     ap.add_argument('--eager', action='store_true', help='no hipGraph: launch every call each step')
     ap.add_argument('--one-stream', action='store_true',
                     help='graph mode: one graph per step (criterion and detect in stream order)')
-    ap.add_argument('--priority', choices=('none', 'detect', 'criterion'), default='criterion',
+    ap.add_argument('--priority', choices=('none', 'detect', 'criterion'), default='detect',
                     help='graph mode: which of the two streams gets the high HIP stream priority')
+    ap.add_argument('--order', choices=('criterion_first', 'detect_first'), default='criterion_first',
+                    help='graph mode: which graph of a step is submitted first')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-dcn', action='store_true')
     ap.add_argument('--batches', type=int, default=6,
@@ -185,28 +187,51 @@ def cpu_baseline(B, threads_all, det_images_one=8):
 
 # ----------------------------------------------------------------------------- DCN (config C4)
 def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
-    """DeformConv2d (a14) forward+backward at config C4's largest map: TF/s of the three
-    contractions (fwd, d-cols, d-weight: 3 x 2*M*O*C*9) against the fp32 MFMA peak."""
+    """DeformConv2d (a14) forward+backward at one of config C4's maps: TF/s of the three
+    contractions (fwd, d-cols, d-weight: 3 x 2*M*O*C*9) against the fp32 MFMA peak.  The step is
+    out = deform_conv2d(...) and the four input gradients by torch.autograd.grad (as after a
+    zero_grad(set_to_none=True): no accumulation kernels); timed replayed from one hipGraph
+    (``ms``, the primary figure) and launched eagerly through autograd (``eager_ms``: the
+    per-call host cost shows at the small maps)."""
     g = torch.Generator(device=dev).manual_seed(H)
     x = torch.randn(B, C, H, H, device=dev, generator=g).requires_grad_(True)
     off = torch.randn(B, 18, H, H, device=dev, generator=g).requires_grad_(True)
     ml = torch.randn(B, 9, H, H, device=dev, generator=g).requires_grad_(True)
     w = (torch.randn(O, C, 3, 3, device=dev, generator=g) / 48).requires_grad_(True)
     gout = torch.randn(B, O, H, H, device=dev, generator=g)
-    for _ in range(2):
-        core.deform_conv2d(x, off, ml, w).backward(gout)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        core.deform_conv2d(x, off, ml, w).backward(gout)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    tf = 3 * 2.0 * B * H * H * O * C * 9 / ms / 1e9
+    params = (x, off, ml, w)
+
+    def step():
+        return torch.autograd.grad(core.deform_conv2d(x, off, ml, w), params, gout)
+
+    def clock(fn):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / iters
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    graph.replay()
+    ms = clock(graph.replay)
+    eager = clock(step)
+    fl = 3 * 2.0 * B * H * H * O * C * 9
+    tf = fl / ms / 1e9
     return {'config': 'C4 DeformConv2d B=%d %d->%d 3x3 %dx%d fwd+bwd fp32' % (B, C, O, H, H),
-            'ms': round(ms, 3), 'tflops': round(tf, 2), 'peak_tflops': F32_MFMA_PEAK_TFS,
-            'mfma_frac': round(tf / F32_MFMA_PEAK_TFS, 4)}
+            'ms': round(ms, 4), 'tflops': round(tf, 2), 'peak_tflops': F32_MFMA_PEAK_TFS,
+            'mfma_frac': round(tf / F32_MFMA_PEAK_TFS, 4), 'timing': 'hipGraph replay',
+            'eager_ms': round(eager, 4), 'eager_mfma_frac': round(fl / eager / 1e9 / F32_MFMA_PEAK_TFS, 4)}
 
 
 # ----------------------------------------------------------------------------- the step
@@ -219,7 +244,7 @@ class Step:
     buffer and the two-deep pipeline (submit step k, then collect step k-1) needs no copies."""
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
-                 dtype=torch.float32):
+                 dtype=torch.float32, order='criterion_first'):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -241,6 +266,7 @@ class Step:
         self.cap_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'criterion' else 0)
         self.det_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'detect' else 0)
         self.two = two_streams
+        self.detect_first = order == 'detect_first'
         self.graph = None
         self.use_graph = graph
         self.capture_error = None
@@ -335,8 +361,10 @@ class Step:
             self.fast = []
             for ga, gb, _, h in self.slots:
                 h.replayed(self.det_stream)          # creates the event (recorded once here)
-                self.fast.append((core.graph_launches([(ga, self.cap_stream), (gb, self.det_stream)]),
-                                  h._event.cuda_event, self.det_stream.cuda_stream))
+                pairs = [(ga, self.cap_stream), (gb, self.det_stream)]
+                if self.detect_first:
+                    pairs.reverse()
+                self.fast.append((core.graph_launches(pairs), h._event.cuda_event, self.det_stream.cuda_stream))
             torch.cuda.synchronize()
         self.k = 0
         self.pending = None
@@ -348,7 +376,9 @@ class Step:
         ga, gb, loss, h = self.slots[i]
         if self.fast is not None:
             launches, ev, ev_stream = self.fast[i]
-            if self.stage.stage_and_replay(bt.boxes, bt.labels, launches, ev, ev_stream) is not None:
+            # GT packing on the criterion's stream, whichever graph is submitted first
+            if self.stage.stage_and_replay(bt.boxes, bt.labels, launches, ev, ev_stream,
+                                           pack_stream=self.cap_stream.cuda_stream) is not None:
                 return loss, h.rearmed()
         if gb is None:
             with torch.cuda.stream(self.cap_stream):
@@ -393,11 +423,11 @@ class Step:
 
 def c2_figure(dev, steps, warmup, B=16, n_batches=12):
     """Config C2 (SSD512 batch=16 bf16 on 1 GPU): the same captured step with bf16 locs / scores
-    (and bf16 gradients) for the criterion, and the detect on the bf16 activations (widened to
-    fp32 inside the graph, as detect's fp32 kernels take them).  ``n_batches`` resident batches
+    (and bf16 gradients) for the criterion, and the detect reading the bf16 activations directly
+    (SBOD_DETECT_INPUT_BF16: widened exactly on load, no fp32 copies).  ``n_batches`` resident batches
     (~23 MB touched per step) keep the rotation above the Infinity Cache.  Algorithmic bytes of
     the criterion at 2 B/element: SURVEY §8(d) (16.56 MB at B=16)."""
-    st = Step(dev, B, 0, 1, graph=True, n_batches=n_batches, dtype=torch.bfloat16)
+    st = Step(dev, B, 0, 1, graph=True, n_batches=n_batches, dtype=torch.bfloat16, priority='detect')
     for _ in range(max(warmup - 1, 1)):
         st.eager_split()
     torch.cuda.synchronize()
@@ -410,7 +440,7 @@ def c2_figure(dev, steps, warmup, B=16, n_batches=12):
     del st
     torch.cuda.synchronize()
     return {'config': 'C2 SSD512 batch=%d bf16: MultiBoxLoss512(DIoU+focal) fwd+bwd in bf16 + detect '
-                      '(bf16 activations widened to fp32), captured, %d resident batches' % (B, n_batches),
+                      '(bf16 activations read in place), captured, %d resident batches' % (B, n_batches),
             'ms_per_step': round(ms, 4), 'images_per_s': round(B / (ms * 1e-3), 1),
             'criterion_algorithmic_bytes': crit_b, 'steps': steps}
 
@@ -500,7 +530,7 @@ def main():
     L.lib()
     B = a.batch
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
-              n_batches=a.batches)
+              n_batches=a.batches, order=a.order)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -600,7 +630,7 @@ def main():
         'step_algorithmic_bytes': step_bytes,
         'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        'graph': st.use_graph, 'stream_priority': a.priority,
+        'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }

@@ -268,13 +268,16 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
  *   sbod_detect_counter_bytes(B, C) bytes are zero on entry (e.g. the workspace was allocated
  *   zeroed); every call leaves them zero again, so repeated calls (and a captured hipGraph)
  *   need no memset.  Without the flag the call zeroes them itself (one memset).
+ *   SBOD_DETECT_INPUT_BF16 — locs and scores hold bf16 (C <= 32): each value is widened to fp32
+ *   exactly on load, so the results equal those of the fp32 call on the widened tensors (no
+ *   widened copies in HBM).  Without it both are fp32.
  * Workspace: sbod_detect_workspace_bytes(B, P, C). */
 enum { SBOD_BOX_OFFSET = 0, SBOD_BOX_CENTER = 1, SBOD_BOX_CORNER = 2 };
-enum { SBOD_DETECT_COUNTERS_ZEROED = 1 };
+enum { SBOD_DETECT_COUNTERS_ZEROED = 1, SBOD_DETECT_INPUT_BF16 = 2 };
 size_t sbod_detect_counter_bytes(int B, int C);
 enum { SBOD_ACT_SOFTMAX = 0, SBOD_ACT_SIGMOID = 1 };
 size_t sbod_detect_workspace_bytes(int B, int P, int C);
-int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
+int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
                     const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
                     float min_score, float max_overlap, int top_k, float final_nms, int window,
                     int flags, float *det_boxes, int64_t *det_labels, float *det_scores,

@@ -19,7 +19,9 @@ N = 200
 dev = torch.device('cuda', 0)
 torch.cuda.set_device(dev)
 L.lib()
-st = bench.Step(dev, 32, 0, 1, graph=True, two_streams=True)
+C2 = '--c2' in sys.argv      # config C2: SSD512 B=16 bf16, 12 resident batches (bench c2_figure)
+st = (bench.Step(dev, 16, 0, 1, graph=True, n_batches=12, dtype=torch.bfloat16) if C2 else
+      bench.Step(dev, 32, 0, 1, graph=True, two_streams=True))
 for _ in range(3):
     st.eager_split()
 torch.cuda.synchronize()
@@ -52,7 +54,7 @@ def rot(fn):
     return f
 
 
-out = {'resident_batches': R}
+out = {'config': 'C2 bf16 B=16' if C2 else 'SSD512 fp32 B=32', 'resident_batches': R}
 with torch.cuda.stream(st.cap_stream):
     out['criterion_graph_only'] = wall(rot(lambda i: st.slots[i][0].replay()))
 with torch.cuda.stream(st.det_stream):

@@ -174,9 +174,11 @@ class GtStaging:
             self._stage_host(boxes, labels, counts)
         return GtPack(self.boxes, self.labels, self.offsets, counts, gmax=self.capacity)
 
-    def stage_and_replay(self, boxes, labels, launches, event=0, event_stream=0, allow_empty=False):
-        """One-call submit of a captured step: ``stage`` of device lists on the first launch's
-        stream, then every (graph exec, stream) of ``launches`` (from ``graph_launches``), then
+    def stage_and_replay(self, boxes, labels, launches, event=0, event_stream=0, allow_empty=False,
+                         pack_stream=None):
+        """One-call submit of a captured step: ``stage`` of device lists on ``pack_stream`` (a raw
+        hipStream_t; default the first launch's stream — the graph that reads the GT must be on
+        it), then every (graph exec, stream) of ``launches`` (from ``graph_launches``), then
         ``event`` (a raw hipEvent_t, 0 for none) recorded on ``event_stream`` — all in C++
         (_sbodhost.stage_and_replay).  Returns the GtPack, or None when the batch or the build
         needs the Python path (nothing was launched then).
@@ -192,8 +194,8 @@ class GtStaging:
         dev = self.device.index or 0
         r = ext.stage_and_replay(boxes, labels, self.boxes.shape[0], self.capacity, dev,
                                  self.boxes.data_ptr(), self.labels.data_ptr(), self.offsets.data_ptr(),
-                                 launches[0][1], allow_empty, launches, event or None, event_stream or None,
-                                 L._raw_stream(dev) or None)
+                                 pack_stream if pack_stream is not None else launches[0][1], allow_empty,
+                                 launches, event or None, event_stream or None, L._raw_stream(dev) or None)
         if r is None:
             return None
         if type(r) is int:
@@ -588,10 +590,10 @@ def reserve_count_slots(dev, B, n):
 
 
 def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn, out,
-                   dbg, ws, nb, cnt_host, window):
+                   dbg, ws, nb, cnt_host, in_flags, window):
     out_b, out_l, out_s, cnt = out
     need = L.lib().sbod_detect_counter_bytes(B, C)
-    flags = _zeroed_flag(ws, need, L.DETECT_COUNTERS_ZEROED, 'detect')
+    flags = _zeroed_flag(ws, need, L.DETECT_COUNTERS_ZEROED, 'detect') | in_flags
     # a call that fails part-way can leave its counters non-zero (k_det_prepare has added to
     # them, k_det_merge never ran): the workspace counts as clean again only after a success
     _CLEAN.pop(ws.data_ptr(), None)
@@ -618,9 +620,15 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     if top_k <= 0:
         raise ValueError('top_k must be positive')
     dev = scores.device
-    sc = scores.contiguous().float()
     in_place = box_type not in ('offset', 'center')
-    lc = locs if (locs.is_contiguous() and locs.dtype == torch.float32) else locs.contiguous().float()
+    if scores.dtype == torch.bfloat16 and locs.dtype == torch.bfloat16 and C <= 32:
+        # bf16 activations read as they are (widened exactly in the kernel, SBOD_DETECT_INPUT_BF16):
+        # the results of detect on their fp32 values, without widened copies
+        sc, lc, in_flags = scores.contiguous(), locs.contiguous(), L.DETECT_INPUT_BF16
+    else:
+        sc = scores.contiguous().float()
+        lc = locs if (locs.is_contiguous() and locs.dtype == torch.float32) else locs.contiguous().float()
+        in_flags = 0
     pri = priors_cxcy.contiguous().float() if priors_cxcy is not None else None
     pm = pos_mask.contiguous().to(torch.uint8) if pos_mask is not None else None
     out_b = torch.empty(B, top_k, 4, dtype=torch.float32, device=dev)
@@ -647,7 +655,7 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     else:
         cnt_host, ev = _count_slot(dev, B)
     launch = (lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn,
-              (out_b, out_l, out_s, cnt), (dbg_p, dbg_b), ws, nb, cnt_host)
+              (out_b, out_l, out_s, cnt), (dbg_p, dbg_b), ws, nb, cnt_host, in_flags)
     _detect_launch(*launch, window)
     if not capture:
         ev.record(torch.cuda.current_stream(dev))

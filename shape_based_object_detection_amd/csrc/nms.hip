@@ -447,17 +447,36 @@ __device__ __forceinline__ void prep_slots(const DetArgs &a, int b, int C, int t
 // exponentials and the sum need no per-slot guards); CM == 0: any C, rows in LDS.  CE > 0: the
 // class count is the compile-time CE (VOC's 21), so no slot needs a padding select or a k < C
 // test, and only CE exponentials are evaluated.
-template <int CM, int CE>
-__global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__restrict__ locs,
-                                                        const float *__restrict__ scores) {
-  // dynamic LDS: score tile [kDTile][C] f32 | ballots [kDTile/64][C] u64 | slot bases [C] u32,
+// Input element types: float, or uint16_t holding bf16 bit patterns (widened exactly on load, so
+// every later decision sees the fp32 value of the bf16 activation — the same values the fp32 path
+// gets from a widened copy).
+__device__ __forceinline__ float widen(float v) { return v; }
+__device__ __forceinline__ float widen(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+__device__ __forceinline__ Box4 ld_box(const float *p) { return ld4(p); }
+__device__ __forceinline__ Box4 ld_box(const uint16_t *p) {
+  const uint2 v = *reinterpret_cast<const uint2 *>(p);
+  return Box4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+              __uint_as_float(v.y & 0xffff0000u)};
+}
+__device__ __forceinline__ void st_box(float *p, Box4 b) { st4(p, b); }
+__device__ __forceinline__ void st_box(uint16_t *p, Box4 b) {   // values that came from bf16: exact
+  *reinterpret_cast<uint2 *>(p) = make_uint2((__float_as_uint(b.a) >> 16) | (__float_as_uint(b.b) & 0xffff0000u),
+                                             (__float_as_uint(b.c) >> 16) | (__float_as_uint(b.d) & 0xffff0000u));
+}
+
+template <int CM, int CE, typename T = float>
+__global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, T *__restrict__ locs,
+                                                        const T *__restrict__ scores) {
+  static_assert(CM > 0 || sizeof(T) == 4, "k_det_prepare: bf16 input takes the register-row path");
+  // dynamic LDS: score tile [kDTile][C] T | ballots [kDTile/64][C] u64 | slot bases [C] u32,
   // sized to C so 6+ workgroups fit per CU (one round for B x ceil(P/256) workgroups at B=32)
   extern __shared__ float s_sc[];
   STAMP_BEGIN();
   span_begin(a.span);
   const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
   const int P = a.P, C = CE > 0 ? CE : a.C;
-  unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_sc + kDTile * C);
+  T *const s_tile = reinterpret_cast<T *>(s_sc);
+  unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_tile + kDTile * C);
   uint32_t *s_wbf = reinterpret_cast<uint32_t *>(s_balf + (kDTile / 64) * C);   // per-wave slot bases
 #define s_bal(w, c) s_balf[(w) * C + (c)]
 #define s_wb(w, c) s_wbf[(w) * C + (c)]
@@ -477,36 +496,44 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
   // BEFORE the score tile below is even issued — one whole memory round trip on every
   // workgroup's critical path.  Absent priors / positive mask read a valid dummy address (this
   // row's locs) and are ignored by the uses.
-  const Box4 l = ld4(locs + 4 * ic);
-  const float *pp = a.box_type == SBOD_BOX_OFFSET ? a.priors + 4 * static_cast<int64_t>(valid ? p : p0) : locs + 4 * ic;
+  const Box4 l = ld_box(locs + 4 * ic);
+  const float *pp = a.box_type == SBOD_BOX_OFFSET ? a.priors + 4 * static_cast<int64_t>(valid ? p : p0)
+                                                  : a.boxes_ws + 4 * ic;
   const Box4 pr = ld4(pp);
   const auto *posp = (const __attribute__((address_space(1))) uint8_t *)(
-      a.pos != nullptr ? a.pos + ic : reinterpret_cast<const uint8_t *>(locs + 4 * ic));
+      a.pos != nullptr ? a.pos + ic : reinterpret_cast<const uint8_t *>(a.boxes_ws + 4 * ic));
   const uint8_t posraw = *posp;
+  constexpr int kPer16 = 16 / static_cast<int>(sizeof(T));   // elements per 16-byte chunk
 #if SBOD_PREP_GLDS
   if (CM > 0 && (reinterpret_cast<uintptr_t>(scores + rbase * C) & 15) == 0) {
     // LDS-DMA: each wave-instruction copies 64 x 16 B of the tile straight into LDS (lane-linear,
-    // no VGPR round trip, no LDS write instructions); the tail floats go the ordinary way
+    // no VGPR round trip, no LDS write instructions); the tail elements go the ordinary way
     const float4 *src4 = reinterpret_cast<const float4 *>(scores + rbase * C);
-    const int n = np * C, n4 = n >> 2, wv0 = tid >> 6;
+    const int n = np * C, n4 = n / kPer16, wv0 = tid >> 6;
 #pragma unroll
-    for (int k = 0; k < (CM > 0 ? (CM + 3) / 4 : 1); ++k) {
-      const int q0 = k * kDTile + 64 * wv0;   // the wave's first float4 (uniform)
+    for (int k = 0; k < (CM > 0 ? (CM + kPer16 - 1) / kPer16 : 1); ++k) {
+      const int q0 = k * kDTile + 64 * wv0;   // the wave's first 16-byte chunk (uniform)
       if (q0 + lane < n4)
         __builtin_amdgcn_global_load_lds(src4 + q0 + lane,
                                          (__attribute__((address_space(3))) void *)(reinterpret_cast<float4 *>(s_sc) + q0),
                                          16, 0, 0);
     }
-    for (int e = (n4 << 2) + tid; e < n; e += kDTile) s_sc[e] = scores[rbase * C + e];
-  } else {
+    for (int e = n4 * kPer16 + tid; e < n; e += kDTile) s_tile[e] = scores[rbase * C + e];
+  } else if constexpr (sizeof(T) == 4) {
     tile_load_f32<(CM > 0 ? (CM + 3) / 4 : 8)>(s_sc, scores + rbase * C, np * C);
+  } else {
+    for (int e = tid; e < np * C; e += kDTile) s_tile[e] = scores[rbase * C + e];
   }
 #else
-  tile_load_f32<(CM > 0 ? (CM + 3) / 4 : 8)>(s_sc, scores + rbase * C, np * C);
+  if constexpr (sizeof(T) == 4)
+    tile_load_f32<(CM > 0 ? (CM + 3) / 4 : 8)>(s_sc, scores + rbase * C, np * C);
+  else
+    for (int e = tid; e < np * C; e += kDTile) s_tile[e] = scores[rbase * C + e];
 #endif
   __syncthreads();
   SEG_PHASE(1);
-  float *row = s_sc + tid * C;
+  float *row = s_sc + tid * C;         // (CM == 0 only: fp32 rows)
+  const T *rowt = s_tile + tid * C;
   if (valid) {
     Box4 d;
     if (a.box_type == SBOD_BOX_OFFSET) {
@@ -518,7 +545,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     }
     d = Box4{fminf(fmaxf(d.a, 0.f), 1.f), fminf(fmaxf(d.b, 0.f), 1.f), fminf(fmaxf(d.c, 0.f), 1.f),
              fminf(fmaxf(d.d, 0.f), 1.f)};
-    if (a.box_type == SBOD_BOX_CORNER) st4(locs + 4 * i, d);  // models/utils.py:224 clamp_ in place
+    if (a.box_type == SBOD_BOX_CORNER) st_box(locs + 4 * i, d);  // models/utils.py:224 clamp_ in place
     st4_nt(a.boxes_ws + 4 * i, d);
     if (a.dbg_boxes) st4(a.dbg_boxes + 4 * i, d);
     if constexpr (CM == 0) {
@@ -557,7 +584,7 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, float *__rest
     float r[KN];
 #pragma unroll
     for (int k = 0; k < KN; ++k) {
-      const float v = row[k];
+      const float v = widen(rowt[k]);
       r[k] = (CE > 0 || k < CM - 8 || k < C) ? v : -__builtin_inff();
     }
     const bool softmax = a.act == SBOD_ACT_SOFTMAX;
@@ -2073,13 +2100,16 @@ size_t sbod_detect_workspace_bytes(int B, int P, int C) {
   return carve_det(nullptr, B, P, C, clampw(kMaxWindow, P)).bytes;
 }
 
-int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
+int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
                     const float *priors_cxcy, const uint8_t *pos_mask, int box_type, int act,
                     float min_score, float max_overlap, int top_k, float final_nms, int window,
                     int flags, float *det_boxes, int64_t *det_labels, float *det_scores,
                     int32_t *det_count, int32_t *det_count_host, float *debug_probs,
                     float *debug_boxes, void *workspace, size_t workspace_bytes, void *stream) {
-  SBOD_REQUIRE((flags & ~SBOD_DETECT_COUNTERS_ZEROED) == 0, "sbod_detect_f32: unknown flags 0x%x", flags);
+  SBOD_REQUIRE((flags & ~(SBOD_DETECT_COUNTERS_ZEROED | SBOD_DETECT_INPUT_BF16)) == 0,
+               "sbod_detect_f32: unknown flags 0x%x", flags);
+  const bool bf16 = (flags & SBOD_DETECT_INPUT_BF16) != 0;
+  SBOD_REQUIRE(!bf16 || C <= 32, "sbod_detect_f32: bf16 input supports C <= 32 (C=%d)", C);
   SBOD_REQUIRE(B > 0 && P > 0 && C >= 2 && C <= 256 && locs && scores && det_boxes && det_labels &&
                    det_scores && det_count && top_k > 0,
                "sbod_detect_f32: bad arguments (B=%d P=%d C=%d top_k=%d)", B, P, C, top_k);
@@ -2124,14 +2154,24 @@ int sbod_detect_f32(float *locs, const float *scores, int B, int P, int C,
     KernelTimer kt("k_det_prepare", s, true);
     a.span = kt.span();
     const dim3 pg((P + kDTile - 1) / kDTile, B);
-    const size_t pl = static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12;
-    if (C <= 8) tlaunch(kt, k_det_prepare<8, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 16) tlaunch(kt, k_det_prepare<16, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C == 21) tlaunch(kt, k_det_prepare<24, 21>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 24) tlaunch(kt, k_det_prepare<24, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
-    else if (C <= 32) tlaunch(kt, k_det_prepare<32, 0>, pg, dim3(kDTile), pl, s, a, locs, scores);
+    const size_t pl = static_cast<size_t>(kDTile) * C * (bf16 ? 2 : 4) + (kDTile / 64) * C * 12;
+    uint16_t *lh = reinterpret_cast<uint16_t *>(locs);
+    const uint16_t *sh = reinterpret_cast<const uint16_t *>(scores);
+    float *lf = reinterpret_cast<float *>(locs);
+    const float *sf = reinterpret_cast<const float *>(scores);
+    if (bf16) {
+      if (C <= 8) tlaunch(kt, k_det_prepare<8, 0, uint16_t>, pg, dim3(kDTile), pl, s, a, lh, sh);
+      else if (C <= 16) tlaunch(kt, k_det_prepare<16, 0, uint16_t>, pg, dim3(kDTile), pl, s, a, lh, sh);
+      else if (C == 21) tlaunch(kt, k_det_prepare<24, 21, uint16_t>, pg, dim3(kDTile), pl, s, a, lh, sh);
+      else if (C <= 24) tlaunch(kt, k_det_prepare<24, 0, uint16_t>, pg, dim3(kDTile), pl, s, a, lh, sh);
+      else tlaunch(kt, k_det_prepare<32, 0, uint16_t>, pg, dim3(kDTile), pl, s, a, lh, sh);
+    } else if (C <= 8) tlaunch(kt, k_det_prepare<8, 0>, pg, dim3(kDTile), pl, s, a, lf, sf);
+    else if (C <= 16) tlaunch(kt, k_det_prepare<16, 0>, pg, dim3(kDTile), pl, s, a, lf, sf);
+    else if (C == 21) tlaunch(kt, k_det_prepare<24, 21>, pg, dim3(kDTile), pl, s, a, lf, sf);
+    else if (C <= 24) tlaunch(kt, k_det_prepare<24, 0>, pg, dim3(kDTile), pl, s, a, lf, sf);
+    else if (C <= 32) tlaunch(kt, k_det_prepare<32, 0>, pg, dim3(kDTile), pl, s, a, lf, sf);
     else tlaunch(kt, k_det_prepare<0, 0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
-                 static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, locs, scores);
+                 static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, lf, sf);
   }
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};

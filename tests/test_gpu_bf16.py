@@ -104,3 +104,26 @@ def test_c4_refinedet_full_size_vs_oracle():
     for name, t, r in zip(('arm_locs', 'arm_scores', 'odm_locs', 'odm_scores'), ts, rs):
         np.testing.assert_allclose(t.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-4, atol=1e-8,
                                    err_msg=name)
+
+
+@pytest.mark.parametrize('box_type', ['offset', 'corner'])
+def test_c2_detect_native_bf16_equals_widened_fp32(box_type):
+    """bf16 locs/scores go to the kernels as they are (SBOD_DETECT_INPUT_BF16, widened exactly on
+    load): boxes, labels and scores are bit-identical to detect on the fp32-widened tensors, and
+    the corner form's in-place clamp (models/utils.py:224) lands in the caller's bf16 tensor."""
+    P = torch.from_numpy(prior_table('SSD512'))
+    B, C = 16, 21
+    locs, scores = synth.make_preds(B, P.shape[0], C, seed=218, bg_shift=6.0)
+    if box_type == 'corner':
+        locs = locs * 5 + 0.5                  # xyxy-ish values, many outside [0, 1]
+    lo16, sc16 = locs.bfloat16().to(DEV), scores.bfloat16().to(DEV)
+    lo32 = lo16.float()
+    nat = core.detect(lo16, sc16, 0.01, 0.45, 200, P.to(DEV), box_type=box_type)
+    wid = core.detect(lo32, sc16.float(), 0.01, 0.45, 200, P.to(DEV), box_type=box_type)
+    for x, y in zip(nat, wid):
+        for b in range(B):
+            assert torch.equal(x[b], y[b])
+    if box_type == 'corner':
+        assert lo16.dtype == torch.bfloat16
+        assert torch.equal(lo16.float(), lo32)      # both clamped in place, identically
+        assert float(lo16.min()) >= 0.0 and float(lo16.max()) <= 1.0
