@@ -221,7 +221,8 @@ def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
             step()
     torch.cuda.current_stream(dev).wait_stream(side)
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    # captured on the warm-up stream: the cached workspaces are per stream
+    with torch.cuda.graph(graph, stream=side):
         step()
     graph.replay()
     ms = clock(graph.replay)

@@ -121,8 +121,12 @@ int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int 
  *   Outputs [B,P]: obj (object per prior, int32), ovl (overlap per prior after the forced match).
  *   n_pos [B+1] int32: positives per image (+ the batch total at n_pos[B]).  Labels and the
  *   negative mask are derived from (obj, ovl, gt_labels) by the loss kernels.
- * Workspace: sbod_match_workspace_bytes(B, Gmax). */
-enum { SBOD_MATCH_BINARY = 1, SBOD_MATCH_ODM = 2 };
+ * Workspace: sbod_match_workspace_bytes(B, Gmax): per-(image, object) best-prior keys and
+ * per-image positive counts, which must be zero on entry.  Every successful call leaves them
+ * zero, so a caller that knows the workspace is clean (a previous successful call on it, or its
+ * own memset) passes SBOD_MATCH_WS_ZEROED and the call issues no memset (hipGraph capture);
+ * without the flag the call zeroes them first (hipMemsetAsync). */
+enum { SBOD_MATCH_BINARY = 1, SBOD_MATCH_ODM = 2, SBOD_MATCH_WS_ZEROED = 256 };
 size_t sbod_match_workspace_bytes(int B, int Gmax);          /* enough for P <= 2^20 */
 size_t sbod_match_workspace_bytes_p(int B, int Gmax, int P);  /* exact for this P */
 int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt_offsets,

@@ -63,11 +63,13 @@ def main():
         f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         res = []
         for rep in range(3):
-            f(kid, None, 0)
+            f(1 << kid, None, 0)
             fn()
             torch.cuda.synchronize()
-            buf = np.zeros(2 * nblk, dtype=np.uint64)
-            f(-1, buf.ctypes.data, nblk)
+            reg = 4096   # SBOD_STAMP_REGION: kernel id k owns workgroups [k * reg, (k + 1) * reg)
+            buf = np.zeros(2 * 16 * reg, dtype=np.uint64)
+            f(0, buf.ctypes.data, 16 * reg)
+            buf = buf[2 * kid * reg: 2 * (kid * reg + min(nblk, reg))]
             st = (buf[0::2] & np.uint64(0xffffffffffff)).astype(np.int64)
             en_raw = buf[1::2]
             ok = st > 0

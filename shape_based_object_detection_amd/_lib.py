@@ -71,7 +71,7 @@ SIGNATURES = {
 
 # Constants of include/sbod.h.
 IOU_METRICS, IOU_PLAIN, IOU_INTER = 0, 1, 2
-MATCH_BINARY, MATCH_ODM = 1, 2
+MATCH_BINARY, MATCH_ODM, MATCH_WS_ZEROED = 1, 2, 256
 CODEC = dict(xy_to_cxcy=0, cxcy_to_xy=1, encode_tenfive=2, decode_tenfive=3, encode_var=4,
              decode_var=5, decode_tenfive_xy=6)
 REG = dict(smoothl1=0, l1=1, diou=2)

@@ -268,10 +268,14 @@ def match(gt, anchors, P, threshold=0.5, flags=0, priors_cxcy=None, arm_scores=N
     npos = torch.empty(B + 1, dtype=torch.int32, device=dev)
     nb = L.lib().sbod_match_workspace_bytes_p(B, gt.gmax, P)
     ws = workspace(nb, dev, 'match')
+    # the keys / counts are left zero by every successful call (SBOD_MATCH_WS_ZEROED)
+    zflag = _zeroed_flag(ws, nb, L.MATCH_WS_ZEROED, 'match')
+    _CLEAN.pop(ws.data_ptr(), None)
     L.call('sbod_match_f32', L.ptr(gt.boxes), L.ptr(gt.labels), L.ptr(gt.offsets), B, gt.gmax,
            L.ptr(anchors.contiguous()), L.ptr(priors_cxcy), L.ptr(arm_scores), P, float(threshold),
-           float(theta), int(flags), L.ptr(obj), L.ptr(ovl), L.ptr(npos), L.ptr(ws), nb,
+           float(theta), int(flags) | zflag, L.ptr(obj), L.ptr(ovl), L.ptr(npos), L.ptr(ws), nb,
            L.stream_of(anchors))
+    _CLEAN[ws.data_ptr()] = nb
     return obj, ovl, npos
 
 

@@ -15,6 +15,8 @@
 
 namespace sbod {
 
+SBOD_STAMP_DECL
+
 constexpr int kPackImgs = 64;   // images per launch (kernel-argument table: 1,284 B)
 
 struct GtPackArgs {
@@ -27,6 +29,7 @@ __global__ __launch_bounds__(64) void k_gt_pack(GtPackArgs a, int n_img, int las
                                                 float *__restrict__ out_boxes,
                                                 int64_t *__restrict__ out_labels,
                                                 int32_t *__restrict__ out_off) {
+  STAMP_BEGIN();
   const int i = blockIdx.x;
   const int r0 = a.off[i], G = a.off[i + 1] - r0;
   const float4 *src = reinterpret_cast<const float4 *>(a.boxes[i]);
@@ -45,6 +48,7 @@ __global__ __launch_bounds__(64) void k_gt_pack(GtPackArgs a, int n_img, int las
     out_off[i] = r0;
     if (last_chunk && i == n_img - 1) out_off[n_img] = r0 + G;
   }
+  STAMP_END(8, 1);
 }
 
 }  // namespace sbod
@@ -83,3 +87,5 @@ extern "C" int sbod_gt_pack(const void *const *box_ptrs, const void *const *labe
   }
   return SBOD_OK;
 }
+
+SBOD_STAMP_EXPORT(gtpack)

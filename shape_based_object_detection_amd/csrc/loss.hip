@@ -791,6 +791,7 @@ __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ pa
                                                     const int32_t *__restrict__ npos_total, int reg,
                                                     int cls, int flags, float reg_weight,
                                                     float *__restrict__ out) {
+  STAMP_BEGIN();
   __shared__ double s_red[16];
   double c = 0.0, l = 0.0;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
@@ -811,6 +812,7 @@ __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ pa
     out[2] = loc;
     out[3] = n;
   }
+  STAMP_END(6, 1);
 }
 
 // ----------------------------------------------------------------------------- standalone

@@ -76,41 +76,39 @@ __device__ __forceinline__ Anchor load_anchor(const float *anchors, const float 
 
 // Matching in two launches.
 //
-// k_match_tile (B x ceil(P / 256) workgroups, one prior per thread; 2 and 4 consecutive priors
-// per thread measured slower: fewer waves to hide the per-object latency chain):
+// k_match_tile (B x ceil(P / 256) workgroups of four INDEPENDENT waves, one prior per lane: no
+// barrier and no LDS anywhere in the kernel):
 //   per prior: the best object (first index on ties) -> obj / ovl;
-//   per object: this tile's best prior as a packed (ord(overlap) << 32 | ~prior) key (the lowest
+//   per object: the image's best prior as a packed (ord(overlap) << 32 | ~prior) key (the lowest
 //     prior on ties), for overlaps > 0 only (an object whose best overlap is <= 0 is never
-//     forced, so every such key may read 0).  No cross-lane work in the object loop: each thread
-//     leaves its overlap's ord per object in LDS, and after the loop one pass reduces the
-//     [objects x priors] table (a thread per (object, 16-prior segment), then a DPP max over the
-//     16 lanes holding one object) -> one 16-byte record per (tile, object) {key, obj and ovl of
-//     the key's prior (-1 when not known: objects beyond one LDS chunk)};
-//   a wave whose priors overlap none of an object (the common case: a wave's priors are one
-//     small patch of one feature map) skips that object's divisions: every overlap there is
-//     <= 0, which can neither raise a prior's best (>= 0 from object 0 on) nor make a key;
-//   the tile's positive count before the forced match -> tcount.
-// k_match_final (one workgroup per image): every record of the image in flight at once, the max
-// key per object through LDS, then the forced match of models/SSD512.py:546-553 (filter objects
-// whose best overlap > 0, overlap 1.0 and object j = the FILTERED position, last writer wins),
-// the positive count adjusted for exactly the priors it rewrites -> n_pos[b], n_pos[B].  Up to 64
-// objects the forced match runs in wave 0's registers (lane = object: ballots, readlanes and one
-// permute, no barrier); more objects take the LDS form.
-// (An in-launch finish by each image's last-arriving tile, with write-through records and
-// arrival counters, measured slower: the write-through drain, the counter round trip and the
-// fabric-latency record loads cost more than this launch boundary — DESIGN.md §9.)
-constexpr int kGc = 16;       // objects per chunk of the per-thread best table in LDS
-constexpr int kSegCols = 16;  // threads (columns) per first-pass reduction segment
-constexpr int kNSeg = kMThreads / kSegCols;
+//     forced): each wave reduces its 64 lanes (u32 DPP max of the ord, then the lowest lane
+//     holding it) and one lane folds the result into best[b][shard][g] with a no-return
+//     agent-scope 64-bit atomic max (executed at the memory side, so waves on different XCDs
+//     meet in one word; kKeyShards words per object, by workgroup, keep the queue per word short);
+//   lane j holds object j of the current 64-object chunk (box, area, zero flag, label): object g
+//     reaches the wave's scalar registers by readlane, so there is no per-object memory access;
+//   a wave skips every object whose box misses the bounding box of the wave's priors (the common
+//     case: a wave's priors are one small patch of one feature map): every overlap there is <= 0,
+//     which can neither raise a prior's best (>= 0 from object 0 on) nor make a key.  The test
+//     runs once per chunk as a ballot over the object lanes; the wave walks the set bits;
+//   the wave's positive count before the forced match -> wcnt[b][wave] (a plain store: one
+//     counter per image took ~2 µs of queued atomics at the end of the launch).
+// k_match_final (one workgroup per image): the max over each object's key shards and the sum of
+// the image's wave counts, then the forced match of
+// models/SSD512.py:546-553 (filter objects whose best overlap > 0, overlap 1.0 and object j = the
+// FILTERED position, last writer wins) against the phase-1 (obj, ovl) of each forced prior, the
+// positive count adjusted for exactly the priors it rewrites -> n_pos[b], n_pos[B].  Up to 64
+// objects it is ONE wave, lane = object, everything in registers (ballots, readlanes, bpermutes);
+// more objects take the LDS form.  It leaves best[b][*][*] zero again: the workspace's keys are
+// zero on entry to every call after the first (SBOD_MATCH_WS_ZEROED).
+// (Round 2's form — a per-tile LDS table of overlaps reduced per (tile, object) into 16-byte
+// records, block barriers around it — spent ≈10-12 µs per launch at SSD512 B=32, most of it in
+// the barriers and the LDS table)
+constexpr int kKeyShards = 8;   // copies of the per-object key words (one per XCD-sized group of tiles)
+constexpr int kSlots = 16;      // per-wave LDS rows of pending per-object ords
 
-struct MRec {   // 16-byte (tile, object) record
-  unsigned long long key;
-  int32_t obj;
-  float ovl;
-};
-
-// Max of a u64 over each row of 16 lanes, valid in every lane of the row (DPP quad swaps and
-// mirrors; keys are unique, so the max is the row's best).
+// Max of a u64 over each quad of lanes, valid in every lane of the quad (DPP quad swaps; keys are
+// unique, so the max is the quad's best).
 template <int kCtrl>
 __device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) {
   const uint32_t lo = dpp_u32<kCtrl, 0xf>(static_cast<uint32_t>(v));
@@ -118,11 +116,29 @@ __device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) 
   const unsigned long long o = (static_cast<unsigned long long>(hi) << 32) | lo;
   return o > v ? o : v;
 }
-__device__ __forceinline__ unsigned long long row16_max_u64(unsigned long long v) {
-  v = dpp_max_u64<0xB1>(v);    // quad_perm [1,0,3,2]
-  v = dpp_max_u64<0x4E>(v);    // quad_perm [2,3,0,1]
-  v = dpp_max_u64<0x141>(v);   // row_half_mirror
-  return dpp_max_u64<0x140>(v);   // row_mirror
+__device__ __forceinline__ unsigned long long quad_max_u64(unsigned long long v) {
+  v = dpp_max_u64<0xB1>(v);        // quad_perm [1,0,3,2]
+  return dpp_max_u64<0x4E>(v);     // quad_perm [2,3,0,1]
+}
+
+struct GtLane {   // lane j of a chunk: object j
+  float x1, y1, x2, y2, area;
+  int zero, lab;
+};
+
+template <int kFlags>
+__device__ __forceinline__ GtLane load_gt_lane(const float *__restrict__ gt, const int64_t *__restrict__ labels,
+                                               int g0, int gc, int gn, int lane) {
+  const int j = g0 + gc + min(lane, max(gn - 1, 0));
+  const Box4 bx = ld4(gt + 4 * static_cast<int64_t>(j));
+  const float gx = bx.c - bx.a, gy = bx.d - bx.b;
+  int lab = static_cast<int32_t>(labels[j]);
+  if ((kFlags & SBOD_MATCH_BINARY) != 0) lab = lab > 0;
+  return GtLane{bx.a, bx.b, bx.c, bx.d, gx * gy, (fabsf(gx) < kIouEps) && (fabsf(gy) < kIouEps), lab};
+}
+
+__device__ __forceinline__ float rl_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
 template <bool kOdm, int kFlags>
@@ -131,273 +147,196 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile(
     const int32_t *__restrict__ off, const float *__restrict__ anchors,
     const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
     float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
-    MRec *__restrict__ rec, int32_t *__restrict__ tcount, int32_t *__restrict__ npos, int B,
-    SpanRing *span) {
-  // dynamic LDS: [4 * max(Gmax, kMThreads) labels]
-  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  __shared__ __attribute__((aligned(16))) uint32_t s_ord[kGc][kMThreads];  // per object, per prior: ord
-  __shared__ uint32_t s_ev[kMThreads / 64];                                 // per wave: objects evaluated
-  __shared__ int32_t s_fo[kMThreads];                                       // final (obj, ovl) per prior
-  __shared__ float s_fv[kMThreads];
-  __shared__ int s_red[16];
-  __shared__ float4 s_gt[kMThreads];   // this chunk's GT boxes: slot j < 16 = object gc + j
+    unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt, int32_t *__restrict__ npos,
+    int B, SpanRing *span) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_od[kMThreads / 64][kSlots][64];   // per wave
+  __shared__ int s_slot[kMThreads / 64][kSlots];
   STAMP_BEGIN();
   span_begin(span);
-  PHASE_DECL;
-  SEG_PHASE(0);
-  int32_t *s_lab = reinterpret_cast<int32_t *>(s_dyn);
-  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int ntile = gridDim.x;
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   if (blockIdx.x == 0 && b == 0 && tid == 0) npos[B] = 0;   // k_match_final accumulates
-  const int tbase = blockIdx.x * kMThreads;
-  const int p = tbase + tid;
+  const int wbase = blockIdx.x * kMThreads + (tid & ~63);
+  const int p = wbase + lane;
   const bool valid = p < P;
-  // ONE memory round trip before the object loop: the anchor, the first chunk's GT boxes and the
-  // labels are loaded together (unconditional, clamped) and committed to LDS by unconditional
-  // stores before the first barrier, so no load sits under a branch where the compiler would
-  // sink it behind the anchor's wait; the object loop then reads the boxes from LDS instead of a
-  // scalar load round trip per group of objects.  An image without objects reads element 0 (the
-  // GT buffers hold at least one); s_lab has room for max(Gmax, kMThreads) labels.
+  // one memory round trip before the object loop: the anchor and the first chunk's objects
+  // (unconditional, clamped loads; an image without objects reads element 0 — the GT buffers
+  // hold at least one)
   const int pc = min(p, P - 1);
   const Box4 araw = ld4(kOdm ? anchors + 4 * (static_cast<int64_t>(b) * P + pc) : anchors + 4 * static_cast<int64_t>(pc));
   const Box4 apri = kOdm ? ld4(priors + 4 * pc) : Box4{0.f, 0.f, 0.f, 0.f};
   const int g0 = ld_i32_uniform(off + b), G = ld_i32_uniform(off + b + 1) - g0;
-  const Box4 gt0 = ld4(gt + 4 * static_cast<int64_t>(G > 0 ? g0 + min(tid & (kGc - 1), G - 1) : 0));
-  const int32_t lab0 = static_cast<int32_t>(labels[G > 0 ? g0 + min(tid, G - 1) : 0]);
+  const bool has = G > 0;
+  GtLane o = load_gt_lane<kFlags>(gt, labels, has ? g0 : 0, 0, has ? min(G, 64) : 1, lane);
+  float eas0 = 0.f, eas1 = 0.f;
+  if constexpr (kOdm) {
+    const int64_t ic = static_cast<int64_t>(b) * P + pc;
+    eas0 = arm_scores[2 * ic];
+    eas1 = arm_scores[2 * ic + 1];
+  }
   const Anchor a = make_anchor<kOdm>(araw, apri);
-  s_gt[tid] = make_float4(gt0.a, gt0.b, gt0.c, gt0.d);
-  s_lab[tid] = lab0;
-  for (int i = tid + kMThreads; i < G; i += kMThreads) s_lab[i] = static_cast<int32_t>(labels[g0 + i]);
-  // the wave's prior bounding box as monotone integer keys, so each object's "does any prior of
-  // this wave overlap it" test runs on the scalar unit: an object outside the box has
-  // iw <= 0 or ih <= 0 for every prior of the wave (overlap 0 or -1, never a key, never a new
-  // best after object 0), so its divisions are skipped exactly
+  // the wave's prior bounding box as monotone integer keys
   const bool live = valid && !a.zero;
   const uint32_t wx1 = ~wave_max_u32(live ? ~f2ord(a.x1) : 0u), wy1 = ~wave_max_u32(live ? ~f2ord(a.y1) : 0u);
   const uint32_t wx2 = wave_max_u32(live ? f2ord(a.x2) : 0u), wy2 = wave_max_u32(live ? f2ord(a.y2) : 0u);
   const bool wlive = __ballot(live) != 0ull;
-  SEG_PHASE(1);
   float best = 0.f;
-  int bi = 0;
-  const bool one_chunk = G <= kGc;
-  MRec *rrow = rec + (static_cast<int64_t>(b) * ntile + blockIdx.x) * Gmax;
-  for (int gc = 0; gc < G; gc += kGc) {
-    const int gn = min(G - gc, kGc);
-    if (gc > 0) {   // later chunks: their boxes into LDS (the previous chunk's end barrier is behind)
-      const Box4 bx = ld4(gt + 4 * static_cast<int64_t>(g0 + gc + min(tid & (kGc - 1), gn - 1)));
-      s_gt[tid] = make_float4(bx.a, bx.b, bx.c, bx.d);
-    }
-    __syncthreads();
-    uint32_t ev = 0u;   // objects of this chunk evaluated by this wave (wave-uniform)
-    for (int j0 = 0; j0 < gn; j0 += 4) {
-      Box4 t[4];   // LDS broadcast reads made scalar: the wave-box test runs on the scalar unit
+  int bi = 0, blab = 0;
+  // this workgroup's shard of the image's keys (kKeyShards copies: the waves of one image spread
+  // their atomics over kKeyShards words per object instead of queueing on one)
+  unsigned long long *brow = best_key + (static_cast<int64_t>(b) * kKeyShards + (blockIdx.x & (kKeyShards - 1))) * Gmax;
+  // metrics.py:224-250, in the reference's order: this lane's overlap with chunk object j
+  auto iou_of = [&](int j, int &glab) {
+    const float tx1 = rl_f(o.x1, j), ty1 = rl_f(o.y1, j), tx2 = rl_f(o.x2, j), ty2 = rl_f(o.y2, j);
+    const float garea = rl_f(o.area, j);
+    const int gzero = __builtin_amdgcn_readlane(o.zero, j);
+    glab = __builtin_amdgcn_readlane(o.lab, j);
+    float iw = fminf(tx2, a.x2) - fmaxf(tx1, a.x1);
+    if (iw < 0.f) iw = 0.f;
+    float ih = fminf(ty2, a.y2) - fmaxf(ty1, a.y1);
+    if (ih < 0.f) ih = 0.f;
+    const float inner = iw * ih;
+    float ov = inner / (((garea + a.area) - inner) + kIouEps);
+    if (gzero) ov = 0.f;
+    if (a.zero) ov = -1.f;
+    return ov;
+  };
+  // Per-object keys: an object with a positive overlap in this wave leaves its lanes' ords in
+  // one of the wave's kSlots LDS rows (one ds_write, no cross-lane work in the object loop);
+  // flush_keys reduces all filled rows at once — lane = (row, 16-lane segment): the segment's
+  // max ord and lowest lane holding it, then the max over the row's 4 segments (DPP) — and
+  // folds each row's key into the object's word with one atomic.  Rows are wave-private: no
+  // block barrier, only the wave's own LDS order.
+  const int wv = tid >> 6;
+  int nslot = 0;
+  auto flush_keys = [&]() {
+    if (nslot == 0) return;
+    __builtin_amdgcn_wave_barrier();
+    const int j = lane >> 2, q = lane & 3;
+    unsigned long long key = 0ull;
+    if (j < nslot) {
+      const uint4 *row = reinterpret_cast<const uint4 *>(&s_od[wv][j][16 * q]);
+      uint32_t v[16];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 v = s_gt[min(j0 + u, gn - 1)];
-        t[u] = Box4{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
-                    __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y))),
-                    __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z))),
-                    __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w)))};
+      for (int r = 0; r < 4; ++r) {
+        const uint4 x = row[r];
+        v[4 * r] = x.x;
+        v[4 * r + 1] = x.y;
+        v[4 * r + 2] = x.z;
+        v[4 * r + 3] = x.w;
       }
+      uint32_t mx = v[0];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + u;
-        if (j >= gn) break;
-        const int g = gc + j;
-        const bool hitw = wlive && f2ord(t[u].c) > wx1 && f2ord(t[u].a) < wx2 && f2ord(t[u].d) > wy1 &&
-                          f2ord(t[u].b) < wy2;
-        // object 0 is always evaluated (it sets every prior's first best, ties included)
-        if (g == 0 || hitw) {   // metrics.py:224-250, in the reference's order
-          const float gx = t[u].c - t[u].a, gy = t[u].d - t[u].b;
-          const float garea = gx * gy;
-          const bool gzero = (fabsf(gx) < kIouEps) && (fabsf(gy) < kIouEps);
-          float iw = fminf(t[u].c, a.x2) - fmaxf(t[u].a, a.x1);
-          if (iw < 0.f) iw = 0.f;
-          float ih = fminf(t[u].d, a.y2) - fmaxf(t[u].b, a.y1);
-          if (ih < 0.f) ih = 0.f;
-          const float inner = iw * ih;
-          float ov = inner / (((garea + a.area) - inner) + kIouEps);
-          if (gzero) ov = 0.f;
-          if (a.zero) ov = -1.f;
-          if (g == 0 || ov > best) {
-            best = ov;
-            bi = g;
-          }
-          s_ord[j][tid] = (valid && ov > 0.f) ? f2ord(ov) : 0u;
-          ev |= 1u << j;
-        }
-      }
+      for (int c = 1; c < 16; ++c) mx = max(mx, v[c]);
+      int c0 = 15;
+#pragma unroll
+      for (int c = 14; c >= 0; --c) c0 = v[c] == mx ? c : c0;
+      key = mx ? ((static_cast<unsigned long long>(mx) << 32) |
+                  (0xffffffffull - static_cast<uint32_t>(wbase + 16 * q + c0)))
+               : 0ull;
     }
-    if (lane == 0) s_ev[wv] = ev;
-    if (one_chunk) {
-      s_fo[tid] = bi;
-      s_fv[tid] = best;
-    }
-    __syncthreads();
-    // thread -> (object j = tid / 16, segment sg = tid % 16 of 16 priors): the segment's best
-    // (ord, lowest prior), then the max over the row of 16 lanes = the tile's key of object j
-    {
-      const int j = tid / kNSeg, sg = tid - j * kNSeg;
-      unsigned long long kb = 0ull;
-      if (j < gn && ((s_ev[sg / (64 / kSegCols)] >> j) & 1u)) {
-        const uint4 *row = reinterpret_cast<const uint4 *>(&s_ord[j][sg * kSegCols]);
-        uint32_t v[kSegCols];
-#pragma unroll
-        for (int q = 0; q < kSegCols / 4; ++q) {
-          const uint4 x = row[q];
-          v[4 * q] = x.x;
-          v[4 * q + 1] = x.y;
-          v[4 * q + 2] = x.z;
-          v[4 * q + 3] = x.w;
-        }
-        uint32_t m8[8], m4[4];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) m8[c] = max(v[c], v[c + 8]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) m4[c] = max(m8[c], m8[c + 4]);
-        const uint32_t mx = max(max(m4[0], m4[2]), max(m4[1], m4[3]));
-        uint32_t mask = 0u;
-#pragma unroll
-        for (int c = 0; c < kSegCols; ++c) mask |= (v[c] == mx ? 1u : 0u) << c;
-        const int c0 = __builtin_ctz(mask);   // mask != 0: mx is one of v
-        kb = mx ? ((static_cast<unsigned long long>(mx) << 32) |
-                   (0xffffffffull - static_cast<uint32_t>(tbase + sg * kSegCols + c0)))
-                : 0ull;
+    key = quad_max_u64(key);
+    if (q == 0 && j < nslot && key)
+      __hip_atomic_fetch_max(brow + s_slot[wv][j], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_wave_barrier();
+    nslot = 0;
+  };
+  auto note_key = [&](int g, float ov) {
+    const uint32_t od = (valid && ov > 0.f) ? f2ord(ov) : 0u;
+    if (__ballot(od != 0u) == 0ull) return;   // no positive overlap here: never this wave's key
+    s_od[wv][nslot][lane] = od;
+    if (lane == 0) s_slot[wv][nslot] = g;
+    if (++nslot == kSlots) flush_keys();
+  };
+  for (int gc = 0; gc < G; gc += 64) {
+    const int gn = min(G - gc, 64);
+    if (gc > 0) o = load_gt_lane<kFlags>(gt, labels, g0, gc, gn, lane);
+    // objects of this chunk whose box meets the wave's prior box (object 0 always: it sets
+    // every prior's first best, ties included)
+    const bool hit = wlive && lane < gn && f2ord(o.x2) > wx1 && f2ord(o.x1) < wx2 && f2ord(o.y2) > wy1 &&
+                     f2ord(o.y1) < wy2;
+    unsigned long long todo = __ballot(hit) | (gc == 0 ? 1ull : 0ull);
+    // two objects per step (independent IoU chains), applied in object order
+    while (todo) {
+      const int j1 = __builtin_ctzll(todo);
+      todo &= todo - 1ull;
+      const bool two = todo != 0ull;
+      const int j2 = two ? __builtin_ctzll(todo) : j1;
+      if (two) todo &= todo - 1ull;
+      int lab1, lab2;
+      const float ov1 = iou_of(j1, lab1), ov2 = iou_of(j2, lab2);
+      if (gc + j1 == 0 || ov1 > best) {
+        best = ov1;
+        bi = gc + j1;
+        blab = lab1;
       }
-      kb = row16_max_u64(kb);
-      if (sg == 0 && j < gn) {
-        // the prior's final (obj, ovl) when every object is in this chunk
-        int32_t o = -1;
-        float v = 0.f;
-        if (one_chunk && kb) {
-          const int lp = static_cast<int>(0xffffffffu - static_cast<uint32_t>(kb)) - tbase;
-          o = s_fo[lp];
-          v = s_fv[lp];
-        }
-        rrow[gc + j] = MRec{kb, o, v};
+      if (two && ov2 > best) {
+        best = ov2;
+        bi = gc + j2;
+        blab = lab2;
       }
+      note_key(gc + j1, ov1);
+      if (two) note_key(gc + j2, ov2);
     }
-    if (gc + kGc < G) __syncthreads();   // s_ord / s_ev are rewritten by the next chunk
   }
-  SEG_PHASE(2);
-  int pos = 0;
+  flush_keys();
+  bool pos = false;
   if (valid) {
     const int64_t i = static_cast<int64_t>(b) * P + p;
     obj[i] = bi;
     ovl[i] = best;
-    int c = best < thr ? 0 : s_lab[bi];
-    if ((kFlags & SBOD_MATCH_BINARY) != 0) c = c > 0;
-    pos = c > 0;
+    pos = !(best < thr) && blab > 0;
     if constexpr (kOdm) {
-      const float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
-      const float m = fmaxf(z0, z1);
-      const float e0 = expf(z0 - m), e1 = expf(z1 - m);
-      if (e1 / (e0 + e1) < theta) pos = 0;
+      const float m = fmaxf(eas0, eas1);
+      const float e0 = expf(eas0 - m), e1 = expf(eas1 - m);
+      if (e1 / (e0 + e1) < theta) pos = false;
     }
   }
-  pos = block_sum(pos, s_red);
-  if (tid == 0) tcount[b * ntile + blockIdx.x] = pos;
+  // the wave's positive count, one plain store per wave (summed by k_match_final)
+  const int n = __popcll(__ballot(pos));
+  if (lane == 0) wcnt[static_cast<int64_t>(b) * (gridDim.x * (kMThreads / 64)) + (wbase >> 6)] = n;
   span_end(span);
-  SEG_PHASE(3);
-#ifdef SBOD_PHASE_CLOCKS
-  if (PHASE_PRINT_SEL)
-    printf("match_tile x%d b%d G=%d: start %lld objects+keys %lld store+sum %lld total %lld\n", blockIdx.x, b, G,
-           ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
-#endif
   STAMP_END(5, 1);
 }
 
-// k_match_final: one workgroup of kFThreads per image.
+// k_match_final: one workgroup per image; 64 threads when Gmax <= 64 (the register form),
+// else kFThreads (the LDS form).
 constexpr int kFThreads = 256;
-constexpr int kFRegs = 4;   // records per thread kept in registers (G * ntile <= 1024)
 
 template <int kFlags>
 __global__ __launch_bounds__(kFThreads) void k_match_final(
-    const int64_t *__restrict__ labels, const int32_t *__restrict__ off, const MRec *__restrict__ rec,
-    const int32_t *__restrict__ tcount, int ntile, int Gmax, int P, float thr,
-    const float *__restrict__ arm_scores, float theta, int32_t *__restrict__ obj,
+    const int64_t *__restrict__ labels, const int32_t *__restrict__ off,
+    unsigned long long *__restrict__ best_key, const int32_t *__restrict__ wcnt, int nw, int Gmax,
+    int P, float thr, const float *__restrict__ arm_scores, float theta, int32_t *__restrict__ obj,
     float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
-  // LDS per object g: best key, its prior's phase-1 (obj, ovl), label; the LDS forced-match
-  // form also uses prior / easy | previous writer / final object
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  unsigned long long *s_best = reinterpret_cast<unsigned long long *>(s_dyn);
-  int32_t *s_o0 = reinterpret_cast<int32_t *>(s_best + Gmax);
-  float *s_v0 = reinterpret_cast<float *>(s_o0 + Gmax);
-  int32_t *s_lab = reinterpret_cast<int32_t *>(s_v0 + Gmax);
-  int32_t *s_pr = s_lab + Gmax;
-  int32_t *s_easy = s_pr + Gmax;
-  int32_t *s_new = s_easy + Gmax;
   __shared__ int s_red[16];
-  __shared__ int s_cnt;
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  STAMP_BEGIN();
   const int g0 = off[b], G = off[b + 1] - g0;
-  const MRec *rb = rec + static_cast<int64_t>(b) * ntile * Gmax;
-  const int n = G * ntile;
-  const bool inreg = n <= kFRegs * kFThreads;
-  // every record of the image (and the tile counts) in flight at once
-  MRec r[kFRegs];
+  unsigned long long *brow = best_key + static_cast<int64_t>(b) * kKeyShards * Gmax;
+  // the phase-1 positive count: the image's per-wave counts (first wave only; the LDS form
+  // shares it through s_red)
+  int cnt1 = 0;
+  if (tid < 64) {
+    for (int w = lane; w < nw; w += 64) cnt1 += wcnt[static_cast<int64_t>(b) * nw + w];
+    cnt1 = wave_sum_i32(cnt1);
+  }
+  // an object's key: the max over its shards, which return to zero
+  auto take_key = [&](int g) {
+    unsigned long long k = 0ull;
 #pragma unroll
-  for (int q = 0; q < kFRegs; ++q) {
-    const int it = min(tid + q * kFThreads, max(n - 1, 0));
-    const int g = it / ntile, t = it - g * ntile;
-    r[q] = (inreg && n > 0) ? rb[static_cast<int64_t>(t) * Gmax + g] : MRec{0ull, 0, 0.f};
-  }
-  int cnt = 0;
-  for (int t = tid; t < ntile; t += kFThreads) cnt += tcount[b * ntile + t];
-  for (int g = tid; g < G; g += kFThreads) {
-    s_best[g] = 0ull;
-    s_lab[g] = static_cast<int32_t>(labels[g0 + g]);
-  }
-  if (tid == 0) s_cnt = 0;
-  __syncthreads();
-  cnt = wave_sum_i32(cnt);
-  if (lane == 0 && cnt) atomicAdd(&s_cnt, cnt);
-  if (inreg) {
+    for (int s = 0; s < kKeyShards; ++s) {
+      const unsigned long long v = brow[s * Gmax + g];
+      k = v > k ? v : k;
+    }
 #pragma unroll
-    for (int q = 0; q < kFRegs; ++q) {
-      const int it = tid + q * kFThreads;
-      if (it < n && r[q].key) atomicMax(&s_best[it / ntile], r[q].key);
-    }
-  } else {
-    for (int it = tid; it < n; it += kFThreads) {
-      const int g = it / ntile, t = it - g * ntile;
-      const unsigned long long k = rb[static_cast<int64_t>(t) * Gmax + g].key;
-      if (k) atomicMax(&s_best[g], k);
-    }
-  }
-  __syncthreads();
-  // the winning record of each object supplies its prior's phase-1 (obj, ovl)
-  auto take = [&](int g, const MRec &x) {
-    if (x.key && x.key == s_best[g]) {
-      int32_t o = x.obj;
-      float v = x.ovl;
-      if (o < 0) {   // not carried (more objects than one tile chunk): phase 1's outputs
-        const int64_t i = static_cast<int64_t>(b) * P + static_cast<int>(0xffffffffu - static_cast<uint32_t>(x.key));
-        o = obj[i];
-        v = ovl[i];
-      }
-      s_o0[g] = o;
-      s_v0[g] = v;
-    }
+    for (int s = 0; s < kKeyShards; ++s) brow[s * Gmax + g] = 0ull;
+    return k;
   };
-  if (inreg) {
-#pragma unroll
-    for (int q = 0; q < kFRegs; ++q) {
-      const int it = tid + q * kFThreads;
-      if (it < n) take(it / ntile, r[q]);
-    }
-  } else {
-    for (int it = tid; it < n; it += kFThreads) {
-      const int g = it / ntile, t = it - g * ntile;
-      take(g, rb[static_cast<int64_t>(t) * Gmax + g]);
-    }
-  }
-  __syncthreads();
-  const int cnt1 = s_cnt;
-  auto is_pos = [&](int o, float v, int easy) {
-    int c = v < thr ? 0 : s_lab[o];
-    if ((kFlags & SBOD_MATCH_BINARY) != 0) c = c > 0;
-    return c > 0 && !easy;
+  auto lab_of = [&](int g) {
+    int l = static_cast<int32_t>(labels[g0 + g]);
+    if ((kFlags & SBOD_MATCH_BINARY) != 0) l = l > 0;
+    return l;
   };
   auto easy_of = [&](int p) {
     int easy = 0;
@@ -410,53 +349,76 @@ __global__ __launch_bounds__(kFThreads) void k_match_final(
     }
     return easy;
   };
+  // is_pos(label, overlap, easy): the positive rule of the criteria
+  auto is_pos = [&](int lab, float v, int easy) { return !(v < thr) && lab > 0 && !easy; };
   auto publish = [&](int delta) {   // one lane
     const int nb = cnt1 + delta;
     npos[b] = nb;
     atomicAdd(npos + B, nb);
   };
   if (G <= 64) {
-    if (wv == 0) {   // lane = object, everything in registers
-      const unsigned long long k = lane < G ? s_best[lane] : 0ull;
-      const int p = k ? static_cast<int>(0xffffffffu - static_cast<uint32_t>(k)) : -1;
-      const unsigned long long valid = __ballot(p >= 0);
-      const int j = __popcll(valid & ((1ull << lane) - 1ull));   // filtered position
-      int prev = -1;      // the previous writer of the same prior
-      bool lastw = true;  // no later writer of the same prior
-      for (int h = 0; h < G; ++h) {
-        const int ph = __builtin_amdgcn_readlane(p, h);
-        if (p >= 0 && ph == p) {
-          if (h < lane) prev = h;
-          if (h > lane) lastw = false;
-        }
+    if (tid >= 64) return;
+    // lane = object: its best key, the key's prior and that prior's phase-1 (obj, ovl)
+    const unsigned long long k = lane < G ? take_key(lane) : 0ull;
+    const int lab = lane < G ? lab_of(lane) : 0;
+    const int p = k ? static_cast<int>(0xffffffffu - static_cast<uint32_t>(k)) : -1;
+    const int64_t ip = static_cast<int64_t>(b) * P + (p >= 0 ? p : 0);
+    const int o_ph1 = obj[ip];
+    const float v_ph1 = ovl[ip];
+    const int easy = p >= 0 ? easy_of(p) : 0;
+    const unsigned long long valid = __ballot(p >= 0);
+    const int j = __popcll(valid & ((1ull << lane) - 1ull));   // filtered position
+    int prev = -1;      // the previous writer of the same prior
+    bool lastw = true;  // no later writer of the same prior
+    for (int h = 0; h < G; ++h) {
+      const int ph = __builtin_amdgcn_readlane(p, h);
+      if (p >= 0 && ph == p) {
+        if (h < lane) prev = h;
+        if (h > lane) lastw = false;
       }
-      const int jprev = __shfl(j, prev < 0 ? lane : prev, 64);
-      int d = 0;
-      if (p >= 0) {
-        const int easy = easy_of(p);
-        const int o_old = prev >= 0 ? jprev : s_o0[lane];
-        const float v_old = prev >= 0 ? 1.0f : s_v0[lane];
-        d = (is_pos(j, 1.0f, easy) ? 1 : 0) - (is_pos(o_old, v_old, easy) ? 1 : 0);
-        if (lastw) {
-          const int64_t i = static_cast<int64_t>(b) * P + p;
-          obj[i] = j;
-          ovl[i] = 1.0f;
-        }
-      }
-      const int delta = wave_sum_i32(d);
-      if (lane == 0) publish(delta);
     }
+    const int jprev = __shfl(j, prev < 0 ? lane : prev, 64);
+    const int o_old = prev >= 0 ? jprev : o_ph1;
+    const float v_old = prev >= 0 ? 1.0f : v_ph1;
+    // labels of the new object j and the old object, read from the lanes that hold them
+    const int lab_new = __shfl(lab, j & 63, 64), lab_old = __shfl(lab, o_old & 63, 64);
+    int d = 0;
+    if (p >= 0) {
+      d = (is_pos(lab_new, 1.0f, easy) ? 1 : 0) - (is_pos(lab_old, v_old, easy) ? 1 : 0);
+      if (lastw) {
+        obj[ip] = j;
+        ovl[ip] = 1.0f;
+      }
+    }
+    const int delta = wave_sum_i32(d);
+    if (lane == 0) publish(delta);
+    STAMP_END(7, 0);
     return;
   }
-  // more objects: the LDS form of the same rules
-  for (int g = tid; g < G; g += kFThreads) {
-    const unsigned long long k = s_best[g];
+  // more objects: the LDS form of the same rules.  LDS per object: prior, easy | previous writer,
+  // label, final object, phase-1 (obj, ovl)
+  int32_t *s_pr = reinterpret_cast<int32_t *>(s_dyn);
+  int32_t *s_easy = s_pr + Gmax;
+  int32_t *s_lab = s_easy + Gmax;
+  int32_t *s_new = s_lab + Gmax;
+  int32_t *s_o0 = s_new + Gmax;
+  float *s_v0 = reinterpret_cast<float *>(s_o0 + Gmax);
+  if (tid == 0) s_red[15] = cnt1;
+  for (int g = tid; g < G; g += blockDim.x) {
+    const unsigned long long k = take_key(g);
     const int p = k ? static_cast<int>(0xffffffffu - static_cast<uint32_t>(k)) : -1;
     s_pr[g] = p;
+    s_lab[g] = lab_of(g);
+    if (p >= 0) {
+      const int64_t i = static_cast<int64_t>(b) * P + p;
+      s_o0[g] = obj[i];
+      s_v0[g] = ovl[i];
+    }
     s_easy[g] = p >= 0 ? easy_of(p) : 0;
   }
   __syncthreads();
-  for (int g = tid; g < G; g += kFThreads) {
+  cnt1 = s_red[15];
+  for (int g = tid; g < G; g += blockDim.x) {
     int j = 0, prev = -1;
     const int p = s_pr[g];
     for (int h = 0; h < g; ++h) {
@@ -471,15 +433,15 @@ __global__ __launch_bounds__(kFThreads) void k_match_final(
   }
   __syncthreads();
   int delta = 0;
-  for (int g = tid; g < G; g += kFThreads) {
+  for (int g = tid; g < G; g += blockDim.x) {
     if (s_pr[g] < 0) continue;
     const int easy = s_easy[g] & 1, prev = (s_easy[g] >> 1) - 1;
     const int o_old = prev >= 0 ? s_new[prev] : s_o0[g];
     const float v_old = prev >= 0 ? 1.0f : s_v0[g];
-    delta += (is_pos(s_new[g], 1.0f, easy) ? 1 : 0) - (is_pos(o_old, v_old, easy) ? 1 : 0);
+    delta += (is_pos(s_lab[s_new[g]], 1.0f, easy) ? 1 : 0) - (is_pos(s_lab[o_old], v_old, easy) ? 1 : 0);
   }
   delta = block_sum(delta, s_red);
-  for (int g = tid; g < G; g += kFThreads) {
+  for (int g = tid; g < G; g += blockDim.x) {
     const int p = s_pr[g];
     if (p < 0) continue;
     bool lastw = true;   // superseded by a later writer?
@@ -491,6 +453,7 @@ __global__ __launch_bounds__(kFThreads) void k_match_final(
     ovl[i] = 1.0f;
   }
   if (tid == 0) publish(delta);
+  STAMP_END(7, 1);
 }
 
 // Pairwise IoU matrix out[b, g, p].
@@ -640,21 +603,24 @@ __global__ __launch_bounds__(1024) void k_ssd_match_final(
 using namespace sbod;
 
 namespace {
-// Matcher workspace: the per-(tile, object) 16-byte records [B][ntile][Gmax], then the per-tile
-// positive counts [B][ntile].
+// Matcher workspace: the per-(image, shard, object) best-prior keys [B][kKeyShards][Gmax] u64
+// (zero on entry, left zero by k_match_final), then the per-(image, wave) positive counts
+// [B][waves] i32 (written by every wave of k_match_tile, no initial state).
 struct MatchWs {
-  MRec *rec;
-  int32_t *tcount;
-  size_t bytes;
+  unsigned long long *best;
+  int32_t *wcnt;
+  int nw;
+  size_t key_bytes, bytes;
 };
 MatchWs carve_match(void *w, int B, int Gmax, int P) {
-  const size_t ntile = (P + kMThreads - 1) / kMThreads;
   MatchWs r;
+  r.nw = ((P + kMThreads - 1) / kMThreads) * (kMThreads / 64);
   size_t o = 0;
-  r.rec = ws_at<MRec>(w, o);
-  o += align_up(static_cast<size_t>(B) * ntile * Gmax * sizeof(MRec));
-  r.tcount = ws_at<int32_t>(w, o);
-  o += align_up(static_cast<size_t>(B) * ntile * 4);
+  r.best = ws_at<unsigned long long>(w, o);
+  o += align_up(static_cast<size_t>(B) * kKeyShards * Gmax * 8);
+  r.key_bytes = o;
+  r.wcnt = ws_at<int32_t>(w, o);
+  o += align_up(static_cast<size_t>(B) * r.nw * 4);
   r.bytes = o;
   return r;
 }
@@ -663,7 +629,7 @@ MatchWs carve_match(void *w, int B, int Gmax, int P) {
 extern "C" {
 
 size_t sbod_match_workspace_bytes_p(int B, int Gmax, int P) {
-  return carve_match(nullptr, B, Gmax > 0 ? Gmax : 1, P > 0 ? P : 1).bytes;
+  return carve_match(nullptr, B > 0 ? B : 1, Gmax > 0 ? Gmax : 1, P > 0 ? P : 1).bytes;
 }
 
 size_t sbod_match_workspace_bytes(int B, int Gmax) {
@@ -693,6 +659,8 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
                    obj && ovl && n_pos,
                "sbod_match_f32: bad arguments (B=%d Gmax=%d P=%d)", B, Gmax, P);
   SBOD_REQUIRE(Gmax <= 4096, "sbod_match_f32: Gmax %d > 4096 unsupported", Gmax);
+  SBOD_REQUIRE((flags & ~(SBOD_MATCH_BINARY | SBOD_MATCH_ODM | SBOD_MATCH_WS_ZEROED)) == 0,
+               "sbod_match_f32: unknown flags 0x%x", flags);
   const bool odm = (flags & SBOD_MATCH_ODM) != 0;
   SBOD_REQUIRE(!odm || (priors_cxcy && arm_scores), "sbod_match_f32: ODM needs priors and arm_scores");
   const size_t need = sbod_match_workspace_bytes_p(B, Gmax, P);
@@ -703,21 +671,25 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
   hipStream_t s = as_stream(stream);
   const int ntile = (P + kMThreads - 1) / kMThreads;
   MatchWs w = carve_match(workspace, B, Gmax, P);
+  // the keys and counts must be zero on entry: every call leaves them so (k_match_final), so
+  // only a workspace the caller does not know to be clean is zeroed here (not capturable)
+  if ((flags & SBOD_MATCH_WS_ZEROED) == 0 && hipMemsetAsync(workspace, 0, w.key_bytes, s) != hipSuccess)
+    return launch_status("hipMemsetAsync");
   dim3 grid(ntile, B);
+  const int fthreads = Gmax <= 64 ? 64 : kFThreads;
 #define SBOD_MATCH(ODM, FL)                                                                     \
   do {                                                                                          \
     {                                                                                           \
       KernelTimer kt("k_match_tile", s, true);                                                  \
-      tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads),                                \
-              static_cast<size_t>(Gmax > kMThreads ? Gmax : kMThreads) * 4, s,                      \
-              gt_boxes, gt_labels, gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, \
-              theta, obj, ovl, w.rec, w.tcount, n_pos, B, kt.span());                           \
+      tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads), 0, s, gt_boxes, gt_labels,     \
+              gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, ovl, \
+              w.best, w.wcnt, n_pos, B, kt.span());                                              \
     }                                                                                           \
     SBOD_LAUNCHED("k_match_tile");                                                              \
     KernelTimer kt("k_match_final", s, true);                                                   \
-    tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(kFThreads), static_cast<size_t>(Gmax) * 32, s, \
-            gt_labels, gt_offsets, w.rec, w.tcount, ntile, Gmax, P, threshold, arm_scores, theta, \
-            obj, ovl, n_pos, B);                                                                \
+    tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(fthreads),                                   \
+            Gmax <= 64 ? 0 : static_cast<size_t>(Gmax) * 24, s, gt_labels, gt_offsets, w.best,  \
+            w.wcnt, w.nw, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B);           \
   } while (0)
   if (odm)
     SBOD_MATCH(true, SBOD_MATCH_ODM);

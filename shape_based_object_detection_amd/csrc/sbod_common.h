@@ -356,26 +356,34 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
 #endif
 
 #ifdef SBOD_BLOCK_STAMPS
-#define SBOD_STAMP_CAP 65536u
+// Per-workgroup wall-clock stamps (diagnostic build): kernel ID (0..15) owns the region
+// [ID * kStampRegion, +kStampRegion) workgroups of its translation unit's buffer and records only
+// while bit ID of g_stamp_armed is set, so the kernels of one step (both graphs) can be recorded
+// together and lined up on one clock (scripts/step_timeline.py).
+#define SBOD_STAMP_REGION 4096u
+#define SBOD_STAMP_CAP (16u * SBOD_STAMP_REGION)
 #define SBOD_STAMP_DECL                                                  \
   static __device__ unsigned long long g_stamps[2 * SBOD_STAMP_CAP]; \
-  static __device__ int g_stamp_armed = -1;
+  static __device__ int g_stamp_armed = 0;
 #define STAMP_BEGIN() const unsigned long long _st0 = __builtin_amdgcn_s_memrealtime()
 // SYNC: 1 = the whole workgroup is still running (barrier first), 0 = the caller is the last wave
 #define STAMP_END(ID, SYNC)                                                                      \
   do {                                                                                           \
-    if (g_stamp_armed == (ID)) {                                                                 \
+    if (g_stamp_armed & (1 << (ID))) {                                                           \
       if (SYNC) __syncthreads();                                                                 \
       if ((threadIdx.x & 63) == 0 && ((SYNC) == 0 || threadIdx.x == 0)) {                        \
         const unsigned _blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);    \
-        if (_blk < SBOD_STAMP_CAP) {                                                          \
-          g_stamps[2 * _blk] = _st0;                                                             \
-          g_stamps[2 * _blk + 1] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) |     \
-                                   (static_cast<unsigned long long>(__smid() & 0xffff) << 48);  \
+        if (_blk < SBOD_STAMP_REGION) {                                                          \
+          const unsigned _i = (ID) * SBOD_STAMP_REGION + _blk;                                   \
+          g_stamps[2 * _i] = _st0;                                                               \
+          g_stamps[2 * _i + 1] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) |       \
+                                 (static_cast<unsigned long long>(__smid() & 0xffff) << 48);    \
         }                                                                                        \
       }                                                                                          \
     }                                                                                            \
   } while (0)
+// arm = bit mask of kernel IDs to record from now on; host (n > 0): copy the first n stamp pairs
+// of the buffer out BEFORE clearing it.
 #define SBOD_STAMP_EXPORT(TU)                                                                    \
   extern "C" int sbod_debug_stamps_##TU(int arm, unsigned long long *host, int n) {              \
     if (host && n > 0)                                                                           \
