@@ -435,7 +435,8 @@ def c2_figure(dev, steps, warmup, B=16, n_batches=12):
     st.capture()
     for _ in range(len(st.slots) + 1):
         st.replay()
-    el = timed(st.pipelined, steps, None, dev, finish=st.drain)
+    with torch.cuda.stream(st.cap_stream):
+        el = timed(st.pipelined, steps, None, dev, finish=st.drain)
     ms = el / steps * 1e3
     crit_b = B * st.P * 2 * (4 + N_CLASSES) * 2 + 16 * st.P
     del st
@@ -592,7 +593,10 @@ def main():
         for _ in range(len(st.slots) + 1):
             st.replay()
         st.host_submit = st.host_collect = 0.0
-        elapsed = timed(st.pipelined, a.steps, dist, dev, finish=st.drain)
+        # the training loop's current stream is the criterion's: the GT lists it hands over
+        # are ordered on the stream that packs them (no cross-stream event pair per step)
+        with torch.cuda.stream(st.cap_stream):
+            elapsed = timed(st.pipelined, a.steps, dist, dev, finish=st.drain)
         host_submit, host_collect = st.host_submit, st.host_collect
         # the in-graph span of the dominant kernel (a host-synchronous read, so outside the
         # timed region): each batch's graph keeps the record of its latest replay, so after
