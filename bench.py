@@ -74,6 +74,8 @@ def parse(argv=None):
                     help='graph mode: which of the two streams gets the high HIP stream priority')
     ap.add_argument('--order', choices=('criterion_first', 'detect_first'), default='criterion_first',
                     help='graph mode: which graph of a step is submitted first')
+    ap.add_argument('--det-streams', type=int, default=2,
+                    help='graph mode: streams the detect graphs alternate over (1 = one detect stream)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-dcn', action='store_true')
     ap.add_argument('--batches', type=int, default=6,
@@ -245,7 +247,7 @@ class Step:
     buffer and the two-deep pipeline (submit step k, then collect step k-1) needs no copies."""
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
-                 dtype=torch.float32, order='criterion_first'):
+                 dtype=torch.float32, order='criterion_first', det_streams=2):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -265,7 +267,13 @@ class Step:
         # a fork/join INSIDE one graph costs ~30 us per edge on this runtime
         # (scripts/probe_graph_launch.py), two graphs on two streams need no edge at all.
         self.cap_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'criterion' else 0)
-        self.det_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'detect' else 0)
+        # detect graphs alternate over `det_streams` streams (batch i on stream i mod n): step k's
+        # prepare need not wait for step k-1's segment / merge (latency-bound, few workgroups),
+        # so the two overlap instead of the detect chain setting the step period
+        self.det_streams = [torch.cuda.Stream(dev, priority=-1 if priority == 'detect' else 0)
+                            for _ in range(max(1, det_streams))]
+        self.det_stream = self.det_streams[0]
+        self._det_warm = set()
         self.two = two_streams
         self.detect_first = order == 'detect_first'
         self.graph = None
@@ -312,13 +320,15 @@ class Step:
         bt = self._next_batch()
         bt.locs.grad = None
         bt.scores.grad = None
+        ds = self.det_streams[(self.k - 1) % len(self.batches) % len(self.det_streams)]
         self.cap_stream.wait_stream(torch.cuda.current_stream(self.dev))
-        self.det_stream.wait_stream(torch.cuda.current_stream(self.dev))
+        ds.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(self.cap_stream):
             gt = self.stage.stage(bt.boxes, bt.labels)
             loss = self.crit(bt.locs, bt.scores, gt, None)
-        with torch.cuda.stream(self.det_stream):
+        with torch.cuda.stream(ds):
             h = self.detect(bt, False)
+        self._det_warm.add(ds.cuda_stream)
         with torch.cuda.stream(self.cap_stream):
             loss.backward(self.one)
         out = loss, h.wait()
@@ -331,10 +341,16 @@ class Step:
         them).  ``after_first`` runs after the first batch's capture."""
         gt = self.stage.stage(self.batches[0].boxes, self.batches[0].labels)
         n = len(self.batches)
+        for ds in self.det_streams:   # every detect stream's workspace exists before capture
+            if ds.cuda_stream not in self._det_warm:
+                ds.wait_stream(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(ds):
+                    self.detect(self.batches[0], False).wait()
+                self._det_warm.add(ds.cuda_stream)
         core.reserve_count_slots(self.dev, self.B, n)
         torch.cuda.synchronize()
         self.slots = []
-        for bt in self.batches:
+        for bi, bt in enumerate(self.batches):
             bt.locs.grad = None
             bt.scores.grad = None
             if self.two:
@@ -342,7 +358,7 @@ class Step:
                 with torch.cuda.graph(ga, stream=self.cap_stream):
                     loss = self.crit(bt.locs, bt.scores, gt, None)
                     loss.backward(self.one)
-                with torch.cuda.graph(gb, stream=self.det_stream):
+                with torch.cuda.graph(gb, stream=self.det_streams[bi % len(self.det_streams)]):
                     h = self.detect(bt, True)
                 self.slots.append((ga, gb, loss, h))
             else:
@@ -360,12 +376,13 @@ class Step:
         self.fast = None
         if self.two and L.host_ext is not None:
             self.fast = []
-            for ga, gb, _, h in self.slots:
-                h.replayed(self.det_stream)          # creates the event (recorded once here)
-                pairs = [(ga, self.cap_stream), (gb, self.det_stream)]
+            for bi, (ga, gb, _, h) in enumerate(self.slots):
+                ds = self.det_streams[bi % len(self.det_streams)]
+                h.replayed(ds)          # creates the event (recorded once here)
+                pairs = [(ga, self.cap_stream), (gb, ds)]
                 if self.detect_first:
                     pairs.reverse()
-                self.fast.append((core.graph_launches(pairs), h._event.cuda_event, self.det_stream.cuda_stream))
+                self.fast.append((core.graph_launches(pairs), h._event.cuda_event, ds.cuda_stream))
             torch.cuda.synchronize()
         self.k = 0
         self.pending = None
@@ -389,9 +406,10 @@ class Step:
         with torch.cuda.stream(self.cap_stream):
             self.stage.stage(bt.boxes, bt.labels)
             ga.replay()
-        with torch.cuda.stream(self.det_stream):
+        ds = self.det_streams[i % len(self.det_streams)]
+        with torch.cuda.stream(ds):
             gb.replay()
-            return loss, h.replayed(self.det_stream)
+            return loss, h.replayed(ds)
 
     def replay(self):
         loss, h = self.launch_replay()
@@ -532,7 +550,7 @@ def main():
     L.lib()
     B = a.batch
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
-              n_batches=a.batches, order=a.order)
+              n_batches=a.batches, order=a.order, det_streams=a.det_streams)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -636,6 +654,7 @@ def main():
         'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
+        'detect_streams': len(st.det_streams),
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }

@@ -29,6 +29,9 @@ KERNELS = [('gtpack', 8, 'k_gt_pack'), ('match', 5, 'k_match_tile'), ('match', 7
 def main():
     steps = int(sys.argv[sys.argv.index('--steps') + 1]) if '--steps' in sys.argv else 20
     mode = sys.argv[sys.argv.index('--mode') + 1] if '--mode' in sys.argv else 'pipelined'
+    order = sys.argv[sys.argv.index('--order') + 1] if '--order' in sys.argv else 'criterion_first'
+    prio = sys.argv[sys.argv.index('--priority') + 1] if '--priority' in sys.argv else 'detect'
+    nds = int(sys.argv[sys.argv.index('--det-streams') + 1]) if '--det-streams' in sys.argv else 2
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     lib = L.lib()
@@ -37,7 +40,7 @@ def main():
         f = getattr(lib, 'sbod_debug_stamps_' + tu)
         f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         fns[tu] = f
-    st = bench.Step(dev, 32, 0, 1, graph=True, two_streams=True, priority='criterion')
+    st = bench.Step(dev, 32, 0, 1, graph=True, two_streams=True, priority=prio, order=order, det_streams=nds)
     for _ in range(3):
         st.eager_split()
     torch.cuda.synchronize()
@@ -60,10 +63,12 @@ def main():
     def det_only():
         i = st.k % len(st.slots)
         st._next_batch()
-        with torch.cuda.stream(st.det_stream):
+        with torch.cuda.stream(st.det_streams[i % len(st.det_streams)]):
             st.slots[i][1].replay()
 
     fn = {'pipelined': st.pipelined, 'crit': crit_only, 'det': det_only}[mode]
+    ctx = torch.cuda.stream(st.cap_stream)   # as bench.py's timed loop
+    ctx.__enter__()
     reps = []
     for rep in range(3):
         for _ in range(steps):
@@ -94,7 +99,8 @@ def main():
                          'block_us_median': round(float(np.median(d)), 2),
                          'block_us_max': round(float(d.max()), 2)}
         reps.append(out)
-        print(json.dumps({'mode': mode, 'rep': rep, 'kernels': out}), flush=True)
+        print(json.dumps({'mode': mode, 'order': order, 'priority': prio, 'det_streams': nds, 'rep': rep,
+                          'kernels': out}), flush=True)
 
 
 if __name__ == '__main__':

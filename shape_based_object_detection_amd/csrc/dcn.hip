@@ -541,8 +541,22 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
     float g[4], m, tlx, rbx, tly, rby;
     int inr;
   };
+  // Address arithmetic.  AVEC (every 32-pixel chunk whole and inside one image): the chunk's
+  // image and first pixel are wave-uniform (scalar unit), the per-lane parts (channel offsets,
+  // this lane's pixel row / output channel rows) are loop-invariant 32-bit offsets, so a chunk
+  // costs one 64-bit add per load instead of divisions and 64-bit multiply-adds per lane.
+  int cofs[8 / VEC];   // this lane's channel offsets, clamped into the row
+#pragma unroll
+  for (int v = 0; v < 8; v += VEC) cofs[v / VEC] = min(c0 + scg + v, s.C - VEC);
+  const int lane_cf = smm * s.N;                       // coef rows of this lane's pixel
+  const int lane_dc = smm * s.N * s.C;                 // dcols rows of this lane's pixel
+  int lane_o[2];                                       // dout rows (o * HWo) of this lane
+#pragma unroll
+  for (int ri = 0; ri < 2; ++ri) lane_o[ri] = min(o0 + 64 * wv + 32 * ri + l31, s.O - 1) * HWo;
   auto load_cf = [&](int m0) {
-    const float *c = reinterpret_cast<const float *>(coef + static_cast<int64_t>(min(m0 + smm, mend - 1)) * s.N + n);
+    const Coef *cp = AVEC ? coef + (static_cast<int64_t>(m0) * s.N + n) + lane_cf
+                          : coef + static_cast<int64_t>(min(m0 + smm, mend - 1)) * s.N + n;
+    const float *c = reinterpret_cast<const float *>(cp);
     float2 w[7];   // a Coef is 8-byte aligned (56 bytes)
 #pragma unroll
     for (int j = 0; j < 7; ++j) w[j] = reinterpret_cast<const float2 *>(c)[j];
@@ -562,42 +576,55 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
   auto gather = [&](int m0, const CfW &cf) {
-    const int m = min(m0 + smm, mend - 1);
-    const float *xb = xt + static_cast<int64_t>(m / HWo) * HW * s.C;
+    const float *xb;
+    if (AVEC) {
+      xb = xt + static_cast<int64_t>(m0 / HWo) * HW * s.C;   // uniform
+    } else {
+      const int m = min(m0 + smm, mend - 1);
+      xb = xt + static_cast<int64_t>(m / HWo) * HW * s.C;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float *p = xb + static_cast<int64_t>(max(cf.idx[q], 0)) * s.C;
+      // corner pixel * C: both factors < 2^24 (per-image sizes are validated below 2^31)
+      const float *p = xb + __umul24(static_cast<uint32_t>(max(cf.idx[q], 0)), static_cast<uint32_t>(s.C));
 #pragma unroll
       for (int v = 0; v < 8; v += VEC) {
-        const int c = c0 + scg + v;
-        xok[q][v / VEC] = cf.idx[q] >= 0 && c < s.C;
-        load_vec<VEC>(p + min(c, s.C - VEC), true, &X[q][v]);
+        xok[q][v / VEC] = cf.idx[q] >= 0 && c0 + scg + v < s.C;
+        load_vec<VEC>(p + cofs[v / VEC], true, &X[q][v]);
       }
     }
     if constexpr (DOFS) {
-      const float *dr = dcols + (static_cast<int64_t>(m) * s.N + n) * s.C;
+      const float *dr = AVEC ? dcols + (static_cast<int64_t>(m0) * s.N + n) * s.C + lane_dc
+                             : dcols + (static_cast<int64_t>(min(m0 + smm, mend - 1)) * s.N + n) * s.C;
 #pragma unroll
-      for (int v = 0; v < 8; v += VEC) load_vec<VEC>(dr + min(c0 + scg + v, s.C - VEC), true, &D[v]);
+      for (int v = 0; v < 8; v += VEC) load_vec<VEC>(dr + cofs[v / VEC], true, &D[v]);
     }
   };
-  // live: this chunk's offset / mask partials are added (false for the prefetch past the last)
+  // live: this chunk's offset / mask partials are added (false for the prefetch past the last).
+  // The column value and the offset / mask partials use fused multiply-adds (the weight and
+  // offset / mask gradients are checked to fp32 tolerance, not bit-exactly):
+  //   raw = g0 X0 + g1 X1 + g2 X2 + g3 X3,
+  //   d/dx = (1 + tly)(X3 - X0) + (1 - rby)(X1 - X2),  d/dy = (1 + tlx)(X2 - X0) + (1 - rbx)(X1 - X3)
+  // (Deformable_convolution.py:59-91 by autograd, corners lt, rb, lb, rt).
   auto store_cols = [&](int buf, const CfW &cf, int m0, bool live) {
-    const bool ok = m0 + smm < mend;
+    const bool ok = AVEC || m0 + smm < mend;
     const float cm = cf.m;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int v = 0; v < 8; ++v) X[q][v] = (ok && xok[q][v / VEC]) ? X[q][v] : 0.f;
     float pm = 0.f, ppx = 0.f, ppy = 0.f;
+    const float ay = 1.f + cf.tly, by = 1.f - cf.rby, ax = 1.f + cf.tlx, bx = 1.f - cf.rbx;
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
-      const float raw = ((cf.g[0] * X[0][v] + cf.g[1] * X[1][v]) + cf.g[2] * X[2][v]) + cf.g[3] * X[3][v];
-      s_cols[buf][smm][scg + v] = raw * cm;   // == combine(): the forward's column value
+      const float raw = __builtin_fmaf(cf.g[3], X[3][v], __builtin_fmaf(cf.g[2], X[2][v],
+                                       __builtin_fmaf(cf.g[1], X[1][v], cf.g[0] * X[0][v])));
+      s_cols[buf][smm][scg + v] = raw * cm;
       if constexpr (DOFS) {
         const float d = c0 + scg + v < s.C ? D[v] : 0.f;
-        pm += d * raw;
-        ppx += d * (-(1.f + cf.tly) * X[0][v] + (1.f - cf.rby) * X[1][v] - (1.f - cf.rby) * X[2][v] + (1.f + cf.tly) * X[3][v]);
-        ppy += d * (-(1.f + cf.tlx) * X[0][v] + (1.f - cf.rbx) * X[1][v] + (1.f + cf.tlx) * X[2][v] - (1.f - cf.rbx) * X[3][v]);
+        pm = __builtin_fmaf(d, raw, pm);
+        ppx = __builtin_fmaf(d, __builtin_fmaf(ay, X[3][v] - X[0][v], by * (X[1][v] - X[2][v])), ppx);
+        ppy = __builtin_fmaf(d, __builtin_fmaf(ax, X[2][v] - X[0][v], bx * (X[1][v] - X[3][v])), ppy);
       }
     }
     if constexpr (DOFS) {   // the 8 lanes of this pixel are lanes 8k..8k+7: quad swaps + half-row mirror
@@ -624,15 +651,17 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
   };
   auto load_a = [&](int m0, float (&a)[2][16]) {   // dout rows; pixels past the slice meet zero columns
     const int mb = m0 + 16 * h;
+    if (AVEC) {   // 32-pixel chunks inside one image, slices of whole chunks: mb + 15 < mend
+      const int b = m0 / HWo;   // uniform
+      const float *pb = gout + static_cast<int64_t>(b) * s.O * HWo + (mb - b * HWo);
 #pragma unroll
-    for (int ri = 0; ri < 2; ++ri) {
-      const int o = min(o0 + 64 * wv + 32 * ri + l31, s.O - 1);
-      if (AVEC) {   // 32-pixel chunks inside one image, slices of whole chunks: mb + 15 < mend
-        const int b = mb / HWo, pix = mb - b * HWo;
-        const float *p = gout + (static_cast<int64_t>(b) * s.O + o) * HWo + pix;
+      for (int ri = 0; ri < 2; ++ri)
 #pragma unroll
-        for (int v = 0; v < 16; v += 4) load_vec<4>(p + v, true, &a[ri][v]);
-      } else {
+        for (int v = 0; v < 16; v += 4) load_vec<4>(pb + lane_o[ri] + v, true, &a[ri][v]);
+    } else {
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri) {
+        const int o = min(o0 + 64 * wv + 32 * ri + l31, s.O - 1);
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
           const int m = min(mb + v, mend - 1);

@@ -657,18 +657,27 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, T *__restrict
     // this phase was ~6K of ~16K cycles per workgroup in the per-lane form).
     // (plain stores: these 8-byte scattered writes must merge into full lines in L2 first —
     // streamed through they cost 1.7x the kernel time)
+    // every class's slot base read from LDS up front (one wait, not one LDS round trip per
+    // class); a lane's rank among the wave's takers is v_mbcnt of the scalar mask; whether the
+    // lane takes class k is bit KN-1-k of cmask (no 64-bit mask test per class)
     unsigned long long *cb = a.cand + static_cast<int64_t>(b) * C * P;
+    uint32_t wb[KN];
+#pragma unroll
+    for (int k = 1; k < KN; ++k) wb[k] = k < C ? s_wb(wv, k) : 0u;
+    const uint32_t klow = 0xffffffffu - static_cast<uint32_t>(p);
 #pragma unroll
     for (int k = 1; k < KN; ++k) {
       if (k < C && bals[k] != 0ull) {
-        const uint32_t base = __builtin_amdgcn_readfirstlane(s_wb(wv, k));
-        const uint32_t slot = base + __popcll(bals[k] & lt);
+        const uint32_t base = __builtin_amdgcn_readfirstlane(wb[k]);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bals[k] >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bals[k]), 0u));
+        const uint32_t slot = base + rank;
         // slot < P always with counters zero on entry (memory-safe otherwise)
-        if (((bals[k] >> lane) & 1ull) && slot < static_cast<uint32_t>(P))
-          cb[static_cast<int64_t>(k) * P + slot] = make_key(r[k], static_cast<uint32_t>(p));
+        if (((cmask >> (KN - 1 - k)) & 1u) && slot < static_cast<uint32_t>(P))
+          cb[static_cast<int64_t>(k) * P + slot] = (static_cast<unsigned long long>(f2ord(r[k])) << 32) | klow;
       }
     }
-    (void)cmask;
+    (void)lt;
   } else {
     SEG_PHASE(2);
     for (int c = 1; c < C; ++c) {
