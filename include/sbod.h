@@ -122,10 +122,10 @@ int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int 
  *   n_pos [B+1] int32: positives per image (+ the batch total at n_pos[B]).  Labels and the
  *   negative mask are derived from (obj, ovl, gt_labels) by the loss kernels.
  * Workspace: sbod_match_workspace_bytes(B, Gmax): per-(image, object) best-prior keys and
- * per-image positive counts, which must be zero on entry.  Every successful call leaves them
- * zero, so a caller that knows the workspace is clean (a previous successful call on it, or its
- * own memset) passes SBOD_MATCH_WS_ZEROED and the call issues no memset (hipGraph capture);
- * without the flag the call zeroes them first (hipMemsetAsync). */
+ * per-wave positive counts, which must be zero on entry.  Every successful call leaves the
+ * whole workspace zero, so a caller that knows it is clean (a previous successful call on it,
+ * of any shape, or its own memset) passes SBOD_MATCH_WS_ZEROED and the call issues no memset
+ * (hipGraph capture); without the flag the call zeroes it first (hipMemsetAsync). */
 enum { SBOD_MATCH_BINARY = 1, SBOD_MATCH_ODM = 2, SBOD_MATCH_WS_ZEROED = 256 };
 size_t sbod_match_workspace_bytes(int B, int Gmax);          /* enough for P <= 2^20 */
 size_t sbod_match_workspace_bytes_p(int B, int Gmax, int P);  /* exact for this P */
@@ -205,6 +205,12 @@ size_t sbod_loss_workspace_bytes(int B, int P);
  * holding the whole batch; the hard-negative gradients and the loss cover this rank's rows
  * (the sum over ranks is the single-device loss).  Same workspace as the deferred call. */
 enum { SBOD_LOSS_DEFER_MINING = 64 };
+/* Focal criteria (no mining pass) finish the loss inside the fused pass: its workgroups fold
+ * their partial sums into fixed-point accumulators in the workspace's first 4224 bytes, which must
+ * be zero on entry and are left zero by every successful call (any B, P).  A caller that knows the workspace is clean (a
+ * previous successful call on it) passes SBOD_LOSS_WS_ZEROED and the call issues no memset
+ * (hipGraph capture); without it the call zeroes them first (hipMemsetAsync, 4224 bytes). */
+enum { SBOD_LOSS_WS_ZEROED = 128 };
 size_t sbod_loss_pool_offset(int B, int P);
 int sbod_multibox_mine_global(const void *scores, int dtype, int B, int P, int C,
                               const int32_t *npos_total, int reg, int cls, int flags,

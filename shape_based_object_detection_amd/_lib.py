@@ -79,6 +79,7 @@ CLS = dict(focal=0, ce=1)
 DT_F32, DT_BF16 = 0, 1
 LOSS_FOCAL_NORM = 4
 LOSS_DEFER_MINING = 64
+LOSS_WS_ZEROED = 128
 POOL = dict(nonpos=0, neg=8, global_neg=16, nonpos_not_easy=32)
 OV = dict(iou=0, giou=1, diou=2, ciou=3)
 FOCAL = dict(softmax=0, sigmoid=1, bce=2)

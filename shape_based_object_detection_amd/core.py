@@ -405,12 +405,16 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
         nb = L.lib().sbod_loss_workspace_bytes(B, P)
         ws = workspace(nb, dev, 'loss')
         flags = spec.flags | (L.LOSS_DEFER_MINING if exchange is not None else 0)
+        # the fused finish's accumulators are left zero by every successful call
+        zflag = _zeroed_flag(ws, _LOSS_ZERO_PREFIX, L.LOSS_WS_ZEROED, 'criterion')
+        _CLEAN.pop(ws.data_ptr(), None)
         L.call('sbod_multibox_loss', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy),
                L.ptr(arm_locs), L.ptr(arm_scores), L.ptr(gt.boxes), L.ptr(gt.labels),
                L.ptr(gt.offsets), L.ptr(obj), L.ptr(ovl), L.ptr(n_pos), L.ptr(npos_total),
-               float(threshold), float(neg_threshold), float(theta), spec.reg, spec.cls, flags,
+               float(threshold), float(neg_threshold), float(theta), spec.reg, spec.cls, flags | zflag,
                int(spec.neg_pos_ratio), float(spec.reg_weight), float(spec.alpha), float(spec.gamma),
                L.ptr(gl), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
+        _CLEAN[ws.data_ptr()] = _LOSS_ZERO_PREFIX   # (only the accumulator prefix is zero)
         if exchange is not None:
             off = L.lib().sbod_loss_pool_offset(B, P)
             pool = ws.narrow(0, off, 4 * B * P).view(torch.float32)
@@ -572,6 +576,7 @@ def _count_slot(dev, B):
 # leaves its candidate counters zero, so after the first call on a workspace no memset is
 # needed — none in a captured graph (SBOD_DETECT_COUNTERS_ZEROED).
 _CLEAN = {}
+_LOSS_ZERO_PREFIX = 4224   # sbod_multibox_loss: the fused finish's accumulators (include/sbod.h)
 
 
 def _zeroed_flag(ws, need, flag, what):

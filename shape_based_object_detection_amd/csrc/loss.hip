@@ -14,6 +14,8 @@
 // Roofline: HBM-bound; algorithmic bytes per launch = B*P*(4+C)*s read + B*P*(4+C)*s written.
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
+
 #include "sbod_common.h"
 
 namespace sbod {
@@ -313,7 +315,86 @@ struct LossArgs {
   float reg_weight, afg, abg, gamma;
   float *partials, *pool;
   SpanRing *span;             // KernelTimer span ring under graph capture, else null
+  // fused finish (no mining pass): fixed-point sums {conf, loc}, non-finite flags and the
+  // arrival counter of the workgroups; null: partials for k_loss_final
+  unsigned long long *fin;
+  float *out;                 // the loss vector {total, conf, loc, n_pos} (fused finish)
 };
+
+// The fused finish of k_multibox (focal / no mining).  Each workgroup folds its partial sums
+// into two 64-bit fixed-point accumulators (value * 2^32, rounded; integer adds are exact and
+// order-free, so the result is bitwise reproducible) with agent-scope atomics executed at the
+// memory side, waits for them, then counts itself in; the workgroup whose count comes last reads
+// the sums back with exchanges (which also leave them zero for the next call) and writes the
+// loss vector exactly as k_loss_final would.  Non-finite partials (NaN rows of the focal loss)
+// travel as flag bits: NaN, +inf, -inf per component.  No data moves through plain stores, so no
+// cache write-back or invalidation is needed between the XCDs.
+constexpr float kFinScale = 4294967296.f;   // 2^32
+__device__ __forceinline__ unsigned nonfinite_bits(float v) {
+  if (v != v) return 1u;
+  if (v == __builtin_inff()) return 2u;
+  if (v == -__builtin_inff()) return 4u;
+  return 0u;
+}
+__device__ __forceinline__ double fin_value(unsigned long long fx, unsigned bits) {
+  if ((bits & 1u) || ((bits & 6u) == 6u)) return __builtin_nan("");
+  if (bits & 2u) return __builtin_inf();
+  if (bits & 4u) return -__builtin_inf();
+  return static_cast<double>(static_cast<long long>(fx)) / 4294967296.0;
+}
+__device__ __forceinline__ void loss_outputs(double c, double l, float n, int reg, int cls, int flags,
+                                             float reg_weight, float *out) {
+  const float conf = (cls == SBOD_CLS_CE || (flags & SBOD_LOSS_FOCAL_NORM)) ? static_cast<float>(c) / n
+                                                                            : static_cast<float>(c);
+  const float loc = reg == SBOD_REG_L1 ? static_cast<float>(l) / (4.f * n) : static_cast<float>(l) / n;
+  out[0] = conf + reg_weight * loc;
+  out[1] = conf;
+  out[2] = loc;
+  out[3] = n;
+}
+constexpr int kFinGroups = 32;   // workgroup groups (linear id mod 32), then one global level
+constexpr int kFinStride = 16;   // u64 words per accumulator set: one 128-byte line each
+constexpr size_t kFinBytes = sizeof(unsigned long long) * kFinStride * (kFinGroups + 1);   // 4224
+__device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, unsigned nblk, float *out) {
+  // accumulators: kFinGroups group lines, then the top line; each {conf, loc, flags, arrivals}.
+  // Two levels because atomics on one word serialise at the memory side (~10 ns each): ~41
+  // arrivals per group word and 32 on the top word instead of every workgroup on one word.
+  const unsigned blk = blockIdx.x + gridDim.x * blockIdx.y;
+  const unsigned ng = nblk < kFinGroups ? nblk : kFinGroups, g = blk % ng;
+  const unsigned in_group = (nblk - g + ng - 1) / ng;
+  unsigned long long *acc = a.fin + kFinStride * g, *top = a.fin + kFinStride * kFinGroups;
+  const unsigned long long bits = nonfinite_bits(conf_l) | (nonfinite_bits(loc_l) << 3);
+  unsigned long long cf = 0, lf = 0;
+  if (!bits) {
+    cf = static_cast<unsigned long long>(__float2ll_rn(conf_l * kFinScale));
+    lf = static_cast<unsigned long long>(__float2ll_rn(loc_l * kFinScale));
+  }
+  auto fold = [&](unsigned long long *w, unsigned long long c, unsigned long long l, unsigned long long f,
+                  unsigned count) {   // true: this caller's count came last on w
+    if (f) __hip_atomic_fetch_or(w + 2, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c) __hip_atomic_fetch_add(w, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l) __hip_atomic_fetch_add(w + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);   // the adds are performed before the count
+    return __hip_atomic_fetch_add(w + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
+  };
+  auto drain = [&](unsigned long long *w, unsigned long long &c, unsigned long long &l, unsigned long long &f) {
+    c = __hip_atomic_exchange(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    l = __hip_atomic_exchange(w + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f = __hip_atomic_exchange(w + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(w + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (!fold(acc, cf, lf, bits, in_group)) return;
+  // this group is complete (every member's adds were performed before it counted itself in):
+  // its totals move to the top line (four exchanges in flight, leaving the group line zero),
+  // and the workgroup that completes the top line drains it.  (Draining all 32 group lines from
+  // the last workgroup instead serialised one lane's exchanges: +9 µs.)
+  unsigned long long c, l, f;
+  drain(acc, c, l, f);
+  if (!fold(top, c, l, f, ng)) return;
+  drain(top, c, l, f);
+  loss_outputs(fin_value(c, static_cast<unsigned>(f) & 7u), fin_value(l, static_cast<unsigned>(f >> 3) & 7u),
+               static_cast<float>(*a.npos_total), a.reg, a.cls, a.flags, a.reg_weight, out);
+}
 
 // exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'
 // budget is 1e-4 relative; the all-classes underflow test (p == 0 -> NaN) stays exact (below).
@@ -638,9 +719,13 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
            ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
 #endif
   if (tid == 0) {
-    const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
-    a.partials[2 * blk] = conf_l;
-    a.partials[2 * blk + 1] = loc_l;
+    if (a.fin != nullptr) {
+      multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, a.out);
+    } else {
+      const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
+      a.partials[2 * blk] = conf_l;
+      a.partials[2 * blk + 1] = loc_l;
+    }
   }
   span_end(a.span);
   STAMP_END(4, 1);
@@ -802,16 +887,7 @@ __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ pa
   c = block_sum(c, s_red);
   __syncthreads();
   l = block_sum(l, s_red);
-  if (threadIdx.x == 0) {
-    const float n = static_cast<float>(*npos_total);
-    const float conf = (cls == SBOD_CLS_CE || (flags & SBOD_LOSS_FOCAL_NORM))
-                           ? static_cast<float>(c) / n : static_cast<float>(c);
-    const float loc = reg == SBOD_REG_L1 ? static_cast<float>(l) / (4.f * n) : static_cast<float>(l) / n;
-    out[0] = conf + reg_weight * loc;
-    out[1] = conf;
-    out[2] = loc;
-    out[3] = n;
-  }
+  if (threadIdx.x == 0) loss_outputs(c, l, static_cast<float>(*npos_total), reg, cls, flags, reg_weight, out);
   STAMP_END(6, 1);
 }
 
@@ -917,14 +993,19 @@ using namespace sbod;
 namespace {
 struct LossWs {
   float *partials, *pool, *hnm;
+  unsigned long long *fin;
   size_t pool_off;   // byte offset of `pool` (sbod_loss_pool_offset)
   size_t bytes;
 };
 LossWs carve(void *w, int B, int P) {
   const size_t nblk = static_cast<size_t>(B) * ((P + kLTile - 1) / kLTile);
   LossWs r;
-  r.partials = ws_at<float>(w, 0);
-  size_t o = align_up(nblk * 2 * sizeof(float));
+  // the fused finish's accumulators first: a fixed prefix whatever B and P are, so "the first
+  // 32 bytes are zero" (SBOD_LOSS_WS_ZEROED) carries over between calls of different shapes
+  r.fin = ws_at<unsigned long long>(w, 0);
+  size_t o = align_up(kFinBytes);
+  r.partials = ws_at<float>(w, o);
+  o += align_up(nblk * 2 * sizeof(float));
   r.pool = ws_at<float>(w, o);
   r.pool_off = o;
   o += align_up(static_cast<size_t>(B) * P * sizeof(float));
@@ -998,9 +1079,19 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
     return SBOD_E_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
+  // no mining pass (focal): the fused pass finishes the loss itself (multibox_finish), so the
+  // step has no k_loss_final launch; its accumulators are zero on entry (SBOD_LOSS_WS_ZEROED)
+  // (every call without the flag zeroes them, fused or not: a caller marks the workspace clean
+  // after ANY successful call, and a mining-path call never touches them)
+  const bool fused = cls == SBOD_CLS_FOCAL && !(flags & SBOD_LOSS_DEFER_MINING) &&
+                     std::getenv("SBOD_NO_FUSED_FINISH") == nullptr;   // (A/B and diagnosis)
+  if ((flags & SBOD_LOSS_WS_ZEROED) == 0 &&
+      hipMemsetAsync(ws.fin, 0, kFinBytes, s) != hipSuccess)
+    return launch_status("hipMemsetAsync(loss)");
   LossArgs a{B, P, C, priors_cxcy, odm_arm_locs, arm_scores, gt_boxes, gt_labels, gt_offsets, obj,
              npos_total, ovl, threshold, neg_threshold, theta, reg, cls, flags, reg_weight,
-             focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool, nullptr};
+             focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool, nullptr,
+             fused ? ws.fin : nullptr, loss_out};
   dim3 grid((P + kLTile - 1) / kLTile, B);
   // + 8 floats: the register path's constant-offset row reads may run up to 7 past the last row
   const size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
@@ -1033,6 +1124,7 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
 #undef SBOD_MB
   }
   SBOD_LAUNCHED("k_multibox");
+  if (fused) return SBOD_OK;
   if (flags & SBOD_LOSS_DEFER_MINING) return SBOD_OK;   // the caller exchanges the pool first
   return mine_and_finish(scores, dtype, B, P, C, n_pos, npos_total, reg, cls, flags, neg_pos_ratio,
                          reg_weight, ws.pool, static_cast<int64_t>(B) * P, 0, grad_scores, loss_out, ws, s);

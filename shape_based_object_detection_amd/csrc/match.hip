@@ -305,7 +305,7 @@ constexpr int kFThreads = 256;
 template <int kFlags>
 __global__ __launch_bounds__(kFThreads) void k_match_final(
     const int64_t *__restrict__ labels, const int32_t *__restrict__ off,
-    unsigned long long *__restrict__ best_key, const int32_t *__restrict__ wcnt, int nw, int Gmax,
+    unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt, int nw, int Gmax,
     int P, float thr, const float *__restrict__ arm_scores, float theta, int32_t *__restrict__ obj,
     float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
@@ -318,7 +318,11 @@ __global__ __launch_bounds__(kFThreads) void k_match_final(
   // shares it through s_red)
   int cnt1 = 0;
   if (tid < 64) {
-    for (int w = lane; w < nw; w += 64) cnt1 += wcnt[static_cast<int64_t>(b) * nw + w];
+    for (int w = lane; w < nw; w += 64) {
+      int32_t *c = wcnt + static_cast<int64_t>(b) * nw + w;
+      cnt1 += *c;
+      *c = 0;   // the whole workspace is zero again after a call (any B, Gmax, P next time)
+    }
     cnt1 = wave_sum_i32(cnt1);
   }
   // an object's key: the max over its shards, which return to zero
@@ -604,13 +608,14 @@ using namespace sbod;
 
 namespace {
 // Matcher workspace: the per-(image, shard, object) best-prior keys [B][kKeyShards][Gmax] u64
-// (zero on entry, left zero by k_match_final), then the per-(image, wave) positive counts
-// [B][waves] i32 (written by every wave of k_match_tile, no initial state).
+// (zero on entry), then the per-(image, wave) positive counts [B][waves] i32 (written by every
+// wave of k_match_tile).  k_match_final leaves ALL of it zero, so a workspace known clean stays
+// clean for a later call of any shape that fits in it (SBOD_MATCH_WS_ZEROED).
 struct MatchWs {
   unsigned long long *best;
   int32_t *wcnt;
   int nw;
-  size_t key_bytes, bytes;
+  size_t bytes;
 };
 MatchWs carve_match(void *w, int B, int Gmax, int P) {
   MatchWs r;
@@ -618,7 +623,6 @@ MatchWs carve_match(void *w, int B, int Gmax, int P) {
   size_t o = 0;
   r.best = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * kKeyShards * Gmax * 8);
-  r.key_bytes = o;
   r.wcnt = ws_at<int32_t>(w, o);
   o += align_up(static_cast<size_t>(B) * r.nw * 4);
   r.bytes = o;
@@ -673,7 +677,7 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
   MatchWs w = carve_match(workspace, B, Gmax, P);
   // the keys and counts must be zero on entry: every call leaves them so (k_match_final), so
   // only a workspace the caller does not know to be clean is zeroed here (not capturable)
-  if ((flags & SBOD_MATCH_WS_ZEROED) == 0 && hipMemsetAsync(workspace, 0, w.key_bytes, s) != hipSuccess)
+  if ((flags & SBOD_MATCH_WS_ZEROED) == 0 && hipMemsetAsync(workspace, 0, w.bytes, s) != hipSuccess)
     return launch_status("hipMemsetAsync");
   dim3 grid(ntile, B);
   const int fthreads = Gmax <= 64 ? 64 : kFThreads;

@@ -213,3 +213,25 @@ def test_unit_grad_backward():
     assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
     assert torch.equal(grads[2][0], grads[0][0] * 2.0) and torch.equal(grads[2][1], grads[0][1] * 2.0)
     assert float(core.unit_grad(DEV)) == 1.0
+
+
+@pytest.mark.gpu
+def test_workspaces_reused_across_shapes():
+    """The matcher's keys and the fused focal finish's accumulators are zero on entry and left
+    zero by every call, so a cached workspace is used without a memset after its first call
+    (SBOD_MATCH_WS_ZEROED / SBOD_LOSS_WS_ZEROED).  Calls of different shapes on the same stream
+    share those workspaces (different layouts over the same bytes): every call must still match
+    the oracle, whatever ran before it."""
+    seq = [('ssd512', 'SSD512', 8, 'diou', 'focal'), ('ssd300', 'SSD300', 4, 'l1', 'ce'),
+           ('ssd300', 'SSD300', 3, 'diou', 'focal'), ('retina', 'RETINA', 2, 'diou', 'focal'),
+           ('ssd512', 'SSD512', 8, 'diou', 'focal')]
+    for i, (kind, arch, B, reg, cls) in enumerate(seq):
+        P = torch.from_numpy(prior_table(arch))
+        boxes, labels = synth.make_gt(B, seed=40 + i, max_objects=24 if i % 2 else 6)
+        locs, scores = synth.make_preds(B, P.shape[0], 21, seed=40 + i)
+        loss, gl, gs = _run(kind, P, locs, scores, boxes, labels, reg, cls, 21)
+        lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
+        ref = LR.criterion(kind, P, lo, sc, boxes, labels, reg, cls)
+        ref.backward()
+        np.testing.assert_allclose(loss, ref.item(), rtol=RTOL, err_msg='call %d %s' % (i, kind))
+        np.testing.assert_allclose(gs, sc.grad.numpy(), rtol=1e-4, atol=1e-8)
