@@ -72,7 +72,7 @@ def parse(argv=None):
                     help='graph mode: one graph per step (criterion and detect in stream order)')
     ap.add_argument('--priority', choices=('none', 'detect', 'criterion'), default='detect',
                     help='graph mode: which of the two streams gets the high HIP stream priority')
-    ap.add_argument('--order', choices=('criterion_first', 'detect_first'), default='criterion_first',
+    ap.add_argument('--order', choices=('criterion_first', 'detect_first', 'detect_early'), default='criterion_first',
                     help='graph mode: which graph of a step is submitted first')
     ap.add_argument('--det-streams', type=int, default=2,
                     help='graph mode: streams the detect graphs alternate over (1 = one detect stream)')
@@ -276,6 +276,7 @@ class Step:
         self._det_warm = set()
         self.two = two_streams
         self.detect_first = order == 'detect_first'
+        self.detect_early = order == 'detect_early'   # detect graph launched before the GT packing
         self.graph = None
         self.use_graph = graph
         self.capture_error = None
@@ -382,7 +383,11 @@ class Step:
                 pairs = [(ga, self.cap_stream), (gb, ds)]
                 if self.detect_first:
                     pairs.reverse()
-                self.fast.append((core.graph_launches(pairs), h._event.cuda_event, ds.cuda_stream))
+                early = None
+                if self.detect_early:   # the detect graph alone first, then packing + criterion
+                    early = core.graph_launches([(gb, ds)])[0]
+                    pairs = [(ga, self.cap_stream)]
+                self.fast.append((core.graph_launches(pairs), h._event.cuda_event, ds.cuda_stream, early))
             torch.cuda.synchronize()
         self.k = 0
         self.pending = None
@@ -393,7 +398,9 @@ class Step:
         bt = self._next_batch()
         ga, gb, loss, h = self.slots[i]
         if self.fast is not None:
-            launches, ev, ev_stream = self.fast[i]
+            launches, ev, ev_stream, early = self.fast[i]
+            if early is not None:
+                L.call('sbod_graph_launch', early[0], early[1])
             # GT packing on the criterion's stream, whichever graph is submitted first
             if self.stage.stage_and_replay(bt.boxes, bt.labels, launches, ev, ev_stream,
                                            pack_stream=self.cap_stream.cuda_stream) is not None:
