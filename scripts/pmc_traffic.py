@@ -3,7 +3,7 @@
     python scripts/pmc_traffic.py <fetch_dir> <write_dir> [--out profiles/pmc_traffic.json]
 
 Each directory holds a `--pmc FETCH_SIZE` resp. `--pmc WRITE_SIZE` counter-collection CSV of the
-same command (the two counters do not fit one pass on gfx950).  Corrections per
+same command (the two counters do not fit one pass on gfx950), grouped by (kernel, grid size).  Corrections per
 MI355X_MICROARCH.md (HBM section): both counters are in KB; FETCH_SIZE reports half of the
 bytes of wide coalesced reads on gfx950, so it is doubled.  Output: mean bytes per launch."""
 import argparse
@@ -26,7 +26,7 @@ def per_kernel(d, counter):
                 continue
             m = re.search(r'sbod::(k_\w+)', r['Kernel_Name'])
             if m:
-                acc[m.group(1)].append(float(r['Counter_Value']))
+                acc[(m.group(1), int(r.get('Grid_Size') or 0))].append(float(r['Counter_Value']))
     return acc
 
 
@@ -41,12 +41,20 @@ def main():
     out = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of '
                      'bench.py; FETCH_SIZE x2 (gfx950 half-count), KB x1024',
            'kernels': {}}
-    for k in sorted(set(fe) & set(wr)):
-        f = 2.0 * 1024.0 * sum(fe[k]) / len(fe[k])
-        w = 1024.0 * sum(wr[k]) / len(wr[k])
-        out['kernels'][k] = {'launches_fetch': len(fe[k]), 'launches_write': len(wr[k]),
-                             'fetch_bytes_per_launch': round(f), 'write_bytes_per_launch': round(w),
-                             'traffic_bytes_per_launch': round(f + w)}
+    # one entry per (kernel, grid size): a kernel launched at several shapes in the same run (the
+    # bench's B=32 fp32 step, its C2 B=16 bf16 figure, DCN maps) is not averaged across them.
+    # `kernels[k]` is the largest grid's entry (the bench workload), `by_grid[k]` all of them.
+    out['by_grid'] = {}
+    for key in sorted(set(fe) & set(wr)):
+        k, grid = key
+        f = 2.0 * 1024.0 * sum(fe[key]) / len(fe[key])
+        w = 1024.0 * sum(wr[key]) / len(wr[key])
+        e = {'grid_size': grid, 'launches_fetch': len(fe[key]), 'launches_write': len(wr[key]),
+             'fetch_bytes_per_launch': round(f), 'write_bytes_per_launch': round(w),
+             'traffic_bytes_per_launch': round(f + w)}
+        out['by_grid'].setdefault(k, []).append(e)
+        if k not in out['kernels'] or grid > out['kernels'][k]['grid_size']:
+            out['kernels'][k] = e
     s = json.dumps(out, indent=1, sort_keys=True)
     if a.out:
         with open(a.out, 'w') as fh:
