@@ -134,6 +134,7 @@ class GtStaging:
         self._region = region
         self._host = []
         self._host_next = 0
+        self._fixed = None
 
     def _views(self, region):
         nb_b, nb_l, _ = self._nb
@@ -191,11 +192,14 @@ class GtStaging:
         if (ext is None or type(boxes) is not list or type(labels) is not list or not launches
                 or len(boxes) != self.batch or not boxes[0].is_cuda):
             return None
-        dev = self.device.index or 0
-        r = ext.stage_and_replay(boxes, labels, self.boxes.shape[0], self.capacity, dev,
-                                 self.boxes.data_ptr(), self.labels.data_ptr(), self.offsets.data_ptr(),
+        fixed = self._fixed
+        if fixed is None:   # the staging buffers' constants, computed once (per-step host time)
+            dev = self.device.index or 0
+            fixed = self._fixed = (self.boxes.shape[0], self.capacity, dev, self.boxes.data_ptr(),
+                                   self.labels.data_ptr(), self.offsets.data_ptr())
+        r = ext.stage_and_replay(boxes, labels, fixed[0], fixed[1], fixed[2], fixed[3], fixed[4], fixed[5],
                                  pack_stream if pack_stream is not None else launches[0][1], allow_empty,
-                                 launches, event or None, event_stream or None, L._raw_stream(dev) or None)
+                                 launches, event or None, event_stream or None, L._raw_stream(fixed[2]) or None)
         if r is None:
             return None
         if type(r) is int:

@@ -864,8 +864,11 @@ int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logi
   SBOD_LAUNCHED("k_transpose(w)");
   const int mt = (s.M + kFM - 1) / kFM, og = (s.O + 255) / 256;
   const int T = s.N * ((s.C + kFKC - 1) / kFKC);
+  // split-K up to 16 (a sweep of the cap at 32x32 / 16x16 / 8x8, profiles/r3_dcn_split_sweep_s1.jsonl:
+  // 16 is at least as fast as 32 or 64 on every map, 7 % faster at 8x8; fewer slices of the weight
+  // gradient were slower everywhere)
   int split = 1;
-  while (split * 2 <= T && mt * og * split < 512 && split < 64) split *= 2;
+  while (split * 2 <= T && mt * og * split < 512 && split < 16) split *= 2;
   if (split > 1 && hipMemsetAsync(out, 0, static_cast<size_t>(s.M) * s.O * 4, hs) != hipSuccess)
     return launch_status("hipMemsetAsync(dcn out)");
   const dim3 grid(mt, og, split);

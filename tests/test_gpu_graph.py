@@ -245,3 +245,42 @@ def test_graph_span_timing():
     assert all(0.0005 < t < 5.0 for t in times), times
     del g
     L.call('sbod_timing_reset_graphs')
+
+
+def test_bench_pipelined_step_equals_eager():
+    """bench.Step as the bench runs it: per-batch criterion graphs on one stream, detect graphs
+    alternating over two streams, submitted by the one-call C++ path, pipelined two deep, with the
+    criterion's stream current.  Every step's loss, gradients and per-image detections equal the
+    eager two-stream step on the same batch, across two rotations of the resident batches."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    st = bench.Step(DEV, 4, 0, 1, graph=True, two_streams=True, priority='detect', n_batches=4, det_streams=2)
+    ref = []
+    for bt in st.batches:          # eager reference per batch (also warms both detect streams)
+        loss, dets = st.eager_split()
+        ref.append((loss.item(), bt.locs.grad.clone(), bt.scores.grad.clone(),
+                    [[t.clone() for t in part] for part in dets]))
+    for _ in range(2):
+        st.eager_split()
+    torch.cuda.synchronize()
+    st.capture()
+    got = []
+    with torch.cuda.stream(st.cap_stream):
+        for k in range(2 * len(st.batches)):
+            out = st.pipelined()
+            if out is not None:
+                got.append(out)
+        got.append(st.drain())
+    torch.cuda.synchronize()
+    assert len(got) == 2 * len(st.batches)
+    for k, (loss, dets) in enumerate(got):
+        rl, rgl, rgs, rd = ref[k % len(st.batches)]
+        assert loss.item() == rl
+        for part, rpart in zip(dets, rd):
+            assert len(part) == len(rpart) == 4
+            for a, b in zip(part, rpart):
+                assert torch.equal(a, b)
+    for i, bt in enumerate(st.batches):   # the captured backward left the same gradients
+        assert torch.equal(bt.locs.grad, ref[i][1]) and torch.equal(bt.scores.grad, ref[i][2])
