@@ -589,9 +589,11 @@ def main():
     L.timing_enable(None)
     dominant = max(HBM_KERNELS, key=lambda k: kernel_us.get(k, 0.0))
     L.timing_enable(dominant)
-    for _ in range(max(a.timing_steps, 10)):
+    t_win0 = time.monotonic_ns()    # the pass's host window: a kernel trace of this run selects
+    for _ in range(max(a.timing_steps, 10)):   # the same dispatches (scripts/roofline_check.py)
         st.eager_split()
     torch.cuda.synchronize()
+    t_win1 = time.monotonic_ns()
     n_dom, ms_dom = L.timing_query(dominant)
     L.timing_enable(None)
     dom_avg_s = ms_dom / n_dom * 1e-3 if n_dom else float('nan')
@@ -675,6 +677,7 @@ def main():
                    'launch stream, %d eager two-stream steps rotating %d HBM-resident batches'
                    % (max(a.timing_steps, 10), len(st.batches))),
         'algorithmic_bytes_per_launch': algo,
+        'trace_window_ns': [t_win0, t_win1],
     }
     if spans:
         sp = sum(spans) / len(spans)

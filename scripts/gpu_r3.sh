@@ -12,7 +12,9 @@ SBOD_TOL_PROBE=$PWD/gpurun_out/tol_$TAG.jsonl timeout -k 10 400 python -u -m pyt
 timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_$TAG.log 2>&1 && \
 timeout -k 10 300 python -u bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
-    python3 bench.py --no-cpu-baseline "$@" > gpurun_out/prof_$TAG.log 2>&1
+    python3 bench.py --no-cpu-baseline "$@" > gpurun_out/prof_$TAG.log 2>&1 && \
+    python3 scripts/roofline_check.py gpurun_out/bench_$TAG.json gpurun_out/prof_$TAG/run_kernel_trace.csv \
+        gpurun_out/roofline_check_$TAG.json gpurun_out/prof_$TAG.log > /dev/null
 rc=$?
 echo "EXIT $rc"
 exit $rc

@@ -2,7 +2,7 @@
 """Cross-check a bench line's roofline against the rocprofv3 kernel trace of the same command.
 
     python scripts/roofline_check.py gpurun_out/bench_TAG.json gpurun_out/prof_TAG/run_kernel_trace.csv \
-        [profiles/r3_roofline_check_TAG.json]
+        [profiles/r3_roofline_check_TAG.json] [gpurun_out/prof_TAG.log]
 
 For every HBM-bound kernel of the bench's ALGO_BYTES table, the dispatches of the bench
 workload (grid = B x ceil(P/256) workgroups of 256 threads, so the C2 bf16 step and other
@@ -10,6 +10,12 @@ shapes in the same run are excluded) are averaged from the trace (End - Start, n
 dispatch-level time rocprofv3 reports).  Written: per kernel, the rocprof average, the bench's
 event-timed average (kernel_us_per_step), algorithmic bytes per launch, the HBM fraction from
 each, and their relative difference; plus the headline kernel's line frac vs the rocprof frac.
+
+With the profiled run's own bench line (its stdout, 4th argument), the headline kernel's
+dispatches are also taken from the window of the line's dominant-kernel timing pass only
+(`roofline.trace_window_ns`, host CLOCK_MONOTONIC, the clock of rocprofv3's timestamps): the
+same eager launches the line's `avg_us` averages, without the warm-up, capture and graph
+phases the whole-trace average mixes in.
 """
 import csv
 import json
@@ -20,7 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 
-def main(bench_json, trace_csv, out=None):
+def main(bench_json, trace_csv, out=None, prof_log=None):
     import bench as BM
     line = json.loads(open(bench_json).read().strip().splitlines()[-1])
     cfg = line['config']
@@ -34,6 +40,11 @@ def main(bench_json, trace_csv, out=None):
         algo['k_det_prepare'] = line['step_algorithmic_bytes'] - BM.criterion_bytes(B, P, C)
     grid_x = 256 * ((P + 255) // 256)
     durs = {k: [] for k in algo}
+    win, wdurs = None, []
+    if prof_log:
+        for ln in open(prof_log):
+            if ln.startswith('{') and '"roofline"' in ln:
+                win = json.loads(ln)['roofline'].get('trace_window_ns')
     with open(trace_csv) as f:
         for r in csv.DictReader(f):
             name = r['Kernel_Name']
@@ -42,7 +53,10 @@ def main(bench_json, trace_csv, out=None):
                     if 'unsigned short' in name:      # the bf16 (C2) instantiation
                         continue
                     if int(r['Grid_Size_X']) == grid_x and int(r['Grid_Size_Y']) == B:
-                        durs[k].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+                        t0, t1 = int(r['Start_Timestamp']), int(r['End_Timestamp'])
+                        durs[k].append(t1 - t0)
+                        if k == rl['kernel'] and win and win[0] <= t0 and t1 <= win[1]:
+                            wdurs.append(t1 - t0)
     res = {'bench': os.path.basename(bench_json), 'trace': os.path.basename(trace_csv),
            'workload': {'B': B, 'P': P, 'C': C}, 'peak_GBps': BM.HBM_PEAK_GBS, 'kernels': {}}
     for k, d in durs.items():
@@ -62,6 +76,15 @@ def main(bench_json, trace_csv, out=None):
         res['headline'] = {'kernel': hk, 'line_frac': rl['frac'], 'line_avg_us': rl['avg_us'],
                            'rocprof_frac': fr, 'rel_diff': round(rl['frac'] / fr - 1.0, 4),
                            'within_5pct': abs(rl['frac'] / fr - 1.0) <= 0.05}
+        if wdurs:
+            us = sum(wdurs) / len(wdurs) / 1e3
+            fw = round(algo[hk] / (us * 1e-6) / 1e9 / BM.HBM_PEAK_GBS, 4)
+            res['headline'].update({
+                'window_dispatches': len(wdurs), 'window_rocprof_avg_us': round(us, 3),
+                'window_rocprof_frac': fw, 'window_rel_diff': round(rl['frac'] / fw - 1.0, 4),
+                'window_within_5pct': abs(rl['frac'] / fw - 1.0) <= 0.05})
+        elif win:
+            res['headline']['window_dispatches'] = 0   # clocks did not line up: whole-trace only
     txt = json.dumps(res, indent=1)
     print(txt)
     if out:
@@ -70,4 +93,4 @@ def main(bench_json, trace_csv, out=None):
 
 
 if __name__ == '__main__':
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
