@@ -169,3 +169,25 @@ def test_codecs_golden():
                                rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(core.codec('encode_var', bx, p).cpu().numpy(), d['encode'], rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(core.codec('decode_var', lc, p).cpu().numpy(), d['decode'], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('counts', [(64, 1, 64), (1, 63, 64, 65, 127, 128, 129), (65, 2)])
+def test_match_object_count_boundaries(counts):
+    """Object counts at the 64-object chunk of k_match_tile and the register / LDS switch of
+    k_match_final (Gmax <= 64 vs > 64), in one batch; an object repeated across a chunk boundary
+    (objects 10 and 70 identical) so the forced match's last writer sits in another chunk."""
+    P = prior_table('SSD512')
+    pxy_np = M.cxcy_to_xy(P)
+    pxy = torch.from_numpy(pxy_np).to(DEV)
+    rng = np.random.default_rng(sum(counts))
+    boxes, labels = [], []
+    for g in counts:
+        xy = rng.uniform(0, 0.7, (g, 2)).astype(np.float32)
+        wh = rng.uniform(0.02, 0.3, (g, 2)).astype(np.float32)
+        bx = np.concatenate([xy, np.minimum(xy + wh, 1.0)], 1).astype(np.float32)
+        if g > 70:
+            bx[70] = bx[10]
+        boxes.append(bx)
+        labels.append(rng.integers(1, 21, g).astype(np.int64))
+    obj, ovl, npos = core.match(_gt(boxes, labels), pxy, P.shape[0])
+    _check_oracle(boxes, labels, obj, ovl, npos, pxy_np)
