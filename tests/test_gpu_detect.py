@@ -173,3 +173,27 @@ def test_detect_beyond_largest_window_near_duplicates():
         np.testing.assert_array_equal(ol[b].cpu().numpy(), rl[b])
         np.testing.assert_array_equal(os_[b].cpu().numpy(), rs[b])
         np.testing.assert_array_equal(ob[b].cpu().numpy(), rb[b])
+
+
+@pytest.mark.parametrize('final', [None, 0.7])
+def test_detect_empty_image_and_single_class(final):
+    """An image without a single candidate (the reference's placeholder row: box [0, 0, 1, 1],
+    label 0, score 0, models/utils.py:274-280), one whose candidates are all in one class (19
+    empty segments), and an ordinary one, in one batch; shared activations as above."""
+    Pn = prior_table('SSD512')
+    P = torch.from_numpy(Pn).to(DEV)
+    locs, scores = synth.make_preds(3, Pn.shape[0], 21, seed=11, bg_shift=6.0)
+    scores[1, :, 0] += 40.0
+    keep5 = scores[2, :, 5].clone()
+    scores[2, :, 1:] = -50.0
+    scores[2, :, 5] = keep5
+    (ob, ol, os_), probs, boxes = core.detect(locs.to(DEV), scores.to(DEV), 0.01, 0.45, 200, P,
+                                              final_nms=final, debug=True)
+    rb, rl, rs = M.detect(probs.cpu().numpy(), boxes.cpu().numpy(), 0.01, 0.45, 200, final_nms=final,
+                          nms_variant='tv')
+    assert rl[1].tolist() == [0] and rs[1].tolist() == [0.0]
+    assert set(rl[2].tolist()) == {5}
+    for b in range(3):
+        np.testing.assert_array_equal(ol[b].cpu().numpy(), rl[b])
+        np.testing.assert_array_equal(os_[b].cpu().numpy(), rs[b])
+        np.testing.assert_array_equal(ob[b].cpu().numpy(), rb[b])
