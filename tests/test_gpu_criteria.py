@@ -86,6 +86,24 @@ def test_criteria_vs_oracle_full(kind, arch, B, reg, cls):
     np.testing.assert_allclose(gs, sc.grad.numpy(), rtol=1e-4, atol=1e-8)
 
 
+@pytest.mark.parametrize('reg,cls', [('diou', 'focal'), ('smoothl1', 'ce')])
+def test_criteria_many_objects_vs_oracle(reg, cls):
+    """Up to 150 objects per image: the matcher's LDS finish form (Gmax > 64) and several
+    64-object chunks per tile under the fused loss (focal: finished inside k_multibox)."""
+    P = torch.from_numpy(prior_table('SSD512'))
+    C, B = 21, 4
+    boxes, labels = synth.make_gt(B, seed=9, max_objects=150)
+    assert max(b.shape[0] for b in boxes) > 64
+    locs, scores = synth.make_preds(B, P.shape[0], C, seed=9)
+    loss, gl, gs = _run('ssd512', P, locs, scores, boxes, labels, reg, cls, C)
+    lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
+    ref = LR.criterion('ssd512', P, lo, sc, boxes, labels, reg, cls)
+    ref.backward()
+    np.testing.assert_allclose(loss, ref.item(), rtol=RTOL)
+    np.testing.assert_allclose(gl, lo.grad.numpy(), rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(gs, sc.grad.numpy(), rtol=1e-4, atol=1e-8)
+
+
 def test_refinedet_golden():
     d = load_golden('crit_refinedet.npz')
     P = torch.from_numpy(prior_table('REFINEDET')[::int(d['prior_stride'])].copy()).to(DEV)
