@@ -1640,6 +1640,13 @@ __device__ __forceinline__ int merge_rank(
   __syncthreads();
   SEG_PHASE(3);
   const int m = r_m;
+  // the box of this thread's first entry, loaded now (unconditional, clamped: m >= top_k >= 1)
+  // so its latency runs under the rank counting; emitted below if the entry's rank < top_k
+  const int e0 = min(tid, m - 1);
+  const uint32_t low0 = 0xffffffffu - static_cast<uint32_t>(sk[e0]);
+  const Box4 box0 = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P +
+                                        key_low(sl[(static_cast<int>(low0 >> 24) - 1) * wmax +
+                                                   static_cast<int>(low0 & 0xffffffu)])));
   const int nsplit = max(1, min(16, NT / m)), per = (m + nsplit - 1) / nsplit;
   for (int t = tid; t < m * nsplit; t += NT) {
     const int e = t % m, part = t / m;
@@ -1669,7 +1676,14 @@ __device__ __forceinline__ int merge_rank(
       const unsigned long long k = sk[e];
       const uint32_t low = 0xffffffffu - static_cast<uint32_t>(k);
       const int c = static_cast<int>(low >> 24), pos = static_cast<int>(low & 0xffffffu);
-      emit(static_cast<int>(rank), c, sl[(c - 1) * wmax + pos]);
+      const unsigned long long key = sl[(c - 1) * wmax + pos];
+      if (e == tid) {   // the prefetched box
+        st4(ob + 4 * rank, box0);
+        ol[rank] = c;
+        os[rank] = key_score(key);
+      } else {
+        emit(static_cast<int>(rank), c, key);
+      }
       if (rank == static_cast<uint32_t>(top_k - 1)) r_kth = static_cast<uint32_t>(k >> 32);
     }
   }
