@@ -118,6 +118,8 @@ int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int 
  *            [B,P,4] (gcxgcy) decoded on the fly against priors_cxcy, exactly
  *            cxcy_to_xy(gcxgcy_to_cxcy(arm_locs[i], priors_cxcy)) (RefineDet512.py:850).
  *   arm_scores: [B,P,2] logits, only for SBOD_MATCH_ODM (easy negatives softmax[...,1] < theta).
+ *   gt_boxes / gt_labels must hold at least one row even when every image is empty (the
+ *   matcher's prologue reads row 0 unconditionally; sbod_gt_pack's callers size them max(n, 1)).
  *   Outputs [B,P]: obj (object per prior, int32), ovl (overlap per prior after the forced match).
  *   n_pos [B+1] int32: positives per image (+ the batch total at n_pos[B]).  Labels and the
  *   negative mask are derived from (obj, ovl, gt_labels) by the loss kernels.
@@ -206,11 +208,17 @@ size_t sbod_loss_workspace_bytes(int B, int P);
  * (the sum over ranks is the single-device loss).  Same workspace as the deferred call. */
 enum { SBOD_LOSS_DEFER_MINING = 64 };
 /* Focal criteria (no mining pass) finish the loss inside the fused pass: its workgroups fold
- * their partial sums into fixed-point accumulators in the workspace's first 4224 bytes, which must
- * be zero on entry and are left zero by every successful call (any B, P).  A caller that knows the workspace is clean (a
- * previous successful call on it) passes SBOD_LOSS_WS_ZEROED and the call issues no memset
- * (hipGraph capture); without it the call zeroes them first (hipMemsetAsync, 4224 bytes). */
-enum { SBOD_LOSS_WS_ZEROED = 128 };
+ * their partial sums into exact 128-bit fixed-point accumulators (2^-64 resolution; a partial
+ * that is non-finite or >= 2^40 in magnitude switches the finish to a double sum of the fp32
+ * partials, as the separate finaliser computes it) in the workspace's first
+ * sbod_loss_zero_prefix_bytes() bytes, which must be zero on entry and are left zero by every
+ * successful call (any B, P).  A caller that knows the workspace is clean (a previous successful
+ * call on it) passes SBOD_LOSS_WS_ZEROED and the call issues no memset (hipGraph capture);
+ * without it the call zeroes them first (one hipMemsetAsync).  SBOD_LOSS_UNFUSED_FINISH
+ * (diagnostics, tests) finishes a focal criterion with the separate finaliser launch instead
+ * (per-workgroup partials summed in double). */
+enum { SBOD_LOSS_WS_ZEROED = 128, SBOD_LOSS_UNFUSED_FINISH = 512 };
+size_t sbod_loss_zero_prefix_bytes(void);
 size_t sbod_loss_pool_offset(int B, int P);
 int sbod_multibox_mine_global(const void *scores, int dtype, int B, int P, int C,
                               const int32_t *npos_total, int reg, int cls, int flags,

@@ -1,0 +1,20 @@
+#!/bin/bash
+# GPU box, round 4: the -m gpu suite, smoke(), the bench line and a rocprofv3 kernel-stats run of
+# the same bench command.  Every GPU step has its own time limit; the chain stops at the first
+# failure.   Usage: bash scripts/gpu_r3.sh TAG [bench args...]
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-run}; shift
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    > gpurun_out/tests_$TAG.log 2>&1 && \
+timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_$TAG.log 2>&1 && \
+timeout -k 10 300 python -u bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
+    python3 bench.py --no-cpu-baseline "$@" > gpurun_out/prof_$TAG.log 2>&1 && \
+    python3 scripts/roofline_check.py gpurun_out/bench_$TAG.json gpurun_out/prof_$TAG/run_kernel_trace.csv \
+        gpurun_out/roofline_check_$TAG.json gpurun_out/prof_$TAG.log > /dev/null
+rc=$?
+echo "EXIT $rc"
+exit $rc

@@ -37,6 +37,7 @@ SIGNATURES = {
     'sbod_multibox_loss': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, P, F32, F32,
                                  F32, I32, I32, I32, I32, F32, F32, F32, P, P, P, P, SZ, P]),
     'sbod_loss_pool_offset': (SZ, [I32, I32]),
+    'sbod_loss_zero_prefix_bytes': (SZ, []),
     'sbod_multibox_mine_global': (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, F32, P, I64, I64, P,
                                         P, P, SZ, P]),
     'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),
@@ -80,6 +81,7 @@ DT_F32, DT_BF16 = 0, 1
 LOSS_FOCAL_NORM = 4
 LOSS_DEFER_MINING = 64
 LOSS_WS_ZEROED = 128
+LOSS_UNFUSED_FINISH = 512
 POOL = dict(nonpos=0, neg=8, global_neg=16, nonpos_not_easy=32)
 OV = dict(iou=0, giou=1, diou=2, ciou=3)
 FOCAL = dict(softmax=0, sigmoid=1, bce=2)

@@ -226,28 +226,38 @@ def graph_launches(pairs):
 
 
 _WS = {}
+_WS_CAPTURED = set()   # data_ptr of workspaces handed out under hipGraph capture
+_WS_RETIRED = []       # grown-out-of workspaces a captured graph may still address (kept alive)
 
 
 def workspace(nbytes, device, slot='default'):
     """Device scratch, cached per (device, current stream, slot) and grown on demand.  Reuse is
-    safe because every user of a slot runs in stream order on that stream."""
+    safe because every user of a slot runs in stream order on that stream.  A buffer handed out
+    under hipGraph capture is never returned to the allocator when the slot grows later (the
+    graph keeps its address and writes it on every replay): it is retired and kept alive."""
     dev = device if isinstance(device, torch.device) else torch.device(device)
     key = (dev, L._raw_stream(dev.index if dev.index is not None else torch.cuda.current_device())
            if dev.type == 'cuda' else 0, slot)
     buf = _WS.get(key)
     n = max(int(nbytes), 1)
+    capturing = dev.type == 'cuda' and torch.cuda.is_current_stream_capturing()
     if buf is None or buf.numel() < n:
-        if dev.type == 'cuda' and torch.cuda.is_current_stream_capturing():
+        if capturing:
             # a workspace first allocated under hipGraph capture has faulted replays on this
             # runtime: the caller warms up on the capture stream so it exists beforehand
             raise L.SbodError('sbod workspace %r (%d bytes) would be allocated under hipGraph capture: '
                               'run the same calls once on the capture stream before capturing'
                               % (slot, n))
         if buf is not None:
-            _CLEAN.pop(buf.data_ptr(), None)   # its memory returns to the allocator
+            _CLEAN.pop(buf.data_ptr(), None)
+            if buf.data_ptr() in _WS_CAPTURED:
+                _WS_RETIRED.append(buf)        # a captured graph still writes it on replay
+            # else its memory returns to the allocator
         buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8, device=dev)
         _CLEAN.pop(buf.data_ptr(), None)
         _WS[key] = buf
+    if capturing:
+        _WS_CAPTURED.add(buf.data_ptr())
     return buf
 
 
@@ -410,7 +420,8 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
         ws = workspace(nb, dev, 'loss')
         flags = spec.flags | (L.LOSS_DEFER_MINING if exchange is not None else 0)
         # the fused finish's accumulators are left zero by every successful call
-        zflag = _zeroed_flag(ws, _LOSS_ZERO_PREFIX, L.LOSS_WS_ZEROED, 'criterion')
+        zprefix = _loss_zero_prefix()
+        zflag = _zeroed_flag(ws, zprefix, L.LOSS_WS_ZEROED, 'criterion')
         _CLEAN.pop(ws.data_ptr(), None)
         L.call('sbod_multibox_loss', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy),
                L.ptr(arm_locs), L.ptr(arm_scores), L.ptr(gt.boxes), L.ptr(gt.labels),
@@ -418,7 +429,7 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
                float(threshold), float(neg_threshold), float(theta), spec.reg, spec.cls, flags | zflag,
                int(spec.neg_pos_ratio), float(spec.reg_weight), float(spec.alpha), float(spec.gamma),
                L.ptr(gl), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
-        _CLEAN[ws.data_ptr()] = _LOSS_ZERO_PREFIX   # (only the accumulator prefix is zero)
+        _CLEAN[ws.data_ptr()] = zprefix   # (only the accumulator prefix is zero)
         if exchange is not None:
             off = L.lib().sbod_loss_pool_offset(B, P)
             pool = ws.narrow(0, off, 4 * B * P).view(torch.float32)
@@ -580,7 +591,13 @@ def _count_slot(dev, B):
 # leaves its candidate counters zero, so after the first call on a workspace no memset is
 # needed — none in a captured graph (SBOD_DETECT_COUNTERS_ZEROED).
 _CLEAN = {}
-_LOSS_ZERO_PREFIX = 4224   # sbod_multibox_loss: the fused finish's accumulators (include/sbod.h)
+_LOSS_ZERO_PREFIX = []     # sbod_loss_zero_prefix_bytes(): the fused finish's accumulators (queried once)
+
+
+def _loss_zero_prefix():
+    if not _LOSS_ZERO_PREFIX:
+        _LOSS_ZERO_PREFIX.append(int(L.lib().sbod_loss_zero_prefix_bytes()))
+    return _LOSS_ZERO_PREFIX[0]
 
 
 def _zeroed_flag(ws, need, flag, what):
@@ -827,9 +844,13 @@ class _DeformConv(torch.autograd.Function):
         if tuple(weight.shape) != (O, C, ks, ks):
             raise ValueError('DeformConv2d: weight shape %s' % (tuple(weight.shape),))
         out = torch.empty(B, O, Ho, Wo, dtype=torch.float32, device=x.device)
-        # forward-only size (no dcols rows): an eval forward does not pay the backward's buffers;
-        # the backward grows the same cached workspace when it runs
-        nb = L.lib().sbod_dcn_fwd_workspace_bytes(B, C, H, W, O, ks, stride, padding)
+        # an inference forward takes the forward-only size (no dcols rows); a training forward
+        # takes the backward's full size up front, so the backward never grows (reallocates) the
+        # cached workspace that this forward — possibly captured in a graph — addresses
+        if any(ctx.needs_input_grad[:4]):
+            nb = L.lib().sbod_dcn_workspace_bytes(B, C, H, W, O, ks, stride, padding)
+        else:
+            nb = L.lib().sbod_dcn_fwd_workspace_bytes(B, C, H, W, O, ks, stride, padding)
         ws = workspace(nb, x.device, 'dcn')
         L.call('sbod_dcn_fwd_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight),
                B, C, H, W, O, ks, stride, padding, L.ptr(out), L.ptr(ws), nb, L.stream_of(x))

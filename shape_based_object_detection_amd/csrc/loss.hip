@@ -14,8 +14,6 @@
 // Roofline: HBM-bound; algorithmic bytes per launch = B*P*(4+C)*s read + B*P*(4+C)*s written.
 #include <hip/hip_bf16.h>
 
-#include <cstdlib>
-
 #include "sbod_common.h"
 
 namespace sbod {
@@ -322,26 +320,48 @@ struct LossArgs {
 };
 
 // The fused finish of k_multibox (focal / no mining).  Each workgroup folds its partial sums
-// into two 64-bit fixed-point accumulators (value * 2^32, rounded; integer adds are exact and
-// order-free, so the result is bitwise reproducible) with agent-scope atomics executed at the
-// memory side, waits for them, then counts itself in; the workgroup whose count comes last reads
-// the sums back with exchanges (which also leave them zero for the next call) and writes the
-// loss vector exactly as k_loss_final would.  Non-finite partials (NaN rows of the focal loss)
-// travel as flag bits: NaN, +inf, -inf per component.  No data moves through plain stores, so no
-// cache write-back or invalidation is needed between the XCDs.
-constexpr float kFinScale = 4294967296.f;   // 2^32
-__device__ __forceinline__ unsigned nonfinite_bits(float v) {
-  if (v != v) return 1u;
-  if (v == __builtin_inff()) return 2u;
-  if (v == -__builtin_inff()) return 4u;
-  return 0u;
+// into exact 128-bit fixed-point accumulators (two's complement, 64 fraction bits: value * 2^64
+// as {lo, hi} u64 words) with agent-scope atomics executed at the memory side: the lo add
+// returns the word's previous value, so the adder knows its own carry out of bit 63 and adds it
+// to hi with the high part.  Integer adds are exact and order-free, so the sum is bitwise
+// reproducible, with a resolution of 2^-64 per partial (a loss total of 1e-12 keeps 1e-7
+// relative) and a range of 2^63.  A partial of magnitude >= 2^40 (or a non-finite one) cannot be
+// folded exactly: it travels as a flag bit, and the finishing workgroup then sums every
+// workgroup's fp32 partial in double instead (each workgroup also writes its two partials
+// through with sc1 stores before it counts itself in), as k_loss_final would — the finish is
+// never silently wrong.  Non-finite partials (NaN rows of the focal loss) keep their own flag
+// bits (NaN, +inf, -inf per component).  The adds are drained (s_waitcnt with a compiler memory
+// clobber) before the arrival add, and every hand-off moves through memory-side atomics or sc1
+// stores/loads, so no cache write-back or invalidation is needed between the XCDs.
+constexpr float kFinLimit = 1099511627776.f;   // 2^40: larger partials take the double fallback
+struct Fx128 {
+  unsigned long long lo, hi;
+};
+// v * 2^64 rounded to an integer (|v| < 2^40, finite), as a 128-bit two's complement pair.
+__device__ __forceinline__ Fx128 to_fx128(float v) {
+  const uint32_t bits = __float_as_uint(v) & 0x7fffffffu;
+  const uint32_t E = bits >> 23;
+  const unsigned long long m = E ? ((bits & 0x7fffffu) | 0x800000u) : (bits & 0x7fffffu);
+  const int sh = (E ? static_cast<int>(E) - 150 : -149) + 64;   // |v| * 2^64 = m * 2^sh
+  unsigned long long lo = 0, hi = 0;
+  if (sh >= 64) {
+    hi = m << (sh - 64);
+  } else if (sh >= 0) {
+    lo = m << sh;
+    hi = sh > 40 ? (m >> (64 - sh)) : 0ull;
+  } else if (sh > -25) {
+    lo = (m + (1ull << (-sh - 1))) >> (-sh);   // round half up
+  }
+  if (__float_as_uint(v) >> 31) {   // negate the pair
+    lo = ~lo + 1ull;
+    hi = ~hi + (lo == 0ull ? 1ull : 0ull);
+  }
+  return Fx128{lo, hi};
 }
-__device__ __forceinline__ double fin_value(unsigned long long fx, unsigned bits) {
-  if ((bits & 1u) || ((bits & 6u) == 6u)) return __builtin_nan("");
-  if (bits & 2u) return __builtin_inf();
-  if (bits & 4u) return -__builtin_inf();
-  return static_cast<double>(static_cast<long long>(fx)) / 4294967296.0;
+__device__ __forceinline__ double fx128_value(unsigned long long lo, unsigned long long hi) {
+  return static_cast<double>(static_cast<long long>(hi)) + static_cast<double>(lo) * 5.421010862427522170e-20;
 }
+__device__ __forceinline__ bool fx_foldable(float v) { return fabsf(v) < kFinLimit; }   // false for NaN / inf
 __device__ __forceinline__ void loss_outputs(double c, double l, float n, int reg, int cls, int flags,
                                              float reg_weight, float *out) {
   const float conf = (cls == SBOD_CLS_CE || (flags & SBOD_LOSS_FOCAL_NORM)) ? static_cast<float>(c) / n
@@ -355,45 +375,90 @@ __device__ __forceinline__ void loss_outputs(double c, double l, float n, int re
 constexpr int kFinGroups = 32;   // workgroup groups (linear id mod 32), then one global level
 constexpr int kFinStride = 16;   // u64 words per accumulator set: one 128-byte line each
 constexpr size_t kFinBytes = sizeof(unsigned long long) * kFinStride * (kFinGroups + 1);   // 4224
+// Accumulator set (one 128-byte line): conf {lo, hi}, loc {lo, hi}, fallback flag, arrivals.
+enum { kFinConf = 0, kFinLoc = 2, kFinFlag = 4, kFinArrive = 5 };
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// w[0..1] += v (128-bit): the lo add returns the previous word, which gives this add's carry.
+__device__ __forceinline__ void fx_add(unsigned long long *w, Fx128 v) {
+  unsigned long long carry = 0;
+  if (v.lo) {
+    const unsigned long long old = __hip_atomic_fetch_add(w, v.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    carry = old + v.lo < old ? 1ull : 0ull;
+  }
+  if (v.hi + carry) __hip_atomic_fetch_add(w + 1, v.hi + carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long xchg0(unsigned long long *w) {
+  return __hip_atomic_exchange(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Called by wave 0 of every workgroup (all 64 lanes; conf_l / loc_l uniform).  The partials
+// array holds each workgroup's fp32 {conf, loc} for the double fallback.
 __device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, unsigned nblk, float *out) {
-  // accumulators: kFinGroups group lines, then the top line; each {conf, loc, flags, arrivals}.
-  // Two levels because atomics on one word serialise at the memory side (~10 ns each): ~41
-  // arrivals per group word and 32 on the top word instead of every workgroup on one word.
+  // accumulators: kFinGroups group lines, then the top line.  Two levels because atomics on one
+  // word serialise at the memory side (~10 ns each): ~41 arrivals per group word and 32 on the
+  // top word instead of every workgroup on one word.
+  const int lane = threadIdx.x & 63;
   const unsigned blk = blockIdx.x + gridDim.x * blockIdx.y;
   const unsigned ng = nblk < kFinGroups ? nblk : kFinGroups, g = blk % ng;
   const unsigned in_group = (nblk - g + ng - 1) / ng;
   unsigned long long *acc = a.fin + kFinStride * g, *top = a.fin + kFinStride * kFinGroups;
-  const unsigned long long bits = nonfinite_bits(conf_l) | (nonfinite_bits(loc_l) << 3);
-  unsigned long long cf = 0, lf = 0;
-  if (!bits) {
-    cf = static_cast<unsigned long long>(__float2ll_rn(conf_l * kFinScale));
-    lf = static_cast<unsigned long long>(__float2ll_rn(loc_l * kFinScale));
+  int last = 0;
+  if (lane == 0) {
+    const bool ok = fx_foldable(conf_l) && fx_foldable(loc_l);
+    st_wt_u32(reinterpret_cast<int32_t *>(a.partials) + 2 * blk, __float_as_uint(conf_l));
+    st_wt_u32(reinterpret_cast<int32_t *>(a.partials) + 2 * blk + 1, __float_as_uint(loc_l));
+    if (ok) {
+      fx_add(acc + kFinConf, to_fx128(conf_l));
+      fx_add(acc + kFinLoc, to_fx128(loc_l));
+    } else {
+      __hip_atomic_fetch_or(acc + kFinFlag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    drain_vm();   // the adds (and the partials' write-through) are performed before the count
+    last = __hip_atomic_fetch_add(acc + kFinArrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1;
   }
-  auto fold = [&](unsigned long long *w, unsigned long long c, unsigned long long l, unsigned long long f,
-                  unsigned count) {   // true: this caller's count came last on w
-    if (f) __hip_atomic_fetch_or(w + 2, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c) __hip_atomic_fetch_add(w, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (l) __hip_atomic_fetch_add(w + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);   // the adds are performed before the count
-    return __hip_atomic_fetch_add(w + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
-  };
-  auto drain = [&](unsigned long long *w, unsigned long long &c, unsigned long long &l, unsigned long long &f) {
-    c = __hip_atomic_exchange(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    l = __hip_atomic_exchange(w + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    f = __hip_atomic_exchange(w + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_exchange(w + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  if (!fold(acc, cf, lf, bits, in_group)) return;
+  if (!__builtin_amdgcn_readfirstlane(last)) return;
   // this group is complete (every member's adds were performed before it counted itself in):
-  // its totals move to the top line (four exchanges in flight, leaving the group line zero),
+  // its totals move to the top line (exchanges in flight together, leaving the group line zero),
   // and the workgroup that completes the top line drains it.  (Draining all 32 group lines from
   // the last workgroup instead serialised one lane's exchanges: +9 µs.)
-  unsigned long long c, l, f;
-  drain(acc, c, l, f);
-  if (!fold(top, c, l, f, ng)) return;
-  drain(top, c, l, f);
-  loss_outputs(fin_value(c, static_cast<unsigned>(f) & 7u), fin_value(l, static_cast<unsigned>(f >> 3) & 7u),
-               static_cast<float>(*a.npos_total), a.reg, a.cls, a.flags, a.reg_weight, out);
+  if (lane == 0) {
+    const Fx128 c{xchg0(acc + kFinConf), xchg0(acc + kFinConf + 1)};
+    const Fx128 l{xchg0(acc + kFinLoc), xchg0(acc + kFinLoc + 1)};
+    const unsigned long long f = xchg0(acc + kFinFlag);
+    xchg0(acc + kFinArrive);
+    fx_add(top + kFinConf, c);
+    fx_add(top + kFinLoc, l);
+    if (f) __hip_atomic_fetch_or(top + kFinFlag, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    drain_vm();
+    last = __hip_atomic_fetch_add(top + kFinArrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+  }
+  if (!__builtin_amdgcn_readfirstlane(last)) return;
+  double c = 0.0, l = 0.0;
+  int fallback = 0;
+  if (lane == 0) {
+    const unsigned long long clo = xchg0(top + kFinConf), chi = xchg0(top + kFinConf + 1);
+    const unsigned long long llo = xchg0(top + kFinLoc), lhi = xchg0(top + kFinLoc + 1);
+    fallback = xchg0(top + kFinFlag) != 0ull;
+    xchg0(top + kFinArrive);
+    c = fx128_value(clo, chi);
+    l = fx128_value(llo, lhi);
+  }
+  if (__builtin_amdgcn_readfirstlane(fallback)) {
+    // a non-finite or huge partial: the double sum of every workgroup's fp32 partials, as
+    // k_loss_final computes it (the partials were written through before their arrivals)
+    c = 0.0;
+    l = 0.0;
+    const int32_t *pp = reinterpret_cast<const int32_t *>(a.partials);
+    for (unsigned i = lane; i < nblk; i += 64) {
+      c += static_cast<double>(__uint_as_float(ld_wt_u32(pp + 2 * i)));
+      l += static_cast<double>(__uint_as_float(ld_wt_u32(pp + 2 * i + 1)));
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      c += __shfl_xor(c, m, 64);
+      l += __shfl_xor(l, m, 64);
+    }
+  }
+  if (lane == 0) loss_outputs(c, l, static_cast<float>(*a.npos_total), a.reg, a.cls, a.flags, a.reg_weight, out);
 }
 
 // exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'
@@ -718,14 +783,12 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     printf("multibox x%d b%d: load %lld compute %lld store+sum %lld total %lld\n", blockIdx.x, b,
            ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
 #endif
-  if (tid == 0) {
-    if (a.fin != nullptr) {
-      multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, a.out);
-    } else {
-      const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
-      a.partials[2 * blk] = conf_l;
-      a.partials[2 * blk + 1] = loc_l;
-    }
+  if (a.fin != nullptr) {
+    if (tid < 64) multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, a.out);
+  } else if (tid == 0) {
+    const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
+    a.partials[2 * blk] = conf_l;
+    a.partials[2 * blk + 1] = loc_l;
   }
   span_end(a.span);
   STAMP_END(4, 1);
@@ -1083,8 +1146,7 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   // step has no k_loss_final launch; its accumulators are zero on entry (SBOD_LOSS_WS_ZEROED)
   // (every call without the flag zeroes them, fused or not: a caller marks the workspace clean
   // after ANY successful call, and a mining-path call never touches them)
-  const bool fused = cls == SBOD_CLS_FOCAL && !(flags & SBOD_LOSS_DEFER_MINING) &&
-                     std::getenv("SBOD_NO_FUSED_FINISH") == nullptr;   // (A/B and diagnosis)
+  const bool fused = cls == SBOD_CLS_FOCAL && !(flags & (SBOD_LOSS_DEFER_MINING | SBOD_LOSS_UNFUSED_FINISH));
   if ((flags & SBOD_LOSS_WS_ZEROED) == 0 &&
       hipMemsetAsync(ws.fin, 0, kFinBytes, s) != hipSuccess)
     return launch_status("hipMemsetAsync(loss)");
@@ -1129,6 +1191,8 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   return mine_and_finish(scores, dtype, B, P, C, n_pos, npos_total, reg, cls, flags, neg_pos_ratio,
                          reg_weight, ws.pool, static_cast<int64_t>(B) * P, 0, grad_scores, loss_out, ws, s);
 }
+
+size_t sbod_loss_zero_prefix_bytes(void) { return kFinBytes; }
 
 size_t sbod_loss_pool_offset(int B, int P) {
   return carve(nullptr, B, P).pool_off;

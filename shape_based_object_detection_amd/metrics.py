@@ -7,13 +7,17 @@ the HIP kernel; CPU tensors (DataLoader workers: random_crop, dataset/transforms
 the host path in ``host.py``.
 ``calculate_mAP`` (metrics.py:8-145): VOC 11-point mAP on the device —
 sorts, per-(class, image) greedy TP/FP assignment and per-class AP kernels (csrc/map.hip),
-one host sync for the returned Python values, like the reference's ``.item()``/``.tolist()``.
+one host sync for the returned Python values, like the reference's ``.item()``/``.tolist()``;
+CPU tensors take the host path (``hostpath.calculate_mAP``).
+``accuracy`` / ``AverageMeter`` (metrics.py:255-289): the bookkeeping train_anchor.py:21 and
+eval.py:23 import from this module, host-side as in the reference.
 """
 import torch
 
 from . import _lib as L
 from . import core
 from . import host
+from . import hostpath
 
 _RTHR = {}
 _ONE_IMAGE_OFFSETS = {}
@@ -83,6 +87,12 @@ def calculate_mAP(det_boxes, det_labels, det_scores, true_boxes, true_labels, tr
         true_labels) == len(true_difficulties)
     n_classes = len(label_map)
     B = len(det_boxes)
+    rev_label_map = {v: k for k, v in label_map.items()}
+    if all(not t.is_cuda for g in (det_boxes, det_labels, det_scores, true_boxes, true_labels,
+                                   true_difficulties) for t in g):
+        aps, mean_ap = hostpath.calculate_mAP(det_boxes, det_labels, det_scores, true_boxes, true_labels,
+                                              true_difficulties, threshold, n_classes)
+        return {rev_label_map[c + 1]: v for c, v in enumerate(aps)}, mean_ap
     dev = torch.device(device)
     for group in (det_boxes, det_labels, det_scores, true_boxes, true_labels, true_difficulties):
         L.require_device(*group, what='calculate_mAP')
@@ -106,5 +116,31 @@ def calculate_mAP(det_boxes, det_labels, det_scores, true_boxes, true_labels, tr
            L.ptr(ws), nb, L.stream_of(db))
     aps = ap.cpu().tolist()
     mean_average_precision = float(mean.cpu().item())
-    rev_label_map = {v: k for k, v in label_map.items()}
     return {rev_label_map[c + 1]: v for c, v in enumerate(aps)}, mean_average_precision
+
+
+def accuracy(scores, targets, k):
+    """Top-k accuracy in percent (metrics.py:255-268): the share of rows whose target is among
+    the k highest scores, times 100."""
+    _, ind = scores.topk(k, 1, True, True)
+    hits = ind.eq(targets.view(-1, 1).expand_as(ind)).view(-1).float().sum()
+    return hits.item() * (100.0 / targets.size(0))
+
+
+class AverageMeter(object):
+    """Latest value, running sum, count and mean of a metric (metrics.py:271-289)."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.val = 0
+        self.avg = 0
+        self.sum = 0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count

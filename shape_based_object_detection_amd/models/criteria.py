@@ -6,6 +6,9 @@ the fused HIP path (matcher kernels + one fused loss pass + mining + finaliser).
   * ``RetinaFocalLoss``  — ``models/RetinaNet.py:353-506`` (focal / n_pos, negatives-only pool)
   * ``RefineDetLoss``    — ``models/RefineDet512.py:698-956`` (binary ARM + ODM on decoded ARM)
 
+CPU tensors (the reference's ``device = 'cpu'``, train_anchor.py:65-71; config C1) take the host
+path (``hostpath.py``: torch-CPU restatement, autograd backward); ROCm tensors the HIP path.
+
 Constructed as ``criterion(priors_cxcy=model.priors_cxcy, config=config)`` (train_anchor.py:172)
 with ``config`` exposing ``reg_weights, device, n_classes, reg_loss, cls_loss``; called as
 ``criterion(locs [B,P,4], scores [B,P,C], boxes: list of [G_i,4], labels: list of [G_i])``.
@@ -25,7 +28,9 @@ from torch import nn
 
 from .. import _lib as L
 from .. import core
+from .. import hostpath
 from ..dataset.transforms import cxcy_to_xy
+from ..metrics import on_host
 
 
 def _cfg(config, key, default=None):
@@ -83,11 +88,17 @@ class _AnchorCriterion(nn.Module):
         return core.CriterionSpec(reg, cls, flags, self.neg_pos_ratio, float(self.alpha))
 
     def forward(self, predicted_locs, predicted_scores, boxes, labels):
-        if not (predicted_locs.is_cuda and predicted_scores.is_cuda):
-            L.require_device(predicted_locs, predicted_scores, what=type(self).__name__)
         B, P, _ = predicted_scores.shape
         n_priors = self.priors_cxcy.size(0)
         assert n_priors == predicted_locs.size(1) == predicted_scores.size(1)
+        if not self.distributed and on_host(predicted_locs, predicted_scores):
+            # the reference's CPU device (train_anchor.py:65-71): the host path, no kernels
+            # (data parallelism is the ROCm path's: its RCCL exchange steps need device tensors)
+            return hostpath.anchor_criterion(self.KIND, self.priors_cxcy.cpu(), self.priors_xy.cpu(),
+                                             predicted_locs, predicted_scores, boxes, labels,
+                                             _cfg(self.config, 'reg_loss', 'smoothl1'),
+                                             _cfg(self.config, 'cls_loss', 'ce'), self.threshold,
+                                             self.neg_pos_ratio, self.alpha)
         gt = core.pack_gt(boxes, labels)
         obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold)
         tot = (core.allreduce_npos(npos, self.process_group, self.force_collectives)
@@ -164,6 +175,9 @@ class RefineDetLoss(nn.Module):
 
     def compute_arm_loss(self, arm_locs, arm_scores, boxes, labels):
         """Binary anchor-refinement loss vs the fixed priors (RefineDet512.py:730-820)."""
+        if not self.distributed and on_host(arm_locs, arm_scores):
+            return hostpath.refinedet_arm(self.priors_cxcy.cpu(), self.priors_xy.cpu(), arm_locs, arm_scores,
+                                          boxes, labels, self.threshold, self.neg_pos_ratio, self.alpha)
         L.require_device(arm_locs, arm_scores, what='RefineDetLoss')
         B, P, _ = arm_scores.shape
         gt = core.pack_gt(boxes, labels)
@@ -179,6 +193,10 @@ class RefineDetLoss(nn.Module):
     def compute_odm_loss(self, arm_locs, arm_scores, odm_locs, odm_scores, boxes, labels):
         """Refined-detection loss vs the per-image decoded ARM boxes with easy negatives
         (softmax(ARM)[...,1] < theta) removed (RefineDet512.py:822-939)."""
+        if not self.distributed and on_host(arm_locs, arm_scores, odm_locs, odm_scores):
+            return hostpath.refinedet_odm(self.priors_cxcy.cpu(), arm_locs, arm_scores, odm_locs, odm_scores,
+                                          boxes, labels, self.threshold, self.neg_pos_ratio, self.alpha,
+                                          self.theta)
         L.require_device(arm_locs, arm_scores, odm_locs, odm_scores, what='RefineDetLoss')
         B, P, _ = odm_scores.shape
         assert P == self.priors_cxcy.size(0) == odm_locs.size(1)

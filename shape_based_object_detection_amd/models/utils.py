@@ -7,9 +7,12 @@ order 1..C-1 unless more than top_k objects survive (then the top_k by score), t
 [[0,0,1,1]] / 0 / 0 placeholder for an image without detections, and the in-place clamp of the
 caller's ``predicted_locs`` when box_type is neither 'offset' nor 'center'.
 NMS semantics are torchvision.ops.nms's (models/utils.py:5,265): suppress IoU > max_overlap,
-ties in score resolved by lower prior index.
+ties in score resolved by lower prior index.  CPU tensors (the reference's ``device = 'cpu'``)
+take the host path (``hostpath.detect``), ROCm tensors the HIP kernels.
 """
 from .. import core
+from .. import hostpath
+from ..metrics import on_host
 
 
 def _cfg(config, key, default=None):
@@ -28,6 +31,10 @@ def detect(predicted_locs, predicted_scores, min_score, max_overlap, top_k, prio
     focal_type = str(_cfg(config, 'focal_type', 'softmax'))
     act = 'sigmoid' if focal_type.lower() == 'sigmoid' else 'softmax'
     bt = box_type if box_type in ('offset', 'center') else 'corner'
+    if on_host(predicted_locs, predicted_scores):
+        return hostpath.detect(predicted_locs, predicted_scores, min_score, max_overlap, top_k,
+                               priors_cxcy.cpu() if priors_cxcy is not None else None, bt, act,
+                               prior_positives_idx)
     return core.detect(predicted_locs, predicted_scores, min_score, max_overlap, top_k, priors_cxcy,
                        box_type=bt, act=act, pos_mask=prior_positives_idx)
 

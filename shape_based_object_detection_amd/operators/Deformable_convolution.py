@@ -6,12 +6,14 @@ modulation=True)`` with children ``zero_padding``, ``conv`` (k×k, stride k), ``
 backward hook.  The offset / mask convolutions stay ordinary convolutions (MIOpen); the
 sampling + modulation + k×k contraction, forward and backward, is one C-ABI call each
 (``sbod_dcn_fwd_f32`` / ``sbod_dcn_bwd_f32``, fp32 MFMA) instead of the reference's chain of
-gathers, concatenations and an im2col-sized intermediate.
+gathers, concatenations and an im2col-sized intermediate.  CPU tensors take the host path
+(``hostpath.deform_conv2d``: the reference's sampling arithmetic in torch, autograd backward).
 """
 import torch
 from torch import nn
 
 from .. import core
+from .. import hostpath
 
 
 class DeformConv2d(nn.Module):
@@ -43,6 +45,10 @@ class DeformConv2d(nn.Module):
     def forward(self, x):
         offset = self.p_conv(x)
         mask_logits = self.m_conv(x) if self.modulation else None
+        if not x.is_cuda:
+            out = hostpath.deform_conv2d(x, offset, mask_logits, self.conv.weight, self.kernel_size,
+                                         self.padding, self.stride)
+            return out + self.conv.bias.view(1, -1, 1, 1) if self.conv.bias is not None else out
         out = core.deform_conv2d(x, offset, mask_logits, self.conv.weight, self.kernel_size,
                                  self.padding, self.stride)
         if self.conv.bias is not None:

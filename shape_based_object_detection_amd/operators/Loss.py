@@ -2,12 +2,15 @@
 
 Per-row values and their derivatives come from the sbod kernels; the reductions stay the
 reference's own (sum, ``sum / num`` rows for 'mean', ``Σ(l·w)/Σw`` when ``Σw > 1e-6``) so the
-numbers match Loss.py's.
+numbers match Loss.py's.  CPU tensors take the host path (``hostpath.py``, the reference's own
+torch ops, autograd backward).
 """
 import torch
 from torch import nn
 
 from .. import core
+from .. import hostpath
+from ..metrics import on_host
 from .iou_utils import bbox_overlaps_ciou, bbox_overlaps_diou, bbox_overlaps_giou, bbox_overlaps_iou
 
 
@@ -18,6 +21,8 @@ def focal_loss(y_pred, y_true, alpha=0.25, gamma=2., device='cuda:0'):
         fore_alpha, back_alpha = alpha[0], alpha[1]
     else:
         fore_alpha, back_alpha = alpha, 1 - alpha
+    if on_host(y_pred, y_true):
+        return hostpath.focal_softmax(y_pred, y_true, (fore_alpha, back_alpha), gamma)
     return core.focal_rows('softmax', y_pred, y_true, fore_alpha, back_alpha, gamma).sum()
 
 
@@ -31,6 +36,8 @@ class SigmoidFocalLoss(nn.Module):
         self.device = getattr(config, 'device', None) if not isinstance(config, dict) else config.get('device')
 
     def forward(self, out, target):
+        if on_host(out, target):
+            return hostpath.focal_sigmoid(out, target, self.alpha, self.gamma)
         return core.focal_rows('sigmoid', out, target, self.alpha, 1 - self.alpha, self.gamma).sum()
 
 
@@ -43,6 +50,8 @@ class FocalLoss(nn.Module):
         self.gamma = gamma
 
     def forward(self, pred_logits, targets):
+        if on_host(pred_logits, targets):
+            return hostpath.focal_bce(pred_logits, targets, self.alpha, self.gamma)
         return core.focal_rows('bce', pred_logits, targets, self.alpha, 1 - self.alpha, self.gamma).sum()
 
 
@@ -90,7 +99,10 @@ class SmoothL1Loss(nn.Module):
 
     def forward(self, pred, target, weights=None):
         num = pred.size(0)
-        l1_loss = core.smooth_l1_elementwise(pred, target, self.beta)
+        if on_host(pred, target):
+            l1_loss = hostpath.smooth_l1_elementwise(pred, target, self.beta)
+        else:
+            l1_loss = core.smooth_l1_elementwise(pred, target, self.beta)
         if weights is not None and weights.sum() > 1e-6:
             assert pred.size(0) == target.size(0) == weights.size(0)
             return (l1_loss * weights).sum() / weights.sum()

@@ -6,20 +6,22 @@
     ``intersect`` / ``jaccard`` (:192-233), ``match`` / ``match_ious`` (:236-321, in place into
     ``loc_t[idx]`` / ``conf_t[idx]``), ``encode`` / ``decode`` (:324-368), ``log_sum_exp`` (:371-379),
     ``nms`` / ``diounms`` (:385-530: (keep, count), or the bare zero ``keep`` for empty input).
-Device tensors run the HIP kernels.  CPU tensors run the host path (``host.py``) for the box
-utilities the data-loader side uses (point_form, intersect, jaccard, encode, decode); the rest
-is device-only and raises on CPU tensors.
+Device tensors run the HIP kernels.  CPU tensors run the host path (``host.py`` for the box
+utilities, ``hostpath.py`` for the overlaps, match and NMS): the reference's own CPU arithmetic.
 """
 import torch
 
 from .. import _lib as L
 from .. import core
 from .. import host
+from .. import hostpath
 from .. import metrics as _metrics
 from ..metrics import on_host
 
 
 def _overlaps(kind, bboxes1, bboxes2):
+    if on_host(bboxes1, bboxes2):
+        return hostpath.aligned_overlap(kind, bboxes1, bboxes2)
     rows, cols = bboxes1.shape[0], bboxes2.shape[0]
     if rows * cols == 0:
         return torch.zeros((rows, cols), device=bboxes1.device)
@@ -75,6 +77,8 @@ def jaccard(box_a, box_b):
 
 
 def _match(threshold, truths, priors, variances, labels, loc_t, conf_t, idx, encode):
+    if on_host(truths, priors, labels, loc_t, conf_t):
+        return hostpath.match_ssd(threshold, truths, priors, variances, labels, loc_t, conf_t, idx, encode)
     L.require_device(truths, priors, labels, loc_t, conf_t, what='match')
     if not (loc_t.is_contiguous() and conf_t.is_contiguous() and loc_t.dtype == torch.float32
             and conf_t.dtype == torch.int64):
@@ -115,13 +119,15 @@ def decode(loc, priors, variances):
 
 
 def log_sum_exp(x):
-    """log(sum(exp(x - max), 1)) + max with the GLOBAL max (iou_utils.py:371-379)."""
-    L.require_device(x, what='log_sum_exp')
+    """log(sum(exp(x - max), 1)) + max with the GLOBAL max (iou_utils.py:371-379): element-wise
+    torch arithmetic on either device."""
     x_max = x.data.max()
     return torch.log(torch.sum(torch.exp(x - x_max), 1, keepdim=True)) + x_max
 
 
 def _nms(variant, boxes, scores, overlap, top_k, beta1=1.0):
+    if on_host(boxes, scores):
+        return hostpath.nms_ref(boxes, scores, overlap, top_k, diou=variant == 'diou', beta1=beta1)
     L.require_device(boxes, scores, what=variant)
     if boxes.numel() == 0:
         return scores.new_zeros(scores.size(0), dtype=torch.long)

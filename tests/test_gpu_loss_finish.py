@@ -1,0 +1,122 @@
+"""The focal criteria's in-launch loss finish (loss.hip multibox_finish) at the edges of its
+range, against the oracle (Loss.py:9-38 focal_loss through models/*.py) and against the
+separate double-accumulating finaliser (SBOD_LOSS_UNFUSED_FINISH):
+
+  * RetinaNet-sized grids (B=32, P=32,736: 4,096 workgroups, 128 per accumulator line);
+  * large but finite logits (per-row losses ~100) and huge ones (softmax underflow: the
+    reference's 0 * log 0 NaN, which the finish must carry instead of wrapping);
+  * a near-zero loss (every row exactly 0 but a dozen at 1e-7): the fixed-point resolution.
+
+Tolerance: fp32 losses within 1e-4 relative of the oracle (north_star); the fused and the
+unfused finish sum the same fp32 workgroup partials, so they agree within 1e-6."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import loss_ref as LR
+from shape_based_object_detection_amd import _lib as L
+from shape_based_object_detection_amd import core, synth
+from shape_based_object_detection_amd.models import criteria as CR
+from shape_based_object_detection_amd.models.priors import prior_table
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+class Cfg(dict):
+    __getattr__ = dict.__getitem__
+
+
+CLASSES = {'ssd512': CR.MultiBoxLoss512, 'retina': CR.RetinaFocalLoss}
+
+
+def _crit(kind, P, reg, reg_weights=1.0, unfused=False):
+    crit = CLASSES[kind](priors_cxcy=P.to(DEV), config=Cfg(reg_weights=reg_weights, device=DEV, n_classes=21,
+                                                           reg_loss=reg, cls_loss='focal'))
+    if unfused:
+        s = crit._spec()
+        crit._spec_cache = core.CriterionSpec(s.reg, s.cls, s.flags | L.LOSS_UNFUSED_FINISH, s.neg_pos_ratio,
+                                              s.reg_weight, s.alpha, s.gamma)
+    return crit
+
+
+def _loss(crit, locs, scores, boxes, labels):
+    lo = locs.to(DEV).requires_grad_(True)
+    sc = scores.to(DEV).requires_grad_(True)
+    loss = crit(lo, sc, [b.to(DEV) for b in boxes], [l.to(DEV) for l in labels])
+    comps = crit.last_components.cpu().numpy()
+    loss.backward()
+    return float(loss.item()), comps, sc.grad.cpu().numpy()
+
+
+def _oracle(kind, P, locs, scores, boxes, labels, reg, reg_weights=1.0):
+    lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
+    ref = LR.criterion(kind, P, lo, sc, boxes, labels, reg, 'focal', reg_weights=reg_weights)
+    ref.backward()
+    return float(ref.item()), sc.grad.numpy()
+
+
+def test_fused_finish_retina_full_batch():
+    """B=32 x 32,736 anchors (4,096 workgroups folding into 32 group lines): the fused finish
+    equals the double-accumulated one and the oracle."""
+    P = torch.from_numpy(prior_table('RETINA'))
+    B = 32
+    boxes, labels = synth.make_gt(B, seed=23)
+    locs, scores = synth.make_preds(B, P.shape[0], 21, seed=23)
+    fused, cf, gf = _loss(_crit('retina', P, 'diou'), locs, scores, boxes, labels)
+    unf, cu, gu = _loss(_crit('retina', P, 'diou', unfused=True), locs, scores, boxes, labels)
+    np.testing.assert_allclose(cf, cu, rtol=1e-6)
+    assert np.array_equal(gf, gu)
+    ref, _ = _oracle('retina', P, locs, scores, boxes, labels, 'diou')
+    np.testing.assert_allclose(fused, ref, rtol=1e-4)
+
+
+@pytest.mark.parametrize('scale', [10.0, 1e4])
+def test_fused_finish_large_logits(scale):
+    """Logits x10 (finite, per-row losses up to ~100) and x1e4 (softmax underflows to exactly 0:
+    the reference's loss is NaN, and so must the fused finish's be — never a wrapped value)."""
+    P = torch.from_numpy(prior_table('SSD512'))
+    B = 8
+    boxes, labels = synth.make_gt(B, seed=29)
+    locs, scores = synth.make_preds(B, P.shape[0], 21, seed=29)
+    scores = scores * scale
+    fused, cf, _ = _loss(_crit('ssd512', P, 'diou'), locs, scores, boxes, labels)
+    unf, cu, _ = _loss(_crit('ssd512', P, 'diou', unfused=True), locs, scores, boxes, labels)
+    ref, _ = _oracle('ssd512', P, locs, scores, boxes, labels, 'diou')
+    if np.isnan(ref):
+        assert np.isnan(fused) and np.isnan(unf)
+    else:
+        assert np.isfinite(fused) and fused > 1e5
+        np.testing.assert_allclose(fused, ref, rtol=1e-4)
+        np.testing.assert_allclose(cf, cu, rtol=1e-6)
+
+
+def test_fused_finish_near_zero_loss():
+    """All-confident predictions: every focal row's loss is exactly 0 in fp32 except twelve
+    background rows (in different workgroups) whose probability is 1 - 2^-23, each ~9e-8.  The
+    total (~1e-6) must keep 1e-4 relative — a 2^-32-per-workgroup fixed point would not."""
+    P = torch.from_numpy(prior_table('SSD512'))
+    B, C = 4, 21
+    Pn = P.shape[0]
+    boxes, labels = synth.make_gt(B, seed=31)
+    crit = _crit('ssd512', P, 'smoothl1', reg_weights=0.0)
+    gt = core.pack_gt([b.to(DEV) for b in boxes], [l.to(DEV) for l in labels])
+    obj, ovl, _ = core.match(gt, crit.priors_xy, Pn, crit.threshold)
+    cls, neg, _, _ = core.match_expand(gt, obj, ovl, crit.priors_cxcy, crit.threshold, crit.threshold - 0.1,
+                                       want=('cls', 'neg'))
+    cls, neg = cls.cpu(), neg.cpu()
+    scores = torch.full((B, Pn, C), -40.0)
+    scores.scatter_(2, cls.unsqueeze(2), 0.0)            # the target class: p = 1 exactly in fp32
+    rows = []
+    for b in range(B):                                    # 3 background rows per image, far apart
+        cand = torch.nonzero((cls[b] == 0) & (neg[b] == -1)).flatten()
+        rows += [(b, int(cand[int(q * (len(cand) - 1))])) for q in (0.1, 0.5, 0.9)]
+    for b, p in rows:
+        scores[b, p, 7] = -16.3                           # 1 + e^-16.3 rounds to 1 + 2^-23
+    locs = torch.zeros(B, Pn, 4)
+    fused, cf, _ = _loss(crit, locs, scores, boxes, labels)
+    unf, cu, _ = _loss(_crit('ssd512', P, 'smoothl1', reg_weights=0.0, unfused=True), locs, scores, boxes, labels)
+    ref, _ = _oracle('ssd512', P, locs, scores, boxes, labels, 'smoothl1', reg_weights=0.0)
+    assert 1e-7 < ref < 1e-5
+    np.testing.assert_allclose(fused, ref, rtol=1e-4)
+    np.testing.assert_allclose(cf[1], cu[1], rtol=1e-6)

@@ -121,7 +121,7 @@ def test_codecs_and_match_api():
 
 def test_cpu_and_device_paths_agree():
     """CPU tensors take the host path (DataLoader workers); device tensors the HIP
-    kernel: bit-identical IoU.  Mixed devices raise; device-only ops reject CPU tensors."""
+    kernel: bit-identical IoU.  Mixed devices raise; the C-ABI wrappers reject CPU tensors."""
     from shape_based_object_detection_amd import _lib as L
     from shape_based_object_detection_amd.operators import iou_utils as IU
     g = torch.rand(7, 2)
@@ -135,8 +135,9 @@ def test_cpu_and_device_paths_agree():
     assert torch.equal(IU.jaccard(gt, an), IU.jaccard(gt.cuda(), an.cuda()).cpu())
     with pytest.raises(RuntimeError):
         metrics.find_jaccard_overlap(gt, an.cuda())
+    from shape_based_object_detection_amd import core
     with pytest.raises(L.SbodError):
-        IU.nms(torch.rand(4, 4), torch.rand(4))
+        core.nms(torch.rand(4, 4), torch.rand(4), 0.5)
 
 
 @pytest.mark.parametrize('kind', ['iou', 'giou', 'diou', 'ciou'])
