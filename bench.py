@@ -125,6 +125,9 @@ ALGO_BYTES = {
     'k_multibox': lambda w: w['B'] * w['P'] * (2 * (16 + 4 * w['C']) + 8) + 16 * w['P'],
     # priors read per image tile, obj + overlap written
     'k_match_tile': lambda w: w['B'] * w['P'] * (16 + 8),
+    # the one-launch focal criterion (matcher + loss pass): locs + scores read, their gradients
+    # written, obj + overlap written, priors (xyxy and cxcy) read once
+    'k_criterion': lambda w: w['B'] * w['P'] * (2 * (16 + 4 * w['C']) + 8) + 32 * w['P'],
 }
 HBM_KERNELS = tuple(ALGO_BYTES)
 ALL_KERNELS = HBM_KERNELS + ('k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm')

@@ -236,6 +236,37 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
                        void *grad_locs, void *grad_scores, float *loss_out, void *workspace,
                        size_t workspace_bytes, void *stream);
 
+/* One-launch focal criterion: the matcher (sbod_match_f32 with shared priors) and the fused
+ * focal pass (sbod_multibox_loss, cls = SBOD_CLS_FOCAL) in ONE launch — MultiBoxLoss512 /
+ * MultiBoxLoss300 / RetinaFocalLoss with cls_loss 'focal' on one device
+ * (models/SSD512.py:508-626, SSD300.py:477-594, RetinaNet.py:385-506).  Every workgroup matches
+ * its 256 priors, the last tile of each image runs that image's forced match, and every
+ * workgroup waits (in the launch) until all images are counted in before it applies its priors'
+ * forced rewrites and computes its rows' losses and gradients scaled by the batch's positives.
+ * Same outputs as the two calls: obj / ovl [B,P], n_pos [B+1] (n_pos[B] = the batch total),
+ * grad_locs / grad_scores (may be NULL), loss_out {total, conf, loc, n_pos}.
+ * The grid (B * ceil(P/256) workgroups) must be resident at once; when the occupancy query says
+ * it is not (or with SBOD_CRIT_TWO_LAUNCH / SBOD_LOSS_UNFUSED_FINISH) the call runs the two
+ * launches instead, on the same workspace, with the same results.  Data parallelism (a
+ * normaliser all-reduced between the matcher and the loss) uses the two calls.
+ * Workspace: sbod_criterion_workspace_bytes(B, Gmax, P); its first
+ * sbod_criterion_zero_bytes(B, Gmax, P) bytes must be zero on entry and are left zero by every
+ * successful call: pass SBOD_CRIT_WS_ZEROED when they are (else the call zeroes them, one
+ * hipMemsetAsync).  flags: SBOD_LOSS_FOCAL_NORM, SBOD_CRIT_WS_ZEROED, SBOD_CRIT_TWO_LAUNCH,
+ * SBOD_LOSS_UNFUSED_FINISH.  sbod_criterion_status() (diagnostics, synchronises the stream) reads
+ * the word a bounded in-launch wait sets if it ever gives up (the loss is NaN then). */
+enum { SBOD_CRIT_WS_ZEROED = 128, SBOD_CRIT_TWO_LAUNCH = 1024 };
+size_t sbod_criterion_workspace_bytes(int B, int Gmax, int P);
+size_t sbod_criterion_zero_bytes(int B, int Gmax, int P);
+int sbod_criterion_focal(const void *locs, const void *scores, int dtype, int B, int P, int C,
+                         const float *priors_cxcy, const float *priors_xy, const float *gt_boxes,
+                         const int64_t *gt_labels, const int32_t *gt_offsets, int Gmax, float threshold,
+                         float neg_threshold, int reg, int flags, float reg_weight, float focal_alpha,
+                         float focal_gamma, int32_t *obj, float *ovl, int32_t *n_pos, void *grad_locs,
+                         void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
+                         void *stream);
+int sbod_criterion_status(const void *workspace, void *stream);
+
 /* grad *= (*scale) in place unless *scale == 1 (decided on the device: no host sync).
  * Used by backward to apply the upstream gradient to gradients produced by the fused
  * forward. */

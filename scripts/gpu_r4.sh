@@ -1,12 +1,19 @@
 #!/bin/bash
-# GPU box, round 4: the -m gpu suite, smoke(), the bench line and a rocprofv3 kernel-stats run of
-# the same bench command.  Every GPU step has its own time limit; the chain stops at the first
-# failure.   Usage: bash scripts/gpu_r3.sh TAG [bench args...]
+# GPU box, round 4: the -m gpu suite (the given test files first), smoke(), the bench line and a
+# rocprofv3 kernel-stats run of the same bench command.  Every GPU step has its own time limit;
+# the chain stops at the first failure.
+#   Usage: FIRST="tests/test_x.py ..." bash scripts/gpu_r4.sh TAG [bench args...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-run}; shift
 mkdir -p gpurun_out
+ok=0
+if [ -n "$FIRST" ]; then
+  timeout -k 10 300 python -u -m pytest $FIRST -m gpu -x -v --timeout 120 --timeout-method thread \
+      > gpurun_out/tests_first_$TAG.log 2>&1 || ok=1
+fi
+[ $ok -eq 0 ] && \
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > gpurun_out/tests_$TAG.log 2>&1 && \
 timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_$TAG.log 2>&1 && \
@@ -16,5 +23,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o ru
     python3 scripts/roofline_check.py gpurun_out/bench_$TAG.json gpurun_out/prof_$TAG/run_kernel_trace.csv \
         gpurun_out/roofline_check_$TAG.json gpurun_out/prof_$TAG.log > /dev/null
 rc=$?
+[ $ok -ne 0 ] && rc=1
 echo "EXIT $rc"
 exit $rc

@@ -45,11 +45,16 @@ def main(bench_json, trace_csv, out=None, prof_log=None):
         for ln in open(prof_log):
             if ln.startswith('{') and '"roofline"' in ln:
                 win = json.loads(ln)['roofline'].get('trace_window_ns')
+    def keys_of(name):
+        # k_multibox<..., true> is the one-launch criterion (its KernelTimer name: k_criterion)
+        if 'k_multibox<' in name:
+            return ['k_criterion' if 'true>' in name else 'k_multibox']
+        return [k for k in algo if (k + '<') in name or (k + '(') in name]
     with open(trace_csv) as f:
         for r in csv.DictReader(f):
             name = r['Kernel_Name']
-            for k in algo:
-                if (k + '<') in name or (k + '(') in name:
+            for k in keys_of(name):
+                if k in algo:
                     if 'unsigned short' in name:      # the bf16 (C2) instantiation
                         continue
                     if int(r['Grid_Size_X']) == grid_x and int(r['Grid_Size_Y']) == B:

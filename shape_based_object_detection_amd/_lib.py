@@ -38,6 +38,11 @@ SIGNATURES = {
                                  F32, I32, I32, I32, I32, F32, F32, F32, P, P, P, P, SZ, P]),
     'sbod_loss_pool_offset': (SZ, [I32, I32]),
     'sbod_loss_zero_prefix_bytes': (SZ, []),
+    'sbod_criterion_workspace_bytes': (SZ, [I32, I32, I32]),
+    'sbod_criterion_zero_bytes': (SZ, [I32, I32, I32]),
+    'sbod_criterion_focal': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32, I32, F32, F32, F32,
+                                   P, P, P, P, P, P, P, SZ, P]),
+    'sbod_criterion_status': (I32, [P, P]),
     'sbod_multibox_mine_global': (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, F32, P, I64, I64, P,
                                         P, P, SZ, P]),
     'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),
@@ -82,6 +87,7 @@ LOSS_FOCAL_NORM = 4
 LOSS_DEFER_MINING = 64
 LOSS_WS_ZEROED = 128
 LOSS_UNFUSED_FINISH = 512
+CRIT_WS_ZEROED, CRIT_TWO_LAUNCH = 128, 1024
 POOL = dict(nonpos=0, neg=8, global_neg=16, nonpos_not_easy=32)
 OV = dict(iou=0, giou=1, diou=2, ciou=3)
 FOCAL = dict(softmax=0, sigmoid=1, bce=2)

@@ -104,7 +104,7 @@ def _mark(target, key):
         f.write(key + '\n')
 
 
-_RES_RE = re.compile(r'remark: +(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|'
+_RES_RE = re.compile(r'remark: +(Function Name|VGPRs|AGPRs|TotalSGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|'
                      r'LDS Size \[bytes/block\]): (\S+)')
 
 

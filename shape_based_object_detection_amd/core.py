@@ -445,6 +445,68 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
     return loss, holder[0]
 
 
+def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, neg_threshold,
+                    two_launch=False):
+    """A focal criterion on one device in ONE launch (sbod_criterion_focal): the matcher and the
+    fused loss + gradient pass, the normaliser produced inside the launch.  Returns (scalar loss
+    with autograd, device vector {total, conf, loc, n_pos_total}, (obj, ovl, n_pos)).
+    ``two_launch`` runs the same call as the matcher and loss launches (A/B, tests)."""
+    locs = locs.contiguous()
+    scores = scores.contiguous()
+    if locs.dtype not in (torch.float32, torch.bfloat16) or scores.dtype != locs.dtype:
+        raise TypeError('sbod criterion: locs/scores must both be float32 or bfloat16')
+    dt = L.DT_F32 if locs.dtype == torch.float32 else L.DT_BF16
+    B, P, C = scores.shape
+    if locs.shape != (B, P, 4) or priors_cxcy.shape[0] != P:
+        raise AssertionError('n_priors mismatch: priors %d, locs %s, scores %s'
+                             % (priors_cxcy.shape[0], tuple(locs.shape), tuple(scores.shape)))
+    if gt.batch != B:
+        raise ValueError('criterion: %d images of ground truth for a batch of %d' % (gt.batch, B))
+    dev = locs.device
+    stream = L.stream_of(locs)
+    obj = torch.empty(B, P, dtype=torch.int32, device=dev)
+    ovl = torch.empty(B, P, dtype=torch.float32, device=dev)
+    npos = torch.empty(B + 1, dtype=torch.int32, device=dev)
+    gmax = max(int(gt.gmax), 1)
+    pxy = priors_xy.contiguous()
+    holder = []
+
+    def run(want_grad):
+        out = torch.empty(4, dtype=torch.float32, device=dev)
+        holder.append(out)
+        gl = torch.empty_like(locs) if want_grad else None
+        gs = torch.empty_like(scores) if want_grad else None
+        lib = L.lib()
+        nb = lib.sbod_criterion_workspace_bytes(B, gmax, P)
+        zb = lib.sbod_criterion_zero_bytes(B, gmax, P)
+        ws = workspace(nb, dev, 'criterion')
+        zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion')
+        _CLEAN.pop(ws.data_ptr(), None)
+        flags = (spec.flags & L.LOSS_FOCAL_NORM) | zflag | (L.CRIT_TWO_LAUNCH if two_launch else 0)
+        L.call('sbod_criterion_focal', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy), L.ptr(pxy),
+               L.ptr(gt.boxes), L.ptr(gt.labels), L.ptr(gt.offsets), gmax, float(threshold), float(neg_threshold),
+               spec.reg, flags, float(spec.reg_weight), float(spec.alpha), float(spec.gamma), L.ptr(obj), L.ptr(ovl),
+               L.ptr(npos), L.ptr(gl), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
+        _CLEAN[ws.data_ptr()] = zb   # (only the zero-on-entry prefix is known clean)
+        return out, gl, gs
+
+    want = torch.is_grad_enabled() and (locs.requires_grad or scores.requires_grad)
+    loss = _FusedLoss.apply(locs, scores, run, want)
+    return loss, holder[0], (obj, ovl, npos)
+
+
+def criterion_status(device=None):
+    """The one-launch criterion's in-launch wait status on ``device`` (current stream's cached
+    workspace): 0 = every wait completed.  Synchronises the stream (diagnostics, tests)."""
+    dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+    key = (dev if dev.index is not None else torch.device('cuda', torch.cuda.current_device()),
+           L._raw_stream(dev.index if dev.index is not None else torch.cuda.current_device()), 'criterion')
+    ws = _WS.get(key)
+    if ws is None:
+        return 0
+    return L.lib().sbod_criterion_status(L.ptr(ws), L._raw_stream(key[0].index))
+
+
 _POOL_SIZES_OK = set()   # (group, world, B*P) whose equality over the ranks was verified
 
 

@@ -14,7 +14,10 @@
 // Roofline: HBM-bound; algorithmic bytes per launch = B*P*(4+C)*s read + B*P*(4+C)*s written.
 #include <hip/hip_bf16.h>
 
-#include "sbod_common.h"
+#include <mutex>
+#include <vector>
+
+#include "match_dev.h"
 
 namespace sbod {
 
@@ -317,6 +320,17 @@ struct LossArgs {
   // arrival counter of the workgroups; null: partials for k_loss_final
   unsigned long long *fin;
   float *out;                 // the loss vector {total, conf, loc, n_pos} (fused finish)
+  // one-launch criterion (k_multibox<..., true>): the matcher's in-launch state and outputs
+  const float *anchors;       // priors_xy [P,4]
+  int Gmax;
+  int32_t *obj_out, *npos_out;   // [B,P] object per prior, [B+1] positives per image and total
+  float *ovl_out;             // [B,P] overlap per prior
+  unsigned long long *keys;   // [B][kKeyShards][Gmax] best-prior keys, zero on entry
+  unsigned long long *arrive; // [B] (tiles arrived << 32) | their phase-1 positives, zero on entry
+  unsigned long long *done;   // (images finished << 32) | their positives, zero on entry
+  unsigned *status;           // nonzero: a wait gave up (see kSpinLimit)
+  unsigned long long *forced; // [B][Gmax] (prior << 32 | object) rewritten by the forced match
+  int32_t *nforced;           // [B]
 };
 
 // The fused finish of k_multibox (focal / no mining).  Each workgroup folds its partial sums
@@ -329,10 +343,10 @@ struct LossArgs {
 // folded exactly: it travels as a flag bit, and the finishing workgroup then sums every
 // workgroup's fp32 partial in double instead (each workgroup also writes its two partials
 // through with sc1 stores before it counts itself in), as k_loss_final would — the finish is
-// never silently wrong.  Non-finite partials (NaN rows of the focal loss) keep their own flag
-// bits (NaN, +inf, -inf per component).  The adds are drained (s_waitcnt with a compiler memory
-// clobber) before the arrival add, and every hand-off moves through memory-side atomics or sc1
-// stores/loads, so no cache write-back or invalidation is needed between the XCDs.
+// never silently wrong (a NaN row of the focal loss, the reference's 0 * log 0, makes a NaN loss
+// that way).  The adds are drained (s_waitcnt with a compiler memory clobber) before the arrival
+// add, and every hand-off moves through memory-side atomics or sc1 stores/loads, so no cache
+// write-back or invalidation is needed between the XCDs.
 constexpr float kFinLimit = 1099511627776.f;   // 2^40: larger partials take the double fallback
 struct Fx128 {
   unsigned long long lo, hi;
@@ -377,7 +391,6 @@ constexpr int kFinStride = 16;   // u64 words per accumulator set: one 128-byte 
 constexpr size_t kFinBytes = sizeof(unsigned long long) * kFinStride * (kFinGroups + 1);   // 4224
 // Accumulator set (one 128-byte line): conf {lo, hi}, loc {lo, hi}, fallback flag, arrivals.
 enum { kFinConf = 0, kFinLoc = 2, kFinFlag = 4, kFinArrive = 5 };
-__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // w[0..1] += v (128-bit): the lo add returns the previous word, which gives this add's carry.
 __device__ __forceinline__ void fx_add(unsigned long long *w, Fx128 v) {
   unsigned long long carry = 0;
@@ -392,7 +405,7 @@ __device__ __forceinline__ unsigned long long xchg0(unsigned long long *w) {
 }
 // Called by wave 0 of every workgroup (all 64 lanes; conf_l / loc_l uniform).  The partials
 // array holds each workgroup's fp32 {conf, loc} for the double fallback.
-__device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, unsigned nblk, float *out) {
+__device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, unsigned nblk, float n, float *out) {
   // accumulators: kFinGroups group lines, then the top line.  Two levels because atomics on one
   // word serialise at the memory side (~10 ns each): ~41 arrivals per group word and 32 on the
   // top word instead of every workgroup on one word.
@@ -458,23 +471,58 @@ __device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, un
       l += __shfl_xor(l, m, 64);
     }
   }
-  if (lane == 0) loss_outputs(c, l, static_cast<float>(*a.npos_total), a.reg, a.cls, a.flags, a.reg_weight, out);
+  if (lane == 0) {
+    loss_outputs(c, l, n, a.reg, a.cls, a.flags, a.reg_weight, out);
+    if (a.done != nullptr) {   // one-launch criterion: every workgroup has passed its wait
+      a.npos_out[a.B] = static_cast<int32_t>(n);
+      if (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        out[0] = out[1] = out[2] = __builtin_nanf("");
+      }
+      __hip_atomic_store(a.done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'
 // budget is 1e-4 relative; the all-classes underflow test (p == 0 -> NaN) stays exact (below).
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
+// One-launch criterion: every workgroup waits until all images' forced matches are counted in
+// (their positives are the gradients' normaliser).  The grid is co-resident (the host checks it
+// against the occupancy query before choosing this form), so the wait ends within microseconds;
+// a bound on it keeps a broken launch from hanging the device: past kSpinLimit ticks of the
+// 100 MHz real-time clock the workgroup sets *status and goes on (the loss becomes NaN).
+constexpr unsigned long long kSpinLimit = 2000000ull;   // 20 ms
+__device__ __forceinline__ unsigned wait_all_images(unsigned long long *done, int B, unsigned *status) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const unsigned long long v = ld_wt_u64(done);
+    if ((v >> 32) >= static_cast<unsigned long long>(B)) return static_cast<unsigned>(v);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit) {
+      __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return static_cast<unsigned>(v);
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // CM > 0: class rows of C <= CM in registers (padding slots -inf: no per-slot guards in the
 // max / exp / sum); CM == 0: any C, rows in LDS.
-template <typename T, int CM, int CLS>
+// kFused (focal criteria, shared priors, one rank): the matcher runs in the same launch — the
+// workgroup first matches its own 256 priors (match_wave, keys into the shards, phase-1 (obj, ovl)
+// written through), counts itself in at its image, and the image's last tile runs the image's
+// forced match (match_final_image) and counts the image in; every workgroup then loads its score
+// tile, waits for all images (the normaliser), applies the forced rewrites of its own priors from
+// the image's list, and goes on with the loss pass on registers it already holds.
+template <typename T, int CM, int CLS, bool kFused>
 __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs a, const T *__restrict__ locs,
                                                      const T *__restrict__ scores,
                                                      T *__restrict__ glocs, T *__restrict__ gsc) {
-  extern __shared__ float s_sc[];
+  extern __shared__ __attribute__((aligned(16))) float s_sc[];
   __shared__ float s_red[16];
   __shared__ int2 s_plist[kLTile];        // positive rows: wave w's at [64 w, 64 w + count)
   __shared__ int s_wcnt[kLTile / 64];
+  __shared__ int s_misc[16];
   STAMP_BEGIN();
   span_begin(a.span);
   PHASE_DECL;
@@ -492,29 +540,91 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   constexpr int NB = CM / 4;
   const T *tsrc = scores + rbase * C;
   const bool fast = fast_tile<T, NB>(tsrc, np * C);
-  if (!fast) tile_load(s_sc, tsrc, np * C);
-  const int objv = a.obj[ic];
-  const float v = a.ovl[ic];
-  const int offb = a.off[b];
-  // every load below is unconditional (a tile that is not staged through registers loads an
-  // aligned dummy vector instead): a conditional load makes the wait-count insertion at
-  // the join assume the short path and wait for the whole batch
+  int objv, offb;
+  float v, n;
+  int64_t labg;
   typename TileVec<T>::V tr[NB > 0 ? NB : 1];
-  if constexpr (NB > 0)   // (the workspace's partials: 256-byte aligned, whatever `scores` is)
-    tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
-  __builtin_amdgcn_sched_barrier(0);   // keep the tile's loads ahead of the dependent chain
-  const int g = offb + objv;
-  const int64_t labg = a.labels[g];
-  Box4 lc;
-  if constexpr (sizeof(T) == 4)
-    lc = ld4(reinterpret_cast<const float *>(locs) + 4 * ic);
-  else
-    lc = Box4{ldf(locs + 4 * ic), ldf(locs + 4 * ic + 1), ldf(locs + 4 * ic + 2), ldf(locs + 4 * ic + 3)};
-  const Box4 pri_cxcy = ld4(a.priors + 4 * static_cast<int64_t>(p0 + (valid ? tid : 0)));
-  const Box4 tb = ld4(a.gt + 4 * static_cast<int64_t>(g));
-  if constexpr (NB > 0)
-    if (fast) tile_commit(s_sc, tr, np * C);
-  const float n = static_cast<float>(*a.npos_total);
+  if constexpr (kFused) {
+    offb = a.off[b];
+    // ---- phase 1: this tile's match (the dynamic LDS holds the waves' key rows until the
+    // score tile is loaded)
+    uint32_t(*s_od)[kSlots][64] = reinterpret_cast<uint32_t(*)[kSlots][64]>(s_sc);
+    int *s_slot = reinterpret_cast<int *>(s_sc) + (kLTile / 64) * kSlots * 64;
+    unsigned long long *brow =
+        a.keys + (static_cast<int64_t>(b) * kKeyShards + (blockIdx.x & (kKeyShards - 1))) * a.Gmax;
+    const MatchLane m = match_wave<false, 0>(a.gt, a.labels, a.off, a.anchors, nullptr, nullptr, P, b,
+                                             p0 + (tid & ~63), brow, s_od[wv], s_slot + wv * kSlots);
+    if (m.valid) {   // phase-1 (obj, ovl), written through: the image's forced match reads them
+      st_wt_u32(a.obj_out + ic, static_cast<uint32_t>(m.bi));
+      st_wt_u32(reinterpret_cast<int32_t *>(a.ovl_out) + ic, __float_as_uint(m.best));
+    }
+    const int n1 = __popcll(__ballot(phase1_positive<false>(m, a.thr, 0.f)));
+    drain_vm();   // this wave's key atomics performed and its (obj, ovl) stores written through
+    if (lane == 0) s_wcnt[wv] = n1;
+    __syncthreads();
+    // ---- the tile counts itself in at its image: (1 << 32) | its phase-1 positives; the image's
+    // last tile gets the count of all of them and runs the image's forced match
+    if (tid == 0) {
+      const unsigned nt = static_cast<unsigned>(s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3]);
+      const unsigned long long old =
+          __hip_atomic_fetch_add(a.arrive + b, (1ull << 32) | nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int last = -1;
+      if ((old >> 32) == static_cast<unsigned long long>(gridDim.x - 1)) {
+        last = static_cast<int>(static_cast<unsigned>(old) + nt);
+        __hip_atomic_store(a.arrive + b, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next call
+      }
+      s_misc[15] = last;
+    }
+    __syncthreads();
+    const int cnt1 = s_misc[15];
+    if (cnt1 >= 0) {
+      match_final_image<0, true>(b, a.labels, a.off, a.keys, nullptr, 0, a.Gmax, P, a.thr, nullptr, 0.f, a.obj_out,
+                                 a.ovl_out, a.npos_out, a.B, cnt1, ForcedOut{a.forced, a.nforced, a.done},
+                                 reinterpret_cast<unsigned char *>(s_sc), s_misc);
+      __syncthreads();
+    }
+    // ---- the score tile -> LDS, in flight while the other images finish
+    if (!fast) tile_load(s_sc, tsrc, np * C);
+    if constexpr (NB > 0)
+      tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NB > 0)
+      if (fast) tile_commit(s_sc, tr, np * C);
+    // ---- every image counted in: the batch's positives, then this tile's forced rewrites
+    if (tid == 0) s_misc[14] = static_cast<int>(wait_all_images(a.done, a.B, a.status));
+    __syncthreads();
+    n = static_cast<float>(s_misc[14]);
+    objv = m.bi;
+    v = m.best;
+    const int nf = static_cast<int>(ld_wt_u32(a.nforced + b));
+    for (int k = 0; k < nf; ++k) {
+      const unsigned long long e = ld_wt_u64(a.forced + static_cast<int64_t>(b) * a.Gmax + k);
+      if (static_cast<int>(e >> 32) == m.p) {
+        objv = static_cast<int>(static_cast<uint32_t>(e));
+        v = 1.0f;
+      }
+    }
+    labg = a.labels[offb + objv];
+  } else {
+    // memory schedule: the row's matcher outputs first, then the score tile, then the label
+    // that depends on the matcher outputs — all in flight together;
+    // the tile is committed to LDS last (a tile that does not qualify for the register path is
+    // staged first, with nothing live)
+    if (!fast) tile_load(s_sc, tsrc, np * C);
+    objv = a.obj[ic];
+    v = a.ovl[ic];
+    offb = a.off[b];
+    // every load below is unconditional (a tile that is not staged through registers loads an
+    // aligned dummy vector instead): a conditional load makes the wait-count insertion at
+    // the join assume the short path and wait for the whole batch
+    if constexpr (NB > 0)   // (the workspace's partials: 256-byte aligned, whatever `scores` is)
+      tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
+    __builtin_amdgcn_sched_barrier(0);   // keep the tile's loads ahead of the dependent chain
+    labg = a.labels[offb + objv];
+    if constexpr (NB > 0)
+      if (fast) tile_commit(s_sc, tr, np * C);
+    n = static_cast<float>(*a.npos_total);
+  }
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
   const bool grad = gsc != nullptr;
   // The row's class decision before the barrier, so the tile's positive rows can be listed.
@@ -784,7 +894,7 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
            ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
 #endif
   if (a.fin != nullptr) {
-    if (tid < 64) multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, a.out);
+    if (tid < 64) multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, n, a.out);
   } else if (tid == 0) {
     const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
     a.partials[2 * blk] = conf_l;
@@ -1111,11 +1221,189 @@ int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const in
   SBOD_LAUNCHED("k_loss_final");
   return SBOD_OK;
 }
+// The one-launch criterion's workspace: [done, status | arrivals [B] | matcher workspace (keys
+// first) | loss workspace (the finish's accumulators first) | forced lists [B][Gmax] | their
+// counts [B]].  Everything up to the end of the finish's accumulators must be zero on entry and
+// is left zero by every successful call (zero_bytes); the matcher and loss workspaces are also
+// what the two-launch form of the same call uses.
+struct CritWs {
+  unsigned long long *done, *arrive, *forced;
+  unsigned *status;
+  int32_t *nforced;
+  char *match_ws, *loss_ws;
+  size_t match_bytes, loss_bytes, zero_bytes, bytes;
+};
+CritWs carve_crit(void *w, int B, int Gmax, int P) {
+  CritWs r;
+  r.done = ws_at<unsigned long long>(w, 0);
+  r.status = ws_at<unsigned>(w, 8);
+  size_t o = 256;
+  r.arrive = ws_at<unsigned long long>(w, o);
+  o += align_up(static_cast<size_t>(B) * 8);
+  r.match_ws = ws_at<char>(w, o);
+  r.match_bytes = sbod_match_workspace_bytes_p(B, Gmax, P);
+  o += align_up(r.match_bytes);
+  r.loss_ws = ws_at<char>(w, o);
+  r.loss_bytes = carve(nullptr, B, P).bytes;
+  r.zero_bytes = o + kFinBytes;
+  o += align_up(r.loss_bytes);
+  r.forced = ws_at<unsigned long long>(w, o);
+  o += align_up(static_cast<size_t>(B) * Gmax * 8);
+  r.nforced = ws_at<int32_t>(w, o);
+  o += align_up(static_cast<size_t>(B) * 4);
+  r.bytes = o;
+  return r;
+}
+
+// Workgroups of `kernel` (kLTile threads, `lds` dynamic bytes) resident at once on the current
+// device: the occupancy query times the CU count, cached per (device, kernel, lds).  The
+// one-launch criterion needs its whole grid resident (its workgroups wait for each other).  The
+// query ignores the SGPR file: 256-thread blocks are admitted per CU up to
+// floor(800 / (ceil(sgpr / 16) * 16 + 16)) (MI355X_MICROARCH.md, residency), which is 6 for the
+// k_multibox<..., true> instantiations (TotalSGPRs <= 112 in the build's resource table;
+// tests/test_cpu_host.py checks it), so the count per CU is capped at kCritBlocksPerCU.
+constexpr int kCritBlocksPerCU = 6;
+int resident_capacity(const void *kernel, size_t lds) {
+  struct Entry { int dev; const void *k; size_t lds; int cap; };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> g(mu);
+  for (const Entry &e : cache)
+    if (e.dev == dev && e.k == kernel && e.lds == lds) return e.cap;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kLTile, lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = cus = 0;
+  }
+  if (per_cu > kCritBlocksPerCU) per_cu = kCritBlocksPerCU;
+  cache.push_back(Entry{dev, kernel, lds, per_cu * cus});
+  return per_cu * cus;
+}
 }  // namespace
 
 extern "C" {
 
 size_t sbod_loss_workspace_bytes(int B, int P) { return carve(nullptr, B, P).bytes; }
+
+size_t sbod_criterion_workspace_bytes(int B, int Gmax, int P) {
+  return carve_crit(nullptr, B > 0 ? B : 1, Gmax > 0 ? Gmax : 1, P > 0 ? P : 1).bytes;
+}
+size_t sbod_criterion_zero_bytes(int B, int Gmax, int P) {
+  return carve_crit(nullptr, B > 0 ? B : 1, Gmax > 0 ? Gmax : 1, P > 0 ? P : 1).zero_bytes;
+}
+
+int sbod_criterion_focal(const void *locs, const void *scores, int dtype, int B, int P, int C,
+                         const float *priors_cxcy, const float *priors_xy, const float *gt_boxes,
+                         const int64_t *gt_labels, const int32_t *gt_offsets, int Gmax, float threshold,
+                         float neg_threshold, int reg, int flags, float reg_weight, float focal_alpha,
+                         float focal_gamma, int32_t *obj, float *ovl, int32_t *n_pos, void *grad_locs,
+                         void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
+                         void *stream) {
+  SBOD_REQUIRE(B > 0 && P > 0 && C >= 2 && Gmax > 0 && locs && scores && priors_cxcy && priors_xy && gt_boxes &&
+                   gt_labels && gt_offsets && obj && ovl && n_pos && loss_out,
+               "sbod_criterion_focal: bad arguments (B=%d P=%d C=%d Gmax=%d)", B, P, C, Gmax);
+  SBOD_REQUIRE(dtype == SBOD_DT_F32 || dtype == SBOD_DT_BF16, "sbod_criterion_focal: dtype %d", dtype);
+  SBOD_REQUIRE(reg >= 0 && reg <= 2, "sbod_criterion_focal: reg %d", reg);
+  SBOD_REQUIRE(Gmax <= 4096, "sbod_criterion_focal: Gmax %d > 4096 unsupported", Gmax);
+  SBOD_REQUIRE(C * kLTile * 4 <= 160 * 1024, "sbod_criterion_focal: C=%d too large for one LDS tile", C);
+  SBOD_REQUIRE((flags & ~(SBOD_LOSS_FOCAL_NORM | SBOD_CRIT_WS_ZEROED | SBOD_CRIT_TWO_LAUNCH |
+                          SBOD_LOSS_UNFUSED_FINISH)) == 0,
+               "sbod_criterion_focal: unknown flags 0x%x", flags);
+  const CritWs ws = carve_crit(workspace, B, Gmax, P);
+  if (workspace_bytes < ws.bytes) {
+    set_error("sbod_criterion_focal: workspace %zu < %zu", workspace_bytes, ws.bytes);
+    return SBOD_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if ((flags & SBOD_CRIT_WS_ZEROED) == 0 && hipMemsetAsync(workspace, 0, ws.zero_bytes, s) != hipSuccess)
+    return launch_status("hipMemsetAsync(criterion)");
+  const int lflags = flags & (SBOD_LOSS_FOCAL_NORM | SBOD_LOSS_UNFUSED_FINISH);
+  const dim3 grid((P + kLTile - 1) / kLTile, B);
+  const size_t nblk = static_cast<size_t>(grid.x) * B;
+  // the tile's rows (+ 8 floats, as k_multibox), the match phase's key rows, and the forced
+  // match's LDS form beyond 64 objects: one dynamic region, used in turn
+  size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
+  const size_t keys_lds = (kLTile / 64) * kSlots * (64 + 1) * sizeof(uint32_t);
+  if (lds < keys_lds) lds = keys_lds;
+  if (Gmax > 64 && lds < static_cast<size_t>(Gmax) * 24) lds = static_cast<size_t>(Gmax) * 24;
+  const void *kfused = nullptr;
+#define SBOD_CRIT_K(T, CM) kfused = reinterpret_cast<const void *>(&k_multibox<T, CM, SBOD_CLS_FOCAL, true>)
+#define SBOD_CRIT_C(T)                 \
+  do {                                 \
+    if (C <= 8) SBOD_CRIT_K(T, 8);     \
+    else if (C <= 16) SBOD_CRIT_K(T, 16); \
+    else if (C <= 24) SBOD_CRIT_K(T, 24); \
+    else if (C <= 32) SBOD_CRIT_K(T, 32); \
+    else SBOD_CRIT_K(T, 0);            \
+  } while (0)
+  if (dtype == SBOD_DT_F32) SBOD_CRIT_C(float);
+  else SBOD_CRIT_C(uint16_t);
+#undef SBOD_CRIT_C
+#undef SBOD_CRIT_K
+  const bool one = (flags & (SBOD_CRIT_TWO_LAUNCH | SBOD_LOSS_UNFUSED_FINISH)) == 0 &&
+                   nblk <= static_cast<size_t>(resident_capacity(kfused, lds));
+  if (!one) {   // the two-launch form on the same workspace (both parts are zero on entry)
+    const int st = sbod_match_f32(gt_boxes, gt_labels, gt_offsets, B, Gmax, priors_xy, nullptr, nullptr, P, threshold,
+                                  0.01f, SBOD_MATCH_WS_ZEROED, obj, ovl, n_pos, ws.match_ws, ws.match_bytes, stream);
+    if (st != SBOD_OK) return st;
+    return sbod_multibox_loss(locs, scores, dtype, B, P, C, priors_cxcy, nullptr, nullptr, gt_boxes, gt_labels,
+                              gt_offsets, obj, ovl, n_pos, n_pos + B, threshold, neg_threshold, 0.01f, reg,
+                              SBOD_CLS_FOCAL, lflags | SBOD_LOSS_WS_ZEROED, 3, reg_weight, focal_alpha, focal_gamma,
+                              grad_locs, grad_scores, loss_out, ws.loss_ws, ws.loss_bytes, stream);
+  }
+  const LossWs lw = carve(ws.loss_ws, B, P);
+  LossArgs a{B, P, C, priors_cxcy, nullptr, nullptr, gt_boxes, gt_labels, gt_offsets, nullptr, nullptr, nullptr,
+             threshold, neg_threshold, 0.01f, reg, SBOD_CLS_FOCAL, lflags, reg_weight, focal_alpha,
+             1.f - focal_alpha, focal_gamma, lw.partials, lw.pool, nullptr, lw.fin, loss_out};
+  a.anchors = priors_xy;
+  a.Gmax = Gmax;
+  a.obj_out = obj;
+  a.ovl_out = ovl;
+  a.npos_out = n_pos;
+  a.keys = reinterpret_cast<unsigned long long *>(ws.match_ws);   // the matcher workspace's keys
+  a.arrive = ws.arrive;
+  a.done = ws.done;
+  a.status = ws.status;
+  a.forced = ws.forced;
+  a.nforced = ws.nforced;
+  {
+    KernelTimer kt("k_criterion", s, true);
+    a.span = kt.span();
+#define SBOD_CRIT(T, CM)                                                                                  \
+  tlaunch(kt, (k_multibox<T, CM, SBOD_CLS_FOCAL, true>), grid, dim3(kLTile), lds, s, a,                  \
+          static_cast<const T *>(locs), static_cast<const T *>(scores), static_cast<T *>(grad_locs),      \
+          static_cast<T *>(grad_scores))
+#define SBOD_CRIT_C(T)                 \
+  do {                                 \
+    if (C <= 8) SBOD_CRIT(T, 8);       \
+    else if (C <= 16) SBOD_CRIT(T, 16); \
+    else if (C <= 24) SBOD_CRIT(T, 24); \
+    else if (C <= 32) SBOD_CRIT(T, 32); \
+    else SBOD_CRIT(T, 0);              \
+  } while (0)
+    if (dtype == SBOD_DT_F32) SBOD_CRIT_C(float);
+    else SBOD_CRIT_C(uint16_t);
+#undef SBOD_CRIT_C
+#undef SBOD_CRIT
+  }
+  SBOD_LAUNCHED("k_criterion");
+  return SBOD_OK;
+}
+
+int sbod_criterion_status(const void *workspace, void *stream) {
+  // diagnostics: the one-launch criterion's wait-timeout word (nonzero: a wait gave up), read
+  // with a stream synchronisation
+  SBOD_REQUIRE(workspace != nullptr, "sbod_criterion_status: null workspace");
+  unsigned v = 0;
+  hipStream_t s = as_stream(stream);
+  if (hipMemcpyAsync(&v, static_cast<const char *>(workspace) + 8, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return launch_status("sbod_criterion_status");
+  return static_cast<int>(v);
+}
 
 int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, int P, int C,
                        const float *priors_cxcy, const float *odm_arm_locs,
@@ -1161,7 +1449,7 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
     KernelTimer kt("k_multibox", s, true);
     a.span = kt.span();
 #define SBOD_MB(T, CM, CLS)                                                                       \
-  tlaunch(kt, (k_multibox<T, CM, CLS>), grid, dim3(kLTile), lds, s, a, static_cast<const T *>(locs), \
+  tlaunch(kt, (k_multibox<T, CM, CLS, false>), grid, dim3(kLTile), lds, s, a, static_cast<const T *>(locs), \
                      static_cast<const T *>(scores), static_cast<T *>(grad_locs), static_cast<T *>(grad_scores))
     // rows of C <= CM classes in registers; wider rows take the LDS path
 #define SBOD_MB_C(T)                                                  \

@@ -8,14 +8,13 @@
 //
 // Roofline: HBM-bound.  Algorithmic bytes per launch (matcher alone) = 16*P (priors once) +
 // B*P*8 (obj + ovl written); ~17*G flops per prior-image.
-#include "sbod_common.h"
+#include "match_dev.h"
 
 namespace sbod {
 
 SBOD_STAMP_DECL
 
 constexpr int kTile = 256;
-constexpr int kMThreads = 256;   // k_match_tile: one prior per thread
 
 struct GtTile {
   float x1, y1, x2, y2, area;
@@ -53,27 +52,6 @@ __device__ __forceinline__ void load_gt_tile(GtTile *s, const float *gt, int g0,
   }
 }
 
-struct Anchor {
-  float x1, y1, x2, y2, area;
-  bool zero;
-};
-
-template <bool kOdm>
-__device__ __forceinline__ Anchor make_anchor(Box4 raw, Box4 prior) {
-  Box4 a = raw;
-  if constexpr (kOdm) a = decode_tenfive_xy(raw, prior);
-  float ax = a.c - a.a, ay = a.d - a.b;
-  return Anchor{a.a, a.b, a.c, a.d, ax * ay, (ax < kIouEps) && (ay < kIouEps)};
-}
-
-template <bool kOdm>
-__device__ __forceinline__ Anchor load_anchor(const float *anchors, const float *priors, int b,
-                                              int P, int p) {
-  if constexpr (kOdm)
-    return make_anchor<true>(ld4(anchors + 4 * (static_cast<int64_t>(b) * P + p)), ld4(priors + 4 * p));
-  return make_anchor<false>(ld4(anchors + 4 * static_cast<int64_t>(p)), Box4{0.f, 0.f, 0.f, 0.f});
-}
-
 // Matching in two launches.
 //
 // k_match_tile (B x ceil(P / 256) workgroups of four INDEPENDENT waves, one prior per lane: no
@@ -104,43 +82,6 @@ __device__ __forceinline__ Anchor load_anchor(const float *anchors, const float 
 // (Round 2's form — a per-tile LDS table of overlaps reduced per (tile, object) into 16-byte
 // records, block barriers around it — spent ≈10-12 µs per launch at SSD512 B=32, most of it in
 // the barriers and the LDS table)
-constexpr int kKeyShards = 8;   // copies of the per-object key words (one per XCD-sized group of tiles)
-constexpr int kSlots = 16;      // per-wave LDS rows of pending per-object ords
-
-// Max of a u64 over each quad of lanes, valid in every lane of the quad (DPP quad swaps; keys are
-// unique, so the max is the quad's best).
-template <int kCtrl>
-__device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) {
-  const uint32_t lo = dpp_u32<kCtrl, 0xf>(static_cast<uint32_t>(v));
-  const uint32_t hi = dpp_u32<kCtrl, 0xf>(static_cast<uint32_t>(v >> 32));
-  const unsigned long long o = (static_cast<unsigned long long>(hi) << 32) | lo;
-  return o > v ? o : v;
-}
-__device__ __forceinline__ unsigned long long quad_max_u64(unsigned long long v) {
-  v = dpp_max_u64<0xB1>(v);        // quad_perm [1,0,3,2]
-  return dpp_max_u64<0x4E>(v);     // quad_perm [2,3,0,1]
-}
-
-struct GtLane {   // lane j of a chunk: object j
-  float x1, y1, x2, y2, area;
-  int zero, lab;
-};
-
-template <int kFlags>
-__device__ __forceinline__ GtLane load_gt_lane(const float *__restrict__ gt, const int64_t *__restrict__ labels,
-                                               int g0, int gc, int gn, int lane) {
-  const int j = g0 + gc + min(lane, max(gn - 1, 0));
-  const Box4 bx = ld4(gt + 4 * static_cast<int64_t>(j));
-  const float gx = bx.c - bx.a, gy = bx.d - bx.b;
-  int lab = static_cast<int32_t>(labels[j]);
-  if ((kFlags & SBOD_MATCH_BINARY) != 0) lab = lab > 0;
-  return GtLane{bx.a, bx.b, bx.c, bx.d, gx * gy, (fabsf(gx) < kIouEps) && (fabsf(gy) < kIouEps), lab};
-}
-
-__device__ __forceinline__ float rl_f(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
 template <bool kOdm, int kFlags>
 __global__ __launch_bounds__(kMThreads) void k_match_tile(
     const float *__restrict__ gt, const int64_t *__restrict__ labels,
@@ -155,142 +96,18 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile(
   span_begin(span);
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   if (blockIdx.x == 0 && b == 0 && tid == 0) npos[B] = 0;   // k_match_final accumulates
-  const int wbase = blockIdx.x * kMThreads + (tid & ~63);
-  const int p = wbase + lane;
-  const bool valid = p < P;
-  // one memory round trip before the object loop: the anchor and the first chunk's objects
-  // (unconditional, clamped loads; an image without objects reads element 0 — the GT buffers
-  // hold at least one)
-  const int pc = min(p, P - 1);
-  const Box4 araw = ld4(kOdm ? anchors + 4 * (static_cast<int64_t>(b) * P + pc) : anchors + 4 * static_cast<int64_t>(pc));
-  const Box4 apri = kOdm ? ld4(priors + 4 * pc) : Box4{0.f, 0.f, 0.f, 0.f};
-  const int g0 = ld_i32_uniform(off + b), G = ld_i32_uniform(off + b + 1) - g0;
-  const bool has = G > 0;
-  GtLane o = load_gt_lane<kFlags>(gt, labels, has ? g0 : 0, 0, has ? min(G, 64) : 1, lane);
-  float eas0 = 0.f, eas1 = 0.f;
-  if constexpr (kOdm) {
-    const int64_t ic = static_cast<int64_t>(b) * P + pc;
-    eas0 = arm_scores[2 * ic];
-    eas1 = arm_scores[2 * ic + 1];
-  }
-  const Anchor a = make_anchor<kOdm>(araw, apri);
-  // the wave's prior bounding box as monotone integer keys
-  const bool live = valid && !a.zero;
-  const uint32_t wx1 = ~wave_max_u32(live ? ~f2ord(a.x1) : 0u), wy1 = ~wave_max_u32(live ? ~f2ord(a.y1) : 0u);
-  const uint32_t wx2 = wave_max_u32(live ? f2ord(a.x2) : 0u), wy2 = wave_max_u32(live ? f2ord(a.y2) : 0u);
-  const bool wlive = __ballot(live) != 0ull;
-  float best = 0.f;
-  int bi = 0, blab = 0;
+  const int wbase = blockIdx.x * kMThreads + (tid & ~63), wv = tid >> 6;
   // this workgroup's shard of the image's keys (kKeyShards copies: the waves of one image spread
   // their atomics over kKeyShards words per object instead of queueing on one)
   unsigned long long *brow = best_key + (static_cast<int64_t>(b) * kKeyShards + (blockIdx.x & (kKeyShards - 1))) * Gmax;
-  // metrics.py:224-250, in the reference's order: this lane's overlap with chunk object j
-  auto iou_of = [&](int j, int &glab) {
-    const float tx1 = rl_f(o.x1, j), ty1 = rl_f(o.y1, j), tx2 = rl_f(o.x2, j), ty2 = rl_f(o.y2, j);
-    const float garea = rl_f(o.area, j);
-    const int gzero = __builtin_amdgcn_readlane(o.zero, j);
-    glab = __builtin_amdgcn_readlane(o.lab, j);
-    float iw = fminf(tx2, a.x2) - fmaxf(tx1, a.x1);
-    if (iw < 0.f) iw = 0.f;
-    float ih = fminf(ty2, a.y2) - fmaxf(ty1, a.y1);
-    if (ih < 0.f) ih = 0.f;
-    const float inner = iw * ih;
-    float ov = inner / (((garea + a.area) - inner) + kIouEps);
-    if (gzero) ov = 0.f;
-    if (a.zero) ov = -1.f;
-    return ov;
-  };
-  // Per-object keys: an object with a positive overlap in this wave leaves its lanes' ords in
-  // one of the wave's kSlots LDS rows (one ds_write, no cross-lane work in the object loop);
-  // flush_keys reduces all filled rows at once — lane = (row, 16-lane segment): the segment's
-  // max ord and lowest lane holding it, then the max over the row's 4 segments (DPP) — and
-  // folds each row's key into the object's word with one atomic.  Rows are wave-private: no
-  // block barrier, only the wave's own LDS order.
-  const int wv = tid >> 6;
-  int nslot = 0;
-  auto flush_keys = [&]() {
-    if (nslot == 0) return;
-    __builtin_amdgcn_wave_barrier();
-    const int j = lane >> 2, q = lane & 3;
-    unsigned long long key = 0ull;
-    if (j < nslot) {
-      const uint4 *row = reinterpret_cast<const uint4 *>(&s_od[wv][j][16 * q]);
-      uint32_t v[16];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint4 x = row[r];
-        v[4 * r] = x.x;
-        v[4 * r + 1] = x.y;
-        v[4 * r + 2] = x.z;
-        v[4 * r + 3] = x.w;
-      }
-      uint32_t mx = v[0];
-#pragma unroll
-      for (int c = 1; c < 16; ++c) mx = max(mx, v[c]);
-      int c0 = 15;
-#pragma unroll
-      for (int c = 14; c >= 0; --c) c0 = v[c] == mx ? c : c0;
-      key = mx ? ((static_cast<unsigned long long>(mx) << 32) |
-                  (0xffffffffull - static_cast<uint32_t>(wbase + 16 * q + c0)))
-               : 0ull;
-    }
-    key = quad_max_u64(key);
-    if (q == 0 && j < nslot && key)
-      __hip_atomic_fetch_max(brow + s_slot[wv][j], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_wave_barrier();
-    nslot = 0;
-  };
-  auto note_key = [&](int g, float ov) {
-    const uint32_t od = (valid && ov > 0.f) ? f2ord(ov) : 0u;
-    if (__ballot(od != 0u) == 0ull) return;   // no positive overlap here: never this wave's key
-    s_od[wv][nslot][lane] = od;
-    if (lane == 0) s_slot[wv][nslot] = g;
-    if (++nslot == kSlots) flush_keys();
-  };
-  for (int gc = 0; gc < G; gc += 64) {
-    const int gn = min(G - gc, 64);
-    if (gc > 0) o = load_gt_lane<kFlags>(gt, labels, g0, gc, gn, lane);
-    // objects of this chunk whose box meets the wave's prior box (object 0 always: it sets
-    // every prior's first best, ties included)
-    const bool hit = wlive && lane < gn && f2ord(o.x2) > wx1 && f2ord(o.x1) < wx2 && f2ord(o.y2) > wy1 &&
-                     f2ord(o.y1) < wy2;
-    unsigned long long todo = __ballot(hit) | (gc == 0 ? 1ull : 0ull);
-    // two objects per step (independent IoU chains), applied in object order
-    while (todo) {
-      const int j1 = __builtin_ctzll(todo);
-      todo &= todo - 1ull;
-      const bool two = todo != 0ull;
-      const int j2 = two ? __builtin_ctzll(todo) : j1;
-      if (two) todo &= todo - 1ull;
-      int lab1, lab2;
-      const float ov1 = iou_of(j1, lab1), ov2 = iou_of(j2, lab2);
-      if (gc + j1 == 0 || ov1 > best) {
-        best = ov1;
-        bi = gc + j1;
-        blab = lab1;
-      }
-      if (two && ov2 > best) {
-        best = ov2;
-        bi = gc + j2;
-        blab = lab2;
-      }
-      note_key(gc + j1, ov1);
-      if (two) note_key(gc + j2, ov2);
-    }
+  const MatchLane m = match_wave<kOdm, kFlags>(gt, labels, off, anchors, priors, arm_scores, P, b, wbase, brow,
+                                               s_od[wv], s_slot[wv]);
+  if (m.valid) {
+    const int64_t i = static_cast<int64_t>(b) * P + m.p;
+    obj[i] = m.bi;
+    ovl[i] = m.best;
   }
-  flush_keys();
-  bool pos = false;
-  if (valid) {
-    const int64_t i = static_cast<int64_t>(b) * P + p;
-    obj[i] = bi;
-    ovl[i] = best;
-    pos = !(best < thr) && blab > 0;
-    if constexpr (kOdm) {
-      const float m = fmaxf(eas0, eas1);
-      const float e0 = expf(eas0 - m), e1 = expf(eas1 - m);
-      if (e1 / (e0 + e1) < theta) pos = false;
-    }
-  }
+  const bool pos = phase1_positive<kOdm>(m, thr, theta);
   // the wave's positive count, one plain store per wave (summed by k_match_final)
   const int n = __popcll(__ballot(pos));
   if (lane == 0) wcnt[static_cast<int64_t>(b) * (gridDim.x * (kMThreads / 64)) + (wbase >> 6)] = n;
@@ -310,154 +127,10 @@ __global__ __launch_bounds__(kFThreads) void k_match_final(
     float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   __shared__ int s_red[16];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   STAMP_BEGIN();
-  const int g0 = off[b], G = off[b + 1] - g0;
-  unsigned long long *brow = best_key + static_cast<int64_t>(b) * kKeyShards * Gmax;
-  // the phase-1 positive count: the image's per-wave counts (first wave only; the LDS form
-  // shares it through s_red)
-  int cnt1 = 0;
-  if (tid < 64) {
-    for (int w = lane; w < nw; w += 64) {
-      int32_t *c = wcnt + static_cast<int64_t>(b) * nw + w;
-      cnt1 += *c;
-      *c = 0;   // the whole workspace is zero again after a call (any B, Gmax, P next time)
-    }
-    cnt1 = wave_sum_i32(cnt1);
-  }
-  // an object's key: the max over its shards, which return to zero
-  auto take_key = [&](int g) {
-    unsigned long long k = 0ull;
-#pragma unroll
-    for (int s = 0; s < kKeyShards; ++s) {
-      const unsigned long long v = brow[s * Gmax + g];
-      k = v > k ? v : k;
-    }
-#pragma unroll
-    for (int s = 0; s < kKeyShards; ++s) brow[s * Gmax + g] = 0ull;
-    return k;
-  };
-  auto lab_of = [&](int g) {
-    int l = static_cast<int32_t>(labels[g0 + g]);
-    if ((kFlags & SBOD_MATCH_BINARY) != 0) l = l > 0;
-    return l;
-  };
-  auto easy_of = [&](int p) {
-    int easy = 0;
-    if constexpr ((kFlags & SBOD_MATCH_ODM) != 0) {
-      const int64_t i = static_cast<int64_t>(b) * P + p;
-      const float z0 = arm_scores[2 * i], z1 = arm_scores[2 * i + 1];
-      const float m = fmaxf(z0, z1);
-      const float e0 = expf(z0 - m), e1 = expf(z1 - m);
-      easy = e1 / (e0 + e1) < theta;
-    }
-    return easy;
-  };
-  // is_pos(label, overlap, easy): the positive rule of the criteria
-  auto is_pos = [&](int lab, float v, int easy) { return !(v < thr) && lab > 0 && !easy; };
-  auto publish = [&](int delta) {   // one lane
-    const int nb = cnt1 + delta;
-    npos[b] = nb;
-    atomicAdd(npos + B, nb);
-  };
-  if (G <= 64) {
-    if (tid >= 64) return;
-    // lane = object: its best key, the key's prior and that prior's phase-1 (obj, ovl)
-    const unsigned long long k = lane < G ? take_key(lane) : 0ull;
-    const int lab = lane < G ? lab_of(lane) : 0;
-    const int p = k ? static_cast<int>(0xffffffffu - static_cast<uint32_t>(k)) : -1;
-    const int64_t ip = static_cast<int64_t>(b) * P + (p >= 0 ? p : 0);
-    const int o_ph1 = obj[ip];
-    const float v_ph1 = ovl[ip];
-    const int easy = p >= 0 ? easy_of(p) : 0;
-    const unsigned long long valid = __ballot(p >= 0);
-    const int j = __popcll(valid & ((1ull << lane) - 1ull));   // filtered position
-    int prev = -1;      // the previous writer of the same prior
-    bool lastw = true;  // no later writer of the same prior
-    for (int h = 0; h < G; ++h) {
-      const int ph = __builtin_amdgcn_readlane(p, h);
-      if (p >= 0 && ph == p) {
-        if (h < lane) prev = h;
-        if (h > lane) lastw = false;
-      }
-    }
-    const int jprev = __shfl(j, prev < 0 ? lane : prev, 64);
-    const int o_old = prev >= 0 ? jprev : o_ph1;
-    const float v_old = prev >= 0 ? 1.0f : v_ph1;
-    // labels of the new object j and the old object, read from the lanes that hold them
-    const int lab_new = __shfl(lab, j & 63, 64), lab_old = __shfl(lab, o_old & 63, 64);
-    int d = 0;
-    if (p >= 0) {
-      d = (is_pos(lab_new, 1.0f, easy) ? 1 : 0) - (is_pos(lab_old, v_old, easy) ? 1 : 0);
-      if (lastw) {
-        obj[ip] = j;
-        ovl[ip] = 1.0f;
-      }
-    }
-    const int delta = wave_sum_i32(d);
-    if (lane == 0) publish(delta);
-    STAMP_END(7, 0);
-    return;
-  }
-  // more objects: the LDS form of the same rules.  LDS per object: prior, easy | previous writer,
-  // label, final object, phase-1 (obj, ovl)
-  int32_t *s_pr = reinterpret_cast<int32_t *>(s_dyn);
-  int32_t *s_easy = s_pr + Gmax;
-  int32_t *s_lab = s_easy + Gmax;
-  int32_t *s_new = s_lab + Gmax;
-  int32_t *s_o0 = s_new + Gmax;
-  float *s_v0 = reinterpret_cast<float *>(s_o0 + Gmax);
-  if (tid == 0) s_red[15] = cnt1;
-  for (int g = tid; g < G; g += blockDim.x) {
-    const unsigned long long k = take_key(g);
-    const int p = k ? static_cast<int>(0xffffffffu - static_cast<uint32_t>(k)) : -1;
-    s_pr[g] = p;
-    s_lab[g] = lab_of(g);
-    if (p >= 0) {
-      const int64_t i = static_cast<int64_t>(b) * P + p;
-      s_o0[g] = obj[i];
-      s_v0[g] = ovl[i];
-    }
-    s_easy[g] = p >= 0 ? easy_of(p) : 0;
-  }
-  __syncthreads();
-  cnt1 = s_red[15];
-  for (int g = tid; g < G; g += blockDim.x) {
-    int j = 0, prev = -1;
-    const int p = s_pr[g];
-    for (int h = 0; h < g; ++h) {
-      const int ph = s_pr[h];
-      if (ph >= 0) {
-        ++j;
-        if (ph == p) prev = h;
-      }
-    }
-    s_new[g] = p >= 0 ? j : -1;
-    s_easy[g] = p >= 0 ? ((s_easy[g] & 1) | (prev >= 0 ? ((prev + 1) << 1) : 0)) : 0;
-  }
-  __syncthreads();
-  int delta = 0;
-  for (int g = tid; g < G; g += blockDim.x) {
-    if (s_pr[g] < 0) continue;
-    const int easy = s_easy[g] & 1, prev = (s_easy[g] >> 1) - 1;
-    const int o_old = prev >= 0 ? s_new[prev] : s_o0[g];
-    const float v_old = prev >= 0 ? 1.0f : s_v0[g];
-    delta += (is_pos(s_lab[s_new[g]], 1.0f, easy) ? 1 : 0) - (is_pos(s_lab[o_old], v_old, easy) ? 1 : 0);
-  }
-  delta = block_sum(delta, s_red);
-  for (int g = tid; g < G; g += blockDim.x) {
-    const int p = s_pr[g];
-    if (p < 0) continue;
-    bool lastw = true;   // superseded by a later writer?
-    for (int h = g + 1; h < G && lastw; ++h)
-      if (s_pr[h] == p) lastw = false;
-    if (!lastw) continue;
-    const int64_t i = static_cast<int64_t>(b) * P + p;
-    obj[i] = s_new[g];
-    ovl[i] = 1.0f;
-  }
-  if (tid == 0) publish(delta);
-  STAMP_END(7, 1);
+  match_final_image<kFlags, false>(blockIdx.x, labels, off, best_key, wcnt, nw, Gmax, P, thr, arm_scores, theta,
+                                   obj, ovl, npos, B, 0, ForcedOut{nullptr, nullptr, nullptr}, s_dyn, s_red);
+  STAMP_END(7, 0);
 }
 
 // Pairwise IoU matrix out[b, g, p].

@@ -295,6 +295,10 @@ __device__ __forceinline__ void st_wt_u32(int32_t *p, uint32_t v) {
 __device__ __forceinline__ uint32_t ld_wt_u32(const int32_t *p) {
   return __hip_atomic_load((gu32 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Wait for every outstanding vector-memory operation of the calling wave (stores acknowledged,
+// atomics performed) with a compiler memory barrier: no memory access moves across it (a bare
+// __builtin_amdgcn_s_waitcnt is not a compiler barrier).
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kCpolSc1 = 16;   // gfx950 cache-policy bit SC1 in the buffer intrinsics' aux word
 // 16 bytes written through at byte offset `off` of the wave-uniform region [base, base + bytes).

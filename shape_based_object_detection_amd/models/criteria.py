@@ -56,6 +56,7 @@ class _AnchorCriterion(nn.Module):
         self.process_group = None
         self.grad_reduction = 'mean'
         self.force_collectives = False   # run the collectives even in a one-rank group (tests)
+        self.two_launch = False          # focal on one device: matcher and loss as two launches (A/B)
         self.last_components = None
 
     def increase_threshold(self, increment=0.1):
@@ -100,10 +101,17 @@ class _AnchorCriterion(nn.Module):
                                              _cfg(self.config, 'cls_loss', 'ce'), self.threshold,
                                              self.neg_pos_ratio, self.alpha)
         gt = core.pack_gt(boxes, labels)
+        spec = self._spec()
+        if spec.cls == L.CLS['focal'] and not self.distributed:
+            # one device, no mining: the matcher, the normaliser and the loss pass in one launch
+            loss, comps, _ = core.criterion_focal(predicted_locs, predicted_scores, gt, self.priors_cxcy,
+                                                  self.priors_xy, spec, self.threshold, self.threshold - 0.1,
+                                                  two_launch=self.two_launch)
+            self.last_components = comps
+            return loss
         obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold)
         tot = (core.allreduce_npos(npos, self.process_group, self.force_collectives)
                if self.distributed else npos[B:])
-        spec = self._spec()
         # SSD300's CE mines over the whole batch: data-parallel, the pools are exchanged
         exchange = (core.allgather_pool(self.process_group)
                     if self.distributed and (spec.flags & L.POOL['global_neg']) else None)

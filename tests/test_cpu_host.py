@@ -127,6 +127,25 @@ def test_no_kernel_spills_to_scratch():
     assert bad == {}, bad
 
 
+def test_one_launch_criterion_residency_cap():
+    """The one-launch criterion's grid must be resident at once; the library caps its occupancy
+    query at 6 blocks per CU (loss.hip kCritBlocksPerCU), which holds while the kernels need at
+    most 112 SGPRs: 256-thread blocks per CU <= floor(800 / (ceil(sgpr / 16) * 16 + 16))
+    (MI355X_MICROARCH.md, residency).  A code change that raises the SGPR count past that fails
+    here instead of as an in-launch wait timeout on the GPU."""
+    import json
+    path = os.path.join(REPO, 'shape_based_object_detection_amd', 'lib', 'kernel_resources.json')
+    if not os.path.exists(path):
+        pytest.skip('library not built with resource remarks')
+    usage = json.load(open(path))
+    fused = {k: v for k, v in usage.items() if 'k_multibox' in k and 'Lb1E' in k}
+    assert len(fused) == 10, sorted(fused)
+    for k, v in fused.items():
+        sg = v['TotalSGPRs']
+        assert 800 // ((sg + 15) // 16 * 16 + 16) >= 6, (k, sg)
+        assert v['ScratchSize'] == 0
+
+
 def test_stress_anchor_generator_size():
     # SURVEY §8 C3 stress size: RetinaNet's generator on 896x896 maps
     assert prior_table('RETINA896').shape == (100254, 4)
