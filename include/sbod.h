@@ -320,9 +320,13 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
  *   SBOD_DETECT_INPUT_BF16 — locs and scores hold bf16 (C <= 32): each value is widened to fp32
  *   exactly on load, so the results equal those of the fp32 call on the widened tensors (no
  *   widened copies in HBM).  Without it both are fp32.
+ *   Without a final NMS (window 0, C <= 64) the per-class NMS and the per-image merge run as ONE
+ *   launch (the image's last class merges) and an image its first window of 64 candidates per
+ *   class cannot decide reports det_count -1 (re-run it with a wider window); SBOD_DETECT_TWO_PASS
+ *   keeps them two launches with the wider second window run inline (diagnostics, A/B).
  * Workspace: sbod_detect_workspace_bytes(B, P, C). */
 enum { SBOD_BOX_OFFSET = 0, SBOD_BOX_CENTER = 1, SBOD_BOX_CORNER = 2 };
-enum { SBOD_DETECT_COUNTERS_ZEROED = 1, SBOD_DETECT_INPUT_BF16 = 2 };
+enum { SBOD_DETECT_COUNTERS_ZEROED = 1, SBOD_DETECT_INPUT_BF16 = 2, SBOD_DETECT_TWO_PASS = 4 };
 size_t sbod_detect_counter_bytes(int B, int C);
 enum { SBOD_ACT_SOFTMAX = 0, SBOD_ACT_SIGMOID = 1 };
 size_t sbod_detect_workspace_bytes(int B, int P, int C);

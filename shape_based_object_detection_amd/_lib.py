@@ -94,7 +94,7 @@ FOCAL = dict(softmax=0, sigmoid=1, bce=2)
 BOX = dict(offset=0, center=1, corner=2)
 ACT = dict(softmax=0, sigmoid=1)
 NMS = dict(tv=0, ref=1, diou=2)
-DETECT_COUNTERS_ZEROED, DETECT_INPUT_BF16 = 1, 2
+DETECT_COUNTERS_ZEROED, DETECT_INPUT_BF16, DETECT_TWO_PASS = 1, 2, 4
 
 
 class SbodError(RuntimeError):

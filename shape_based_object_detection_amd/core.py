@@ -700,13 +700,14 @@ def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overl
 
 def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='offset',
            act='softmax', pos_mask=None, final_nms=None, debug=False, window=0, async_=False,
-           capture=False):
+           capture=False, two_pass=False):
     """Batched decode + per-class NMS + top-k.  Returns (boxes, labels, scores) lists of per-image
     tensors (views of batched device outputs).  ONE host sync: the per-image counts (waited on
     through an event).  ``async_=True`` returns a ``DetectHandle`` instead (``.wait()`` gives the
     lists), so a caller can overlap the detect kernels with later host work.  ``capture=True``
     (inside hipGraph capture) returns a persistent handle: call ``.replayed()`` after each replay,
-    then ``.wait()``."""
+    then ``.wait()``.  ``two_pass`` keeps the per-class NMS and the per-image merge as two launches
+    (with the inline second window) where they would be one (A/B, tests)."""
     L.require_device(locs, scores, what='detect')
     B, P, C = scores.shape
     if top_k <= 0:
@@ -721,6 +722,8 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
         sc = scores.contiguous().float()
         lc = locs if (locs.is_contiguous() and locs.dtype == torch.float32) else locs.contiguous().float()
         in_flags = 0
+    if two_pass:
+        in_flags |= L.DETECT_TWO_PASS
     pri = priors_cxcy.contiguous().float() if priors_cxcy is not None else None
     pm = pos_mask.contiguous().to(torch.uint8) if pos_mask is not None else None
     out_b = torch.empty(B, top_k, 4, dtype=torch.float32, device=dev)

@@ -1186,12 +1186,17 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
 //           box is an LDS broadcast, a ballot assembles each row), then wave 0 sweeps the rows
 //           in rank order from registers (row i in lane i, readlane).
 // Same keys, same rank order, same suppression test: results identical to k_det_segment_wave.
-constexpr int kSegW = 4;                       // waves per segment
-constexpr int kSegWRegKeys = 2048;             // keys held in registers (8 per lane)
+constexpr int kSegWRegKeys = 2048;             // keys held in registers (2048 / (64 W) per lane)
 
-__global__ __launch_bounds__(64 * kSegW) void k_det_segment_w4(
+// The segment work of one (image, class) on W waves (the kernel's whole workgroup), shared by
+// k_det_segment_w4 (W = 4) and the fused k_det_nms (W = 8).  kWT: the outputs (kept keys, kc,
+// lastkey) are written through (sc1) for an in-launch reader.  Waves 1..W-1 return before the
+// sweep (no barrier follows it).
+template <int W, bool kWT>
+__device__ __forceinline__ void segment_w(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
     const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
+  constexpr int kSegW = W;
   constexpr int NT = 64 * kSegW, KR = kSegWRegKeys / NT;
   STAMP_BEGIN();
   __shared__ uint32_t s_hist[256];
@@ -1207,8 +1212,13 @@ __global__ __launch_bounds__(64 * kSegW) void k_det_segment_w4(
   const int n = min(static_cast<int>(cand_count[seg]), P);   // counters never exceed P
   if (n == 0) {
     if (tid == 0) {
-      o.kc[seg] = 0;
-      o.lastkey[seg] = 0;
+      if constexpr (kWT) {
+        st_wt_u32(reinterpret_cast<int32_t *>(o.kc) + seg, 0u);
+        st_wt_u64(o.lastkey + seg, 0ull);
+      } else {
+        o.kc[seg] = 0;
+        o.lastkey[seg] = 0;
+      }
     }
     return;
   }
@@ -1274,7 +1284,7 @@ __global__ __launch_bounds__(64 * kSegW) void k_det_segment_w4(
     for (int hb = top; hb >= 0;) {
       const int lo = hb >= 7 ? hb - 7 : 0, width = hb - lo + 1;
       const unsigned long long dmask = (1ull << width) - 1ull;
-      s_hist[tid] = 0u;
+      if (tid < 256) s_hist[tid] = 0u;
       __syncthreads();
       auto count = [&](unsigned long long k) {
         if (k != 0ull && (hb >= 63 || ((k ^ prefix) >> (hb + 1)) == 0ull))
@@ -1438,12 +1448,21 @@ __global__ __launch_bounds__(64 * kSegW) void k_det_segment_w4(
   long long ph_sweep = clock64();
 #endif
   unsigned long long *ko = o.kept + seg * stride;
-  if ((kept >> lane) & 1ull) ko[__popcll(kept & ((1ull << lane) - 1ull))] = v;
   const uint32_t llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), q - 1);
   const uint32_t lhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), q - 1);
-  if (lane == 0) {
-    o.kc[seg] = __popcll(kept);
-    o.lastkey[seg] = n > q ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
+  const unsigned long long lk = n > q ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
+  if constexpr (kWT) {
+    if ((kept >> lane) & 1ull) st_wt_u64(ko + __popcll(kept & ((1ull << lane) - 1ull)), v);
+    if (lane == 0) {
+      st_wt_u32(reinterpret_cast<int32_t *>(o.kc) + seg, static_cast<uint32_t>(__popcll(kept)));
+      st_wt_u64(o.lastkey + seg, lk);
+    }
+  } else {
+    if ((kept >> lane) & 1ull) ko[__popcll(kept & ((1ull << lane) - 1ull))] = v;
+    if (lane == 0) {
+      o.kc[seg] = __popcll(kept);
+      o.lastkey[seg] = lk;
+    }
   }
   STAMP_END(2, 0);
 #ifdef SBOD_PHASE_CLOCKS
@@ -1453,6 +1472,12 @@ __global__ __launch_bounds__(64 * kSegW) void k_det_segment_w4(
            b, c, n, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph_rows - ph[3], ph_sync - ph_rows, ph_sweep - ph_sync,
            ph[4] - ph_sweep, ph[4] - ph[0]);
 #endif
+}
+
+__global__ __launch_bounds__(256) void k_det_segment_w4(
+    const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
+    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
+  segment_w<4, false>(cand, cand_count, boxes_ws, P, C, window, stride, thr, o);
 }
 
 // ----------------------------------------------------------------------------- K3
@@ -1489,11 +1514,12 @@ __device__ __forceinline__ int count_before(const float *a, int n, float s, bool
 //      the block's threads) — no sort, no radix select, three barriers;
 //   4. entries with rank < top_k are written at their rank.
 // Returns -1 when not applicable (the caller's general merge runs), else the merge status.
+template <bool kWT = false>   // kWT: kept / kc / lastkey were written in this launch (sc1 loads)
 __device__ __forceinline__ int merge_rank(
     const unsigned long long *kept, const uint32_t *kc, const unsigned long long *lastkey,
     const float *__restrict__ boxes_ws, int P, int C, int stride, int wmax, int top_k, int pass,
     int32_t *__restrict__ need, float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
-    float *__restrict__ out_scores, int32_t *__restrict__ out_count) {
+    float *__restrict__ out_scores, int32_t *__restrict__ out_count, int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   __shared__ uint32_t r_off[kRankC + 1], r_kc[kRankC];
   __shared__ unsigned long long r_L;
@@ -1501,7 +1527,7 @@ __device__ __forceinline__ int merge_rank(
   __shared__ int r_m, r_total, r_any;
   const int nslot = (C - 1) * wmax;   // kc <= wmax entries per class (stored at `stride`)
   if (C > kRankC || static_cast<size_t>(nslot) * 20 > static_cast<size_t>(kRankLds) || (nslot & 1)) return -1;
-  const int b = blockIdx.x, tid = threadIdx.x, NT = blockDim.x;
+  const int tid = threadIdx.x, NT = blockDim.x;
   const int64_t sb0 = static_cast<int64_t>(b) * C;
 #ifdef SBOD_PHASE_CLOCKS
   long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1518,7 +1544,8 @@ __device__ __forceinline__ int merge_rank(
 #pragma unroll
       for (int k = 0; k < kB; ++k) {
         const int sidx = min(s0 + k * NT + tid, nslot - 1), cc = sidx / wmax;
-        r[k] = kb[static_cast<int64_t>(cc) * stride + (sidx - cc * wmax)];
+        const unsigned long long *kp = kb + static_cast<int64_t>(cc) * stride + (sidx - cc * wmax);
+        r[k] = kWT ? ld_wt_u64(kp) : *kp;
       }
 #pragma unroll
       for (int k = 0; k < kB; ++k) {
@@ -1534,8 +1561,11 @@ __device__ __forceinline__ int merge_rank(
   if (tid < 64) {
     const int c = tid;
     const bool cv = c >= 1 && c < C;
-    kcv = cv ? kc[sb0 + c] : 0u;
-    const unsigned long long lk = cv ? lastkey[sb0 + c] : 0ull;
+    const int64_t sc = sb0 + (cv ? c : 1);
+    const uint32_t kc0 = kWT ? ld_wt_u32(reinterpret_cast<const int32_t *>(kc) + sc) : kc[sc];
+    const unsigned long long lk0 = kWT ? ld_wt_u64(lastkey + sc) : lastkey[sc];
+    kcv = cv ? kc0 : 0u;
+    const unsigned long long lk = cv ? lk0 : 0ull;
     uint32_t incl = kcv;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1727,7 +1757,7 @@ __device__ __forceinline__ int merge_body(
   if (pass == 2 && need[b] == 0) return 0;
   if (final_nms < 0.f && !general) {
     const int st = merge_rank(kept, kc, lastkey, boxes_ws, P, C, window, wmax, top_k, pass, need, out_boxes,
-                              out_labels, out_scores, out_count);
+                              out_labels, out_scores, out_count, b);
     if (st >= 0) return st;
   }
 #ifdef SBOD_PHASE_CLOCKS
@@ -2018,6 +2048,42 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
   clear_counters();
 }
 
+// ----------------------------------------------------------------------------- K2 + K3 fused
+// The segment pass and the per-image merge in ONE launch (detect without a final NMS, the rank
+// path of the merge): (C - 1) x B workgroups of W waves run segment_w for their (image, class),
+// write the class's kept window through (sc1), drain, and count themselves in at their image; the
+// image's last class runs the merge (merge_rank over sc1 loads of the image's windows), writes the
+// outputs and the host count, and leaves the image's candidate counters and arrival word zero.
+// No workgroup waits for another (the last arriver is told by its own atomic), so the grid needs
+// no co-residency.  An image the first window cannot decide reports -1, exactly as the
+// single-pass merge does (the host re-runs it with a wider window).
+template <int W>
+__global__ __launch_bounds__(64 * W) void k_det_nms(
+    const unsigned long long *__restrict__ cand, uint32_t *cand_count, const float *__restrict__ boxes_ws, int P,
+    int C, int window, int stride, float thr, SegOut o, uint32_t *arrive, int top_k, float *__restrict__ out_boxes,
+    int64_t *__restrict__ out_labels, float *__restrict__ out_scores, int32_t *__restrict__ out_count,
+    int32_t *out_count_host) {
+  __shared__ int s_last;
+  segment_w<W, true>(cand, cand_count, boxes_ws, P, C, window, stride, thr, o);
+  drain_vm();   // this wave's kept keys / kc / lastkey written through
+  __syncthreads();
+  const int b = blockIdx.y;
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(arrive + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == static_cast<uint32_t>(C - 2);
+    if (last) __hip_atomic_store(arrive + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  merge_rank<true>(o.kept, o.kc, o.lastkey, boxes_ws, P, C, stride, window, top_k, 0, nullptr, out_boxes, out_labels,
+                   out_scores, out_count, b);
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) cand_count[static_cast<int64_t>(b) * C + c] = 0u;
+  if (out_count_host != nullptr && threadIdx.x == 0) out_count_host[b] = out_count[b];
+}
+constexpr int kNmsW = 8;   // waves per (image, class) in k_det_nms
+
 // ----------------------------------------------------------------------------- single segment
 template <int V>
 __global__ __launch_bounds__(1024) void k_nms_single(const float *__restrict__ boxes,
@@ -2079,7 +2145,7 @@ namespace {
 struct DetWs {
   float *boxes;
   unsigned long long *cand, *kept, *lastkey, *scratch;
-  uint32_t *count, *kc;
+  uint32_t *count, *kc, *arrive;
   int32_t *need;
   size_t bytes;
 };
@@ -2089,7 +2155,8 @@ DetWs carve_det(void *w, int B, int P, int C, int window) {
   // the candidate counters first: their place depends on B * C only (sbod_detect_f32's
   // SBOD_DETECT_COUNTERS_ZEROED contract)
   r.count = ws_at<uint32_t>(w, o);
-  o += align_up(static_cast<size_t>(B) * C * 4);
+  r.arrive = ws_at<uint32_t>(w, static_cast<size_t>(B) * C * 4);   // [B] after the counters
+  o += align_up(static_cast<size_t>(B) * C * 4 + static_cast<size_t>(B) * 4);
   r.boxes = ws_at<float>(w, o);
   o += align_up(static_cast<size_t>(B) * P * 16);
   r.cand = ws_at<unsigned long long>(w, o);
@@ -2117,7 +2184,9 @@ int clampw(int w, int P) {
 
 extern "C" {
 
-size_t sbod_detect_counter_bytes(int B, int C) { return align_up(static_cast<size_t>(B) * C * 4); }
+size_t sbod_detect_counter_bytes(int B, int C) {
+  return align_up(static_cast<size_t>(B) * C * 4 + static_cast<size_t>(B) * 4);   // counters + arrival words
+}
 
 size_t sbod_detect_workspace_bytes(int B, int P, int C) {
   return carve_det(nullptr, B, P, C, clampw(kMaxWindow, P)).bytes;
@@ -2129,7 +2198,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
                     int flags, float *det_boxes, int64_t *det_labels, float *det_scores,
                     int32_t *det_count, int32_t *det_count_host, float *debug_probs,
                     float *debug_boxes, void *workspace, size_t workspace_bytes, void *stream) {
-  SBOD_REQUIRE((flags & ~(SBOD_DETECT_COUNTERS_ZEROED | SBOD_DETECT_INPUT_BF16)) == 0,
+  SBOD_REQUIRE((flags & ~(SBOD_DETECT_COUNTERS_ZEROED | SBOD_DETECT_INPUT_BF16 | SBOD_DETECT_TWO_PASS)) == 0,
                "sbod_detect_f32: unknown flags 0x%x", flags);
   const bool bf16 = (flags & SBOD_DETECT_INPUT_BF16) != 0;
   SBOD_REQUIRE(!bf16 || C <= 32, "sbod_detect_f32: bf16 input supports C <= 32 (C=%d)", C);
@@ -2169,7 +2238,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
                "sbod_detect_f32: exhaustive mode supports top_k <= 2047");
   hipStream_t s = as_stream(stream);
   if ((flags & SBOD_DETECT_COUNTERS_ZEROED) == 0 &&
-      hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4, s) != hipSuccess)
+      hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4 + static_cast<size_t>(B) * 4, s) != hipSuccess)
     return launch_status("hipMemsetAsync(detect)");
   DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.boxes, ws.cand, ws.count,
             debug_probs, debug_boxes, nullptr};
@@ -2198,6 +2267,21 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
   }
   SBOD_LAUNCHED("k_det_prepare");
   SegOut so{ws.kept, ws.kc, ws.lastkey};
+  // K2 + K3 in one launch (k_det_nms): the rank path of the merge (no final NMS, C <= kRankC, the
+  // first window's kept lists fit its LDS), a first window of <= 64, and the single-pass contract
+  // (an undecidable image reports -1 and the host widens its window)
+  const int rank_slots = (C - 1) * w1;
+  const bool fuse = !exhaustive && final_nms < 0.f && two && w1 <= 64 && C <= kRankC &&
+                    static_cast<size_t>(rank_slots) * 20 <= static_cast<size_t>(kRankLds) && (rank_slots & 1) == 0 &&
+                    (flags & SBOD_DETECT_TWO_PASS) == 0;
+  if (fuse) {
+    KernelTimer kt("k_det_nms", s, true);
+    tlaunch(kt, k_det_nms<kNmsW>, dim3(C - 1, B), dim3(64 * kNmsW), static_cast<size_t>(rank_slots) * 20, s,
+            ws.cand, ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, ws.arrive, top_k, det_boxes, det_labels,
+            det_scores, det_count, det_count_host);
+    SBOD_LAUNCHED("k_det_nms");
+    return SBOD_OK;
+  }
   if (exhaustive) {
     KernelTimer kt("k_det_segment", s, true);
     tlaunch(kt, k_det_segment_all, dim3(C - 1, B), dim3(kAllThreads), all_lds, s, ws.cand, ws.count, ws.boxes, P, C,
@@ -2209,7 +2293,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
       tlaunch(kt, k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, ws.boxes,
                          P, C, w1, w2, max_overlap, so, nullptr);
 #else
-      tlaunch(kt, k_det_segment_w4, dim3(C - 1, B), dim3(64 * kSegW), 0, s, ws.cand, ws.count, ws.boxes,
+      tlaunch(kt, k_det_segment_w4, dim3(C - 1, B), dim3(256), 0, s, ws.cand, ws.count, ws.boxes,
                          P, C, w1, w2, max_overlap, so);
 #endif
     else

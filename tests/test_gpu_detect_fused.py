@@ -1,0 +1,53 @@
+"""detect with the per-class NMS and the per-image merge in ONE launch (k_det_nms: the image's
+last class runs the merge) against the two-launch form (k_det_segment + k_det_merge with its
+inline second window) and the oracle: boxes, labels, scores and counts bit-identical, including
+images whose first 64-candidate windows cannot decide the output (the one-launch form reports
+-1 and the host re-runs the call wider)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import match_ref as M
+from shape_based_object_detection_amd import core, synth
+from shape_based_object_detection_amd.models.priors import prior_table
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.mark.parametrize('B,bg,top_k', [(32, 6.0, 200), (4, 2.0, 50), (3, 9.0, 200), (2, 6.0, 400),
+                                        (5, 0.0, 200), (4, 4.0, 20)])
+def test_one_launch_equals_two_launches(B, bg, top_k):
+    Pn = prior_table('SSD512')
+    P = torch.from_numpy(Pn).to(DEV)
+    locs, scores = synth.make_preds(B, Pn.shape[0], 21, seed=100 + B, bg_shift=bg)
+    l, s = locs.to(DEV), scores.to(DEV)
+    one = core.detect(l, s, 0.01, 0.45, top_k, P)
+    two = core.detect(l, s, 0.01, 0.45, top_k, P, two_pass=True)
+    for a, b in zip(one, two):
+        assert len(a) == len(b) == B
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    if B <= 5:   # and the oracle on the kernels' own activations / decodes
+        (ob, ol, os_), probs, bxs = core.detect(l, s, 0.01, 0.45, top_k, P, debug=True)
+        rb, rl, rs = M.detect(probs.cpu().numpy(), bxs.cpu().numpy(), 0.01, 0.45, top_k, nms_variant='tv')
+        for i in range(B):
+            np.testing.assert_array_equal(ol[i].cpu().numpy(), rl[i])
+            np.testing.assert_array_equal(os_[i].cpu().numpy(), rs[i])
+            np.testing.assert_array_equal(ob[i].cpu().numpy(), rb[i])
+
+
+def test_one_launch_counters_left_zero_and_repeatable():
+    """Repeated calls on the cached workspace (candidate counters and per-image arrival words are
+    left zero by the image's merge) give identical outputs, across batch sizes."""
+    Pn = prior_table('SSD512')
+    P = torch.from_numpy(Pn).to(DEV)
+    locs, scores = synth.make_preds(6, Pn.shape[0], 21, seed=7, bg_shift=6.0)
+    l, s = locs.to(DEV), scores.to(DEV)
+    res = [core.detect(l[:B].contiguous(), s[:B].contiguous(), 0.01, 0.45, 200, P) for B in (6, 3, 6)]
+    for a, b in zip(res[0], res[2]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    for a, b in zip(res[1], res[0]):   # B=3 of the same seed: the first three images
+        for x, y in zip(a, b[:3]):
+            assert torch.equal(x, y)
