@@ -66,6 +66,10 @@ int sbod_timing_every(int n);
 double sbod_timing_clock_hz(void);   /* the span clock (hipDeviceAttributeWallClockRate) */
 int sbod_timing_reset_graphs(void);
 
+/* An empty kernel of `blocks` 64-thread workgroups (profiling calibration: the per-dispatch
+ * cost a profiler adds to every kernel it traces). */
+int sbod_null_kernel(int blocks, void *stream);
+
 /* Asynchronous device -> host copy on `stream` (hipMemcpyAsync; dst_host should be pinned, e.g.
  * torch's pin_memory buffers).  Used for detect's per-image counts (the one value the host needs
  * from a detect call, models/utils.py:274-290); the caller orders its host read after an event

@@ -25,6 +25,7 @@ SIGNATURES = {
     'sbod_version': (ctypes.c_char_p, []),
     'sbod_abi_version': (I32, []),
     'sbod_last_error': (ctypes.c_char_p, []),
+    'sbod_null_kernel': (I32, [I32, P]),
     'sbod_iou_pairwise_f32': (I32, [P, P, I32, I32, P, I64, I32, I32, P, P]),
     'sbod_match_workspace_bytes': (SZ, [I32, I32]),
     'sbod_match_workspace_bytes_p': (SZ, [I32, I32, I32]),

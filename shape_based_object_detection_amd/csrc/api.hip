@@ -28,6 +28,10 @@ int launch_status(const char *what) {
   return SBOD_OK;
 }
 
+// An empty kernel (profiling calibration: the fixed per-dispatch cost a tool adds, MEASUREMENT
+// in DESIGN.md / scripts/rocprof_overhead.py).
+__global__ __launch_bounds__(64) void k_null() {}
+
 // grad *= *scale unless *scale == 1 (every block reads the scalar and exits early).
 template <typename T>
 __global__ __launch_bounds__(256) void k_scale(T *__restrict__ g, int64_t n, const float *scale) {
@@ -236,6 +240,14 @@ int sbod_timing_query(const char *kernel, int *launches, double *total_ms) {
 
 const char *sbod_version(void) { return "sbod-hip 0.1.0 (gfx950)"; }
 int sbod_abi_version(void) { return SBOD_ABI_VERSION; }
+
+int sbod_null_kernel(int blocks, void *stream) {
+  SBOD_REQUIRE(blocks > 0, "sbod_null_kernel: blocks %d", blocks);
+  sbod::KernelTimer kt("k_null", sbod::as_stream(stream), true);
+  sbod::tlaunch(kt, sbod::k_null, dim3(blocks), dim3(64), 0, sbod::as_stream(stream));
+  SBOD_LAUNCHED("k_null");
+  return SBOD_OK;
+}
 const char *sbod_last_error(void) { return sbod::g_err; }
 
 int sbod_memcpy_d2h_async(void *dst_host, const void *src_dev, size_t bytes, void *stream) {

@@ -86,7 +86,7 @@ def test_fused_finish_large_logits(scale):
     if np.isnan(ref):
         assert np.isnan(fused) and np.isnan(unf)
     else:
-        assert np.isfinite(fused) and fused > 1e5
+        assert np.isfinite(fused) and fused > 100.0   # normalised by n_pos: ~1e3 at x10
         np.testing.assert_allclose(fused, ref, rtol=1e-4)
         np.testing.assert_allclose(cf, cu, rtol=1e-6)
 
