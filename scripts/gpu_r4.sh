@@ -24,5 +24,15 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o ru
         gpurun_out/roofline_check_$TAG.json gpurun_out/prof_$TAG.log > /dev/null
 rc=$?
 [ $ok -ne 0 ] && rc=1
+# OVH=1: the profiler's per-dispatch cost (scripts/rocprof_overhead.py), plain then profiled
+if [ $rc -eq 0 ] && [ -n "$OVH" ]; then
+  timeout -k 10 180 python -u scripts/rocprof_overhead.py --out gpurun_out/ovh_plain_$TAG.json \
+      > gpurun_out/ovh_$TAG.log 2>&1 && \
+  timeout -k 10 180 rocprofv3 --kernel-trace -d gpurun_out/ovh_$TAG -o run --output-format csv -- \
+      python3 scripts/rocprof_overhead.py --out gpurun_out/ovh_prof_$TAG.json >> gpurun_out/ovh_$TAG.log 2>&1 && \
+  python3 scripts/rocprof_overhead.py --combine gpurun_out/ovh_plain_$TAG.json gpurun_out/ovh_prof_$TAG.json \
+      gpurun_out/ovh_$TAG/run_kernel_trace.csv gpurun_out/rocprof_overhead_$TAG.json >> gpurun_out/ovh_$TAG.log 2>&1
+  rc=$?
+fi
 echo "EXIT $rc"
 exit $rc
