@@ -2237,8 +2237,11 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
   SBOD_REQUIRE(!exhaustive || ((w2 >= top_k || w2 >= P) && all_lds <= 64 * 1024),
                "sbod_detect_f32: exhaustive mode supports top_k <= 2047");
   hipStream_t s = as_stream(stream);
+  // the WHOLE aligned prefix (sbod_detect_counter_bytes): a caller that trusts it clean later (a
+  // larger B * C whose counters reach into this call's alignment padding) must find zeros there,
+  // not the decoded boxes of an earlier, smaller call whose box region began inside it
   if ((flags & SBOD_DETECT_COUNTERS_ZEROED) == 0 &&
-      hipMemsetAsync(ws.count, 0, static_cast<size_t>(B) * C * 4 + static_cast<size_t>(B) * 4, s) != hipSuccess)
+      hipMemsetAsync(ws.count, 0, sbod_detect_counter_bytes(B, C), s) != hipSuccess)
     return launch_status("hipMemsetAsync(detect)");
   DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.boxes, ws.cand, ws.count,
             debug_probs, debug_boxes, nullptr};

@@ -51,3 +51,28 @@ def test_one_launch_counters_left_zero_and_repeatable():
     for a, b in zip(res[1], res[0]):   # B=3 of the same seed: the first three images
         for x, y in zip(a, b[:3]):
             assert torch.equal(x, y)
+
+
+def test_counter_prefix_clean_across_batch_sizes():
+    """The zero-on-entry prefix is the ALIGNED counter region: B=3 puts its decoded boxes inside
+    the alignment padding of B=6's prefix, B=6 (larger, so it zeroes its own prefix) must zero
+    that padding too, because B=8 then trusts the same aligned prefix to be zero (its counters
+    reach into it).  Every call on one stream's workspace equals the same call on a fresh one."""
+    Pn = prior_table('SSD512')
+    P = torch.from_numpy(Pn).to(DEV)
+    locs, scores = synth.make_preds(8, Pn.shape[0], 21, seed=41, bg_shift=6.0)
+    l, s = locs.to(DEV), scores.to(DEV)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        seq = [core.detect(l[:B].contiguous(), s[:B].contiguous(), 0.01, 0.45, 200, P) for B in (3, 6, 8)]
+    torch.cuda.current_stream().wait_stream(side)
+    for B, got in zip((3, 6, 8), seq):
+        fresh = torch.cuda.Stream()
+        fresh.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(fresh):
+            ref = core.detect(l[:B].contiguous(), s[:B].contiguous(), 0.01, 0.45, 200, P)
+        torch.cuda.current_stream().wait_stream(fresh)
+        for a, b in zip(got, ref):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y)
