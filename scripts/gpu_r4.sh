@@ -24,6 +24,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o ru
         gpurun_out/roofline_check_$TAG.json gpurun_out/prof_$TAG.log > /dev/null
 rc=$?
 [ $ok -ne 0 ] && rc=1
+# SUBMIT=1: the host cost of each piece of the step's submit / collect (scripts/submit_probe.py)
+if [ $rc -eq 0 ] && [ -n "$SUBMIT" ]; then
+  timeout -k 10 180 python -u scripts/submit_probe.py --out gpurun_out/submit_probe_$TAG.json \
+      > gpurun_out/submit_probe_$TAG.log 2>&1
+  rc=$?
+fi
 # OVH=1: the profiler's per-dispatch cost (scripts/rocprof_overhead.py), plain then profiled
 if [ $rc -eq 0 ] && [ -n "$OVH" ]; then
   timeout -k 10 180 python -u scripts/rocprof_overhead.py --out gpurun_out/ovh_plain_$TAG.json \
