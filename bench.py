@@ -130,7 +130,7 @@ ALGO_BYTES = {
     'k_criterion': lambda w: w['B'] * w['P'] * (2 * (16 + 4 * w['C']) + 8) + 32 * w['P'],
 }
 HBM_KERNELS = tuple(ALGO_BYTES)
-ALL_KERNELS = HBM_KERNELS + ('k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm')
+ALL_KERNELS = HBM_KERNELS + ('k_det_nms', 'k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm')
 PMC_FILE = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
 
 
