@@ -375,6 +375,23 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
                      int O, int k, int stride, int pad, float *grad_x, float *grad_offset,
                      float *grad_mask_logits, float *grad_weight, void *workspace,
                      size_t workspace_bytes, void *stream);
+/* Training form (what an autograd Function binds; Deformable_convolution.py:33-91 forward and its
+ * autograd backward).  The forward derives, once, everything the backward re-uses — per-(pixel,
+ * kernel point) coefficients, channels-last x, both weight layouts, per-input-pixel sample counts —
+ * into a caller-owned STATE buffer (sbod_dcn_state_bytes) that must stay unchanged until the
+ * backward; the backward reads it (never writes it: a retained graph may run it twice) and
+ * works in SCRATCH (sbod_dcn_scratch_bytes, reusable across calls in stream order).
+ * grad_mask_logits must be NULL when the forward had no mask.  The stateless
+ * sbod_dcn_bwd_f32 above re-derives the state in its own workspace (state + scratch). */
+size_t sbod_dcn_state_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
+size_t sbod_dcn_scratch_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
+int sbod_dcn_fwd_train_f32(const float *x, const float *offset, const float *mask_logits,
+                           const float *weight, int B, int C, int H, int W, int O, int k, int stride,
+                           int pad, float *out, void *state, size_t state_bytes, void *stream);
+int sbod_dcn_bwd_state_f32(const float *grad_out, int B, int C, int H, int W, int O, int k, int stride,
+                           int pad, float *grad_x, float *grad_offset, float *grad_mask_logits,
+                           float *grad_weight, const void *state, size_t state_bytes, void *scratch,
+                           size_t scratch_bytes, void *stream);
 
 /* ---------------------------------------------------------------- f2: VOC 11-point mAP
  * metrics.calculate_mAP (metrics.py:8-145).  Detections and ground truth are the concatenated

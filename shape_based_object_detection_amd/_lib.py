@@ -71,6 +71,10 @@ SIGNATURES = {
     'sbod_gt_pack': (I32, [P, P, P, I32, I64, P, P, P, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
     'sbod_dcn_fwd_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
+    'sbod_dcn_state_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
+    'sbod_dcn_scratch_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
+    'sbod_dcn_fwd_train_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),
+    'sbod_dcn_bwd_state_f32': (I32, [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, P, P, SZ, P, SZ, P]),
     'sbod_dcn_fwd_f32': (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, SZ, P]),
     'sbod_dcn_bwd_f32': (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, P,
                                P, SZ, P]),

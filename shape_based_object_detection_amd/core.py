@@ -893,8 +893,14 @@ def focal_rows(kind, logits, target, alpha_fg, alpha_bg, gamma):
 
 # ----------------------------------------------------------------------------- a14: DeformConv2d
 class _DeformConv(torch.autograd.Function):
-    """out = DCN(x, offset, sigmoid(mask_logits), weight) on the HIP path; backward produces the
-    gradients of all four inputs from one coefficient pass + two MFMA kernels (dcn.hip)."""
+    """out = DCN(x, offset, sigmoid(mask_logits), weight) on the HIP path.
+
+    A training forward (any input needs a gradient) runs ``sbod_dcn_fwd_train_f32`` into a
+    per-call STATE buffer that autograd keeps until the backward: the coefficients, channels-last
+    x, both weight layouts and the per-input-pixel sample counts, so ``sbod_dcn_bwd_state_f32``
+    re-derives none of them (five launches for all four gradients; the state is read-only there,
+    so a retained graph's second backward sees the same state).  An inference forward takes the
+    forward-only workspace (no state kept)."""
 
     @staticmethod
     def forward(ctx, x, offset, mask_logits, weight, ks, padding, stride):
@@ -909,39 +915,41 @@ class _DeformConv(torch.autograd.Function):
         if tuple(weight.shape) != (O, C, ks, ks):
             raise ValueError('DeformConv2d: weight shape %s' % (tuple(weight.shape),))
         out = torch.empty(B, O, Ho, Wo, dtype=torch.float32, device=x.device)
-        # an inference forward takes the forward-only size (no dcols rows); a training forward
-        # takes the backward's full size up front, so the backward never grows (reallocates) the
-        # cached workspace that this forward — possibly captured in a graph — addresses
+        dims = (B, C, H, W, O, ks, stride, padding)
+        ctx.cfg = dims
+        ctx.modulated = mask_logits is not None
         if any(ctx.needs_input_grad[:4]):
-            nb = L.lib().sbod_dcn_workspace_bytes(B, C, H, W, O, ks, stride, padding)
+            nb = L.lib().sbod_dcn_state_bytes(*dims)
+            state = torch.empty(nb, dtype=torch.uint8, device=x.device)
+            L.call('sbod_dcn_fwd_train_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight), *dims,
+                   L.ptr(out), L.ptr(state), nb, L.stream_of(x))
+            ctx.save_for_backward(state)
         else:
-            nb = L.lib().sbod_dcn_fwd_workspace_bytes(B, C, H, W, O, ks, stride, padding)
-        ws = workspace(nb, x.device, 'dcn')
-        L.call('sbod_dcn_fwd_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight),
-               B, C, H, W, O, ks, stride, padding, L.ptr(out), L.ptr(ws), nb, L.stream_of(x))
-        ctx.save_for_backward(x, offset, mask_logits, weight)
-        ctx.cfg = (ks, padding, stride)
+            nb = L.lib().sbod_dcn_fwd_workspace_bytes(*dims)
+            ws = workspace(nb, x.device, 'dcn')
+            L.call('sbod_dcn_fwd_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight), *dims,
+                   L.ptr(out), L.ptr(ws), nb, L.stream_of(x))
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        x, offset, mask_logits, weight = ctx.saved_tensors
-        ks, padding, stride = ctx.cfg
-        B, C, H, W = x.shape
-        O = weight.shape[0]
+        state, = ctx.saved_tensors
+        B, C, H, W, O, ks, stride, padding = dims = ctx.cfg
         g = gout.contiguous().float()
         if g.data_ptr() % 16:          # the weight-gradient kernel reads grad_out as float4
             g = g.clone()
         need = ctx.needs_input_grad
-        gx = torch.empty_like(x) if need[0] else None
-        goff = torch.empty_like(offset) if need[1] else None
-        gm = torch.empty_like(mask_logits) if (mask_logits is not None and need[2]) else None
-        gw = torch.empty_like(weight) if need[3] else None
-        nb = L.lib().sbod_dcn_workspace_bytes(B, C, H, W, O, ks, stride, padding)
-        ws = workspace(nb, x.device, 'dcn')
-        L.call('sbod_dcn_bwd_f32', L.ptr(x), L.ptr(offset), L.ptr(mask_logits), L.ptr(weight),
-               L.ptr(g), B, C, H, W, O, ks, stride, padding, L.ptr(gx), L.ptr(goff), L.ptr(gm),
-               L.ptr(gw), L.ptr(ws), nb, L.stream_of(x))
+        dev = state.device
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        gx = torch.empty(B, C, H, W, dtype=torch.float32, device=dev) if need[0] else None
+        goff = torch.empty(B, 2 * ks * ks, Ho, Wo, dtype=torch.float32, device=dev) if need[1] else None
+        gm = (torch.empty(B, ks * ks, Ho, Wo, dtype=torch.float32, device=dev)
+              if (ctx.modulated and need[2]) else None)
+        gw = torch.empty(O, C, ks, ks, dtype=torch.float32, device=dev) if need[3] else None
+        nb = L.lib().sbod_dcn_scratch_bytes(*dims)
+        ws = workspace(nb, dev, 'dcn_scratch')
+        L.call('sbod_dcn_bwd_state_f32', L.ptr(g), *dims, L.ptr(gx), L.ptr(goff), L.ptr(gm), L.ptr(gw),
+               L.ptr(state), state.numel(), L.ptr(ws), nb, L.stream_of(g))
         return gx, goff, gm, gw, None, None, None
 
 

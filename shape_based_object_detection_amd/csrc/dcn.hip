@@ -8,7 +8,7 @@
 // (a permutation of conv.weight's c*N + n, applied to the weight copies below):
 //   forward      out[o, m]   = sum_K' Wf[o, K'] * cols[K', m]
 //   backward     dcols[m, c] = sum_o dout[o, m] * Wb[n, o, c]   (per n) -> dx, d_offset, d_mask
-//                dWp[o,n,c]  = sum_m dout[o, m] * cols[(n,c), m]
+//                dW[o,c,n]   = sum_m dout[o, m] * cols[(n,c), m]
 // cols[(n,c), m] = sigmoid(mask) * sum_q g_q * x[corner_q] is never materialised: it is built per
 // 32-channel K'-tile into LDS from per-(pixel, kernel point) coefficients computed once
 // (k_dcn_coef), reading x channels-last (xt) so the four corner gathers of a pixel are
@@ -43,9 +43,25 @@ struct DcnShape {
   int B, C, H, W, O, k, N, stride, pad, Ho, Wo, Hp, Wp, M, K;
 };
 
+// Grid-stride zero fill of n floats (16-B stores where aligned) by every thread of a launch: the
+// zero-initialised outputs of a later kernel ride along with an earlier one instead of a memset node.
+__device__ __forceinline__ void zero_fill(float *p, int64_t n) {
+  if (!p || n <= 0) return;
+  const int64_t nthr = static_cast<int64_t>(gridDim.x) * gridDim.y * gridDim.z * blockDim.x;
+  const int64_t id = (static_cast<int64_t>(blockIdx.z) * gridDim.y * gridDim.x +
+                      static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t head = (reinterpret_cast<uintptr_t>(p) & 15) ? n : 0;   // unaligned: scalar stores only
+  const int64_t n4 = (n - head) >> 2;
+  float4 *p4 = reinterpret_cast<float4 *>(p);
+  for (int64_t i = id; i < n4; i += nthr) p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = 4 * n4 + id; i < n; i += nthr) p[i] = 0.f;
+}
+
 __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__restrict__ offset,
                                                   const float *__restrict__ mlog,
-                                                  Coef *__restrict__ coef, uint32_t *__restrict__ tcount) {
+                                                  Coef *__restrict__ coef, uint32_t *__restrict__ tcount,
+                                                  float *__restrict__ zero_out, int64_t n_zero) {
+  zero_fill(zero_out, n_zero);   // the split-K forward's output, accumulated by k_dcn_fwd
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= static_cast<int64_t>(s.M) * s.N) return;
   const int n = static_cast<int>(t % s.N);
@@ -97,9 +113,11 @@ __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__res
 }
 
 
-// Batched transpose in [nb][R][S] -> out [nb][S][R] (64 x 64 LDS tiles).
+// Batched transpose in [nb][R][S] -> out [nb][S][R] (64 x 64 LDS tiles); zeroes `zero` [n_zero]
+// on the side (the sample counters the coefficient pass that follows increments).
 __global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ in, float *__restrict__ out,
-                                                   int R, int S) {
+                                                   int R, int S, float *__restrict__ zero, int64_t n_zero) {
+  zero_fill(zero, n_zero);
   __shared__ float t[64][65];
   const int s0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
   const int64_t base = static_cast<int64_t>(blockIdx.z) * R * S;
@@ -112,6 +130,26 @@ __global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ in,
   for (int i = ty; i < 64; i += 4) {
     const int s = s0 + i, r = r0 + tx;
     if (r < R && s < S) out[base + static_cast<int64_t>(s) * R + r] = t[tx][i];
+  }
+}
+
+// conv.weight [O][C][N] -> the forward's Wf [O][N][C] and (training) the backward's Wb [N][O][C]
+// in one pass: one block per (64-channel chunk, output channel), the chunk's 64 x N contiguous
+// weights staged in LDS, each layout's rows written along c.
+__global__ __launch_bounds__(256) void k_weight_layouts(const float *__restrict__ w, int O, int C, int N,
+                                                        float *__restrict__ wf, float *__restrict__ wb) {
+  __shared__ float t[64][kMaxN + 1];
+  const int c0 = blockIdx.x * 64, o = blockIdx.y;
+  const int nc = min(64, C - c0);
+  const float *src = w + (static_cast<int64_t>(o) * C + c0) * N;
+  for (int e = threadIdx.x; e < nc * N; e += blockDim.x) t[e / N][e % N] = src[e];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * N; e += blockDim.x) {
+    const int n = e >> 6, cl = e & 63;
+    if (cl >= nc) continue;
+    const float v = t[cl][n];
+    wf[(static_cast<int64_t>(o) * N + n) * C + c0 + cl] = v;
+    if (wb) wb[(static_cast<int64_t>(n) * O + o) * C + c0 + cl] = v;
   }
 }
 
@@ -434,8 +472,13 @@ struct DxEnt {
 };
 
 __global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__restrict__ coef,
-                                                     const uint32_t *__restrict__ toff,
-                                                     uint32_t *__restrict__ tcount, DxEnt *__restrict__ ent) {
+                                                     uint32_t *__restrict__ cur, DxEnt *__restrict__ ent,
+                                                     float *__restrict__ z0, int64_t n0, float *__restrict__ z1,
+                                                     int64_t n1, float *__restrict__ z2, int64_t n2) {
+  // the zero-initialised gradients the later kernels accumulate into (offset, mask, weight)
+  zero_fill(z0, n0);
+  zero_fill(z1, n1);
+  zero_fill(z2, n2);
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= static_cast<int64_t>(s.M) * s.N) return;
   const int m = static_cast<int>(t / s.N);
@@ -444,22 +487,36 @@ __global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__r
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (cf.idx[q] < 0) continue;
-    const int64_t tp = ib + cf.idx[q];
-    const uint32_t k = atomicSub(tcount + tp, 1u) - 1u;   // the counters return to zero
-    ent[toff[tp] + k] = DxEnt{static_cast<uint32_t>(t), cf.g[q] * cf.mval};
+    // cur starts at each pixel's first entry (exclusive scan of the counts) and ends at its last + 1
+    const uint32_t k = atomicAdd(cur + ib + cf.idx[q], 1u);
+    ent[k] = DxEnt{static_cast<uint32_t>(t), cf.g[q] * cf.mval};
   }
 }
 
-// One wave per input pixel; lanes hold 4 consecutive channels (C % 4 == 0) or 1.
+// One wave per input pixel, kGxPix pixels per block; lanes hold 4 consecutive channels (C % 4 == 0)
+// or 1.  Each 64*VEC-channel pass lands in LDS and leaves as rows of dx [B][C][H][W] (kGxPix
+// consecutive pixels per channel): the channels-last result is never written to HBM and
+// transposed back.  After k_dcn_dx_fill, cur[tp] is the end of pixel tp's entries and cur[tp - 1]
+// its start.
+constexpr int kGxPix = 16;
+
 template <int VEC>
-__global__ __launch_bounds__(256) void k_dcn_dx_gather(int C, int ntarget, const uint32_t *__restrict__ toff,
-                                                       const DxEnt *__restrict__ ent,
-                                                       const float *__restrict__ dcols, float *__restrict__ gxt) {
+__global__ __launch_bounds__(64 * kGxPix) void k_dcn_dx_gather(int C, int HW, int ntarget,
+                                                              const uint32_t *__restrict__ cur,
+                                                              const DxEnt *__restrict__ ent,
+                                                              const float *__restrict__ dcols, float *__restrict__ gx) {
+  __shared__ float s_t[kGxPix][64 * VEC + 1];
   const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // neighbouring input pixels (overlapping dcols rows) on one XCD
-  const int tp = xcd_logical(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (tp >= ntarget) return;
-  const uint32_t e0 = __builtin_amdgcn_readfirstlane(toff[tp]), e1 = __builtin_amdgcn_readfirstlane(toff[tp + 1]);
+  const int tp0 = xcd_logical(blockIdx.x, gridDim.x) * kGxPix;
+  const int tp = tp0 + wv;
+  const bool live = tp < ntarget;
+  uint32_t e0 = 0, e1 = 0;
+  if (live) {
+    e0 = __builtin_amdgcn_readfirstlane(tp > 0 ? cur[tp - 1] : 0u);
+    e1 = __builtin_amdgcn_readfirstlane(cur[tp]);
+  }
   for (int cb = 0; cb < C; cb += 64 * VEC) {   // uniform trip count: every lane loads entries
     const int c0 = min(cb + VEC * lane, C - VEC);   // lanes past C read a valid column, store nothing
     float acc[VEC];
@@ -493,18 +550,25 @@ __global__ __launch_bounds__(256) void k_dcn_dx_gather(int C, int ntarget, const
         for (int v = 0; v < VEC; ++v) acc[v] += w * x[v];
       }
     }
-    if (cb + VEC * lane >= C) continue;
-    float *dst = gxt + static_cast<int64_t>(tp) * C + c0;
-    if (VEC == 4)
-      *reinterpret_cast<float4 *>(dst) = make_float4(acc[0], acc[1], acc[VEC > 2 ? 2 : 0], acc[VEC > 3 ? 3 : 0]);
-    else
-      dst[0] = acc[0];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) s_t[wv][VEC * lane + v] = acc[v];
+    __syncthreads();
+    const int nc = min(64 * VEC, C - cb);
+    for (int e = threadIdx.x; e < kGxPix * 64 * VEC; e += 64 * kGxPix) {
+      const int px = e % kGxPix, cl = e / kGxPix, p = tp0 + px;
+      if (cl < nc && p < ntarget) {
+        const int b = p / HW, pix = p - b * HW;
+        gx[(static_cast<int64_t>(b) * C + cb + cl) * HW + pix] = s_t[px][cl];
+      }
+    }
+    __syncthreads();
   }
 }
 
 // ----------------------------------------------------------------------------- backward (weight)
 // Block: one kernel point n x 64 channels (blockIdx.x), a slice of pixels (blockIdx.y), 256
-// output channels (blockIdx.z): dWp[o, n, c] += sum_m dout[o, m] cols[(n, c), m].  The mirror of
+// output channels (blockIdx.z): dW[o, c, n] += sum_m dout[o, m] cols[(n, c), m] (conv.weight's
+// own layout: no transpose after).  The mirror of
 // the forward kernel: dout rows go straight from HBM into the MFMA A registers (float4 when a
 // 32-pixel chunk never straddles two images), the columns are re-sampled channels-last into
 // double-buffered LDS, and the next chunk's gathers are in flight during the current MFMAs.
@@ -716,7 +780,7 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.N + n) * s.C + c, acc[a][bq][r]);
+        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.C + c) * s.N + n, acc[a][bq][r]);
       }
     }
 }
@@ -747,12 +811,21 @@ DcnShape make_shape(int B, int C, int H, int W, int O, int k, int stride, int pa
 
 inline bool shape_ok(const DcnShape &s) { return s.B > 0; }
 
-struct DcnWs {
+// Training state (sbod_dcn_state_bytes): what the forward derives and the backward re-uses — the
+// per-(pixel, kernel point) coefficients, channels-last x, both weight layouts and the per-input-
+// pixel sample counts.  The forward-only workspace is its prefix (coef, xt, wf).
+struct DcnState {
   Coef *coef;
-  float *xt, *gxt, *wt, *gwp;
-  // backward dx gather: dcols rows [M][N][C], per-input-pixel counters / entry offsets, entries
+  float *xt, *wf;
+  uint32_t *tcount;   // training: [B*H*W + 1] corner samples per input pixel
+  float *wb;          // training: Wb [N][O][C]
+};
+
+// Backward scratch (sbod_dcn_scratch_bytes): dcols rows [M][N][C], the per-input-pixel entry
+// cursors and entries of the dx gather, the scan's temporary storage.
+struct DcnScratch {
   float *dcols;
-  uint32_t *tcount, *toff;
+  uint32_t *cur;
   DxEnt *ent;
   void *scan_tmp;
   size_t scan_bytes;
@@ -767,29 +840,33 @@ size_t dcn_scan_bytes(int64_t n) {
   return b;
 }
 
-// The forward needs only coef, xt and wt (a prefix of the layout); the backward's buffers
-// follow, so a forward-only caller sizes its workspace with sbod_dcn_fwd_workspace_bytes.
-size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w, bool fwd_only = false) {
+size_t carve_state(const DcnShape &s, void *base, DcnState *w, bool train) {
   char *p = static_cast<char *>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) { char *r = p ? p + off : nullptr; off += align_up(bytes); return r; };
-  const size_t xbytes = static_cast<size_t>(s.B) * s.C * s.H * s.W * 4;
   const size_t wbytes = static_cast<size_t>(s.O) * s.K * 4;
+  const size_t npix = static_cast<size_t>(s.B) * s.H * s.W;
+  DcnState t{};
+  t.coef = reinterpret_cast<Coef *>(take(static_cast<size_t>(s.M) * s.N * sizeof(Coef)));
+  t.xt = reinterpret_cast<float *>(take(npix * s.C * 4));
+  t.wf = reinterpret_cast<float *>(take(wbytes));
+  if (train) {
+    t.tcount = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
+    t.wb = reinterpret_cast<float *>(take(wbytes));
+  }
+  if (w) *w = t;
+  return off;
+}
+
+size_t carve_scratch(const DcnShape &s, void *base, DcnScratch *w) {
+  char *p = static_cast<char *>(base);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char *r = p ? p + off : nullptr; off += align_up(bytes); return r; };
   const size_t rows = static_cast<size_t>(s.M) * s.N;
   const size_t npix = static_cast<size_t>(s.B) * s.H * s.W;
-  DcnWs t{};
-  t.coef = reinterpret_cast<Coef *>(take(rows * sizeof(Coef)));
-  t.xt = reinterpret_cast<float *>(take(xbytes));
-  t.wt = reinterpret_cast<float *>(take(wbytes));
-  if (fwd_only) {
-    if (w) *w = t;
-    return off;
-  }
-  t.gxt = reinterpret_cast<float *>(take(xbytes));
-  t.gwp = reinterpret_cast<float *>(take(wbytes));
+  DcnScratch t{};
   t.dcols = reinterpret_cast<float *>(take(rows * s.C * 4));
-  t.tcount = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
-  t.toff = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
+  t.cur = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
   t.ent = reinterpret_cast<DxEnt *>(take(rows * 4 * sizeof(DxEnt)));
   t.scan_bytes = dcn_scan_bytes(static_cast<int64_t>(npix) + 1);
   t.scan_tmp = take(t.scan_bytes);
@@ -797,25 +874,26 @@ size_t dcn_carve(const DcnShape &s, void *base, DcnWs *w, bool fwd_only = false)
   return off;
 }
 
-void launch_transpose(const float *in, float *out, int nb, int R, int S, hipStream_t hs) {
-  hipLaunchKernelGGL(k_transpose, dim3((S + 63) / 64, (R + 63) / 64, nb), dim3(256), 0, hs, in, out, R, S);
+// The stateless backward's workspace: the training state, then the scratch.
+size_t carve_all(const DcnShape &s, void *base, DcnState *st, DcnScratch *sc) {
+  const size_t a = carve_state(s, base, st, true);
+  return a + carve_scratch(s, base ? static_cast<char *>(base) + a : nullptr, sc);
+}
+
+// split-K of the forward: up to 16 slices of the K' tiles (a sweep of the cap at 32x32 / 16x16 /
+// 8x8, profiles/r3_dcn_split_sweep_s1.jsonl: 16 is at least as fast as 32 or 64 on every map, 7 %
+// faster at 8x8), only while the pixel x output-channel tiles leave the chip under-filled
+int fwd_split(const DcnShape &s) {
+  const int mt = (s.M + kFM - 1) / kFM, og = (s.O + 255) / 256;
+  const int T = s.N * ((s.C + kFKC - 1) / kFKC);
+  int split = 1;
+  while (split * 2 <= T && mt * og * split < 512 && split < 16) split *= 2;
+  return split;
 }
 
 }  // namespace sbod
 
 using namespace sbod;
-
-extern "C" {
-
-size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
-  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
-  return shape_ok(s) ? dcn_carve(s, nullptr, nullptr) : 0;
-}
-
-size_t sbod_dcn_fwd_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
-  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
-  return shape_ok(s) ? dcn_carve(s, nullptr, nullptr, true) : 0;
-}
 
 static int dcn_check(const DcnShape &s, const float *x, const float *offset, const float *weight) {
   SBOD_REQUIRE(x && offset && weight && shape_ok(s),
@@ -828,50 +906,29 @@ static int dcn_check(const DcnShape &s, const float *x, const float *offset, con
   return SBOD_OK;
 }
 
-static int dcn_prepare(const DcnShape &s, const float *x, const float *offset, const float *mask_logits,
-                       void *workspace, size_t workspace_bytes, DcnWs *w, hipStream_t hs, const char *who,
-                       bool count_targets, bool fwd_only) {
-  const size_t need = dcn_carve(s, nullptr, nullptr, fwd_only);
-  if (workspace == nullptr || workspace_bytes < need) {
-    set_error("%s: workspace %zu < %zu", who, workspace_bytes, need);
-    return SBOD_E_WORKSPACE;
-  }
-  dcn_carve(s, workspace, w, fwd_only);
+// Derives the state from the inputs: x -> channels-last xt (training: the sample counters zeroed
+// on the side), the coefficients (training: the counts; split-K: the output zeroed on the side),
+// the weight layouts.  Three launches.
+static int dcn_derive(const DcnShape &s, const float *x, const float *offset, const float *mask_logits,
+                      const float *weight, const DcnState &st, bool train, float *zero_out, int64_t n_zero_out,
+                      hipStream_t hs) {
+  const int64_t npix = static_cast<int64_t>(s.B) * s.H * s.W;
+  const int HW = s.H * s.W;
+  hipLaunchKernelGGL(k_transpose, dim3((s.C + 63) / 64, (HW + 63) / 64, s.B), dim3(256), 0, hs, x, st.xt, s.C, HW,
+                     train ? reinterpret_cast<float *>(st.tcount) : nullptr, train ? npix + 1 : 0);
+  SBOD_LAUNCHED("k_transpose(x)");   // x [B][C][HW] -> xt [B][HW][C]
   const int64_t nc = static_cast<int64_t>(s.M) * s.N;
-  if (count_targets &&
-      hipMemsetAsync(w->tcount, 0, (static_cast<size_t>(s.B) * s.H * s.W + 1) * 4, hs) != hipSuccess)
-    return launch_status("hipMemsetAsync(dcn dx counters)");
-  hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, w->coef,
-                     count_targets ? w->tcount : nullptr);
+  hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, st.coef,
+                     train ? st.tcount : nullptr, zero_out, n_zero_out);
   SBOD_LAUNCHED("k_dcn_coef");
-  launch_transpose(x, w->xt, s.B, s.C, s.H * s.W, hs);   // x [B][C][HW] -> xt [B][HW][C]
-  SBOD_LAUNCHED("k_transpose(x)");
+  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
+                     train ? st.wb : nullptr);
+  SBOD_LAUNCHED("k_weight_layouts");
   return SBOD_OK;
 }
 
-int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logits,
-                     const float *weight, int B, int C, int H, int W, int O, int k, int stride,
-                     int pad, float *out, void *workspace, size_t workspace_bytes, void *stream) {
-  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
-  int st = dcn_check(s, x, offset, weight);
-  if (st != SBOD_OK) return st;
-  SBOD_REQUIRE(out != nullptr, "sbod_dcn_fwd_f32: out is NULL");
-  hipStream_t hs = as_stream(stream);
-  DcnWs w;
-  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_fwd_f32", false, true);
-  if (st != SBOD_OK) return st;
-  launch_transpose(weight, w.wt, s.O, s.C, s.N, hs);   // W [O][C][N] -> Wf [O][N][C]
-  SBOD_LAUNCHED("k_transpose(w)");
-  const int mt = (s.M + kFM - 1) / kFM, og = (s.O + 255) / 256;
-  const int T = s.N * ((s.C + kFKC - 1) / kFKC);
-  // split-K up to 16 (a sweep of the cap at 32x32 / 16x16 / 8x8, profiles/r3_dcn_split_sweep_s1.jsonl:
-  // 16 is at least as fast as 32 or 64 on every map, 7 % faster at 8x8; fewer slices of the weight
-  // gradient were slower everywhere)
-  int split = 1;
-  while (split * 2 <= T && mt * og * split < 512 && split < 16) split *= 2;
-  if (split > 1 && hipMemsetAsync(out, 0, static_cast<size_t>(s.M) * s.O * 4, hs) != hipSuccess)
-    return launch_status("hipMemsetAsync(dcn out)");
-  const dim3 grid(mt, og, split);
+static int dcn_forward(const DcnShape &s, const DcnState &st, float *out, int split, hipStream_t hs) {
+  const dim3 grid((s.M + kFM - 1) / kFM, (s.O + 255) / 256, split);
   KernelTimer kt("k_dcn_fwd", hs);
   const size_t lds = static_cast<size_t>(s.N) * 9 * kFM * 4;   // the block's coefficients
   if (lds > 48 * 1024) {   // k >= 5: above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
@@ -880,74 +937,62 @@ int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logi
       return launch_status("hipFuncSetAttribute(k_dcn_fwd LDS)");
   }
   if (s.C % 4 == 0)
-    hipLaunchKernelGGL(k_dcn_fwd<4>, grid, dim3(kDcnThreads), lds, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
+    hipLaunchKernelGGL(k_dcn_fwd<4>, grid, dim3(kDcnThreads), lds, hs, s, st.xt, st.coef, st.wf, out, split > 1 ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_dcn_fwd<1>, grid, dim3(kDcnThreads), lds, hs, s, w.xt, w.coef, w.wt, out, split > 1 ? 1 : 0);
+    hipLaunchKernelGGL(k_dcn_fwd<1>, grid, dim3(kDcnThreads), lds, hs, s, st.xt, st.coef, st.wf, out, split > 1 ? 1 : 0);
   SBOD_LAUNCHED("k_dcn_fwd");
   return SBOD_OK;
 }
 
-int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logits,
-                     const float *weight, const float *grad_out, int B, int C, int H, int W,
-                     int O, int k, int stride, int pad, float *grad_x, float *grad_offset,
-                     float *grad_mask_logits, float *grad_weight, void *workspace,
-                     size_t workspace_bytes, void *stream) {
-  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
-  int st = dcn_check(s, x, offset, weight);
-  if (st != SBOD_OK) return st;
-  SBOD_REQUIRE(grad_out != nullptr, "sbod_dcn_bwd_f32: grad_out is NULL");
-  hipStream_t hs = as_stream(stream);
-  DcnWs w;
-  st = dcn_prepare(s, x, offset, mask_logits, workspace, workspace_bytes, &w, hs, "sbod_dcn_bwd_f32",
-                   grad_x != nullptr, false);
-  if (st != SBOD_OK) return st;
-  if (!mask_logits) grad_mask_logits = nullptr;
-  const int npix = B * H * W;
-  const bool need_cols = grad_x || grad_offset || grad_mask_logits;
+// The backward from a training state: with dx wanted, scan (the pixels' entry ranges) -> dx_fill
+// (which also zeroes the offset / mask / weight gradients) -> bwd_data (dcols rows) -> dx gather
+// (straight into [B][C][H][W]) -> bwd_weight (weight gradient into [O][C][k][k] and the offset /
+// mask gradients); five launches for all four gradients.
+static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch &sc, const float *grad_out,
+                        float *grad_x, float *grad_offset, float *grad_mask_logits, float *grad_weight, hipStream_t hs) {
+  const int npix = s.B * s.H * s.W;
+  const bool need_om = grad_offset || grad_mask_logits;
+  const bool need_cols = grad_x || need_om;
   SBOD_REQUIRE(!need_cols || (static_cast<int64_t>(s.M) * s.O * 4 < (1ll << 31) &&
                               static_cast<int64_t>(s.N) * s.O * s.C * 4 < (1ll << 31)),
-               "sbod_dcn_bwd_f32: grad_out / weight exceed the 2 GiB buffer-descriptor range");
-  if (grad_x) {   // the input pixels' entry ranges (scan of the counts k_dcn_coef made)
-    size_t tb = w.scan_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tb, w.tcount, w.toff, npix + 1, hs) != hipSuccess)
+               "sbod_dcn_bwd: grad_out / weight exceed the 2 GiB buffer-descriptor range");
+  const int64_t ob = static_cast<int64_t>(s.M) * s.N;
+  const int64_t wn = static_cast<int64_t>(s.O) * s.K;
+  if (grad_x) {   // the input pixels' entry ranges (scan of the counts the forward made)
+    size_t tb = sc.scan_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, tb, st.tcount, sc.cur, npix + 1, hs) != hipSuccess)
       return launch_status("DeviceScan(dcn dx offsets)");
-    const int64_t nc = static_cast<int64_t>(s.M) * s.N;
-    hipLaunchKernelGGL(k_dcn_dx_fill, dim3((nc + 255) / 256), dim3(256), 0, hs, s, w.coef, w.toff, w.tcount, w.ent);
+    hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hs, s, st.coef, sc.cur, sc.ent,
+                       grad_offset, grad_offset ? 2 * ob : 0, grad_mask_logits, grad_mask_logits ? ob : 0,
+                       grad_weight, grad_weight ? wn : 0);
     SBOD_LAUNCHED("k_dcn_dx_fill");
+  } else {
+    if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob * 4, hs) != hipSuccess) return launch_status("memset");
+    if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob * 4, hs) != hipSuccess) return launch_status("memset");
+    if (grad_weight && hipMemsetAsync(grad_weight, 0, wn * 4, hs) != hipSuccess) return launch_status("memset");
   }
   if (need_cols) {
-    launch_transpose(weight, w.wt, 1, s.O * s.C, s.N, hs);   // W [O*C][N] -> Wb [N][O][C]
-    SBOD_LAUNCHED("k_transpose(wb)");
-    {
-      KernelTimer kt("k_dcn_bwd_data", hs);
-      hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
-                         hs, s, w.wt, grad_out, w.dcols);
-    }
-    SBOD_LAUNCHED("k_dcn_bwd_data");
+    KernelTimer kt("k_dcn_bwd_data", hs);
+    hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
+                       hs, s, st.wb, grad_out, sc.dcols);
   }
+  if (need_cols) SBOD_LAUNCHED("k_dcn_bwd_data");
   if (grad_x) {
     {
       KernelTimer kt("k_dcn_dx_gather", hs);
+      const dim3 grid((npix + kGxPix - 1) / kGxPix);
       if (s.C % 4 == 0)
-        hipLaunchKernelGGL(k_dcn_dx_gather<4>, dim3((npix + 3) / 4), dim3(256), 0, hs, s.C, npix, w.toff, w.ent,
-                           w.dcols, w.gxt);
+        hipLaunchKernelGGL(k_dcn_dx_gather<4>, grid, dim3(64 * kGxPix), 0, hs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
+                           sc.dcols, grad_x);
       else
-        hipLaunchKernelGGL(k_dcn_dx_gather<1>, dim3((npix + 3) / 4), dim3(256), 0, hs, s.C, npix, w.toff, w.ent,
-                           w.dcols, w.gxt);
+        hipLaunchKernelGGL(k_dcn_dx_gather<1>, grid, dim3(64 * kGxPix), 0, hs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
+                           sc.dcols, grad_x);
     }
     SBOD_LAUNCHED("k_dcn_dx_gather");
-    launch_transpose(w.gxt, grad_x, s.B, s.H * s.W, s.C, hs);   // [B][HW][C] -> [B][C][HW]
-    SBOD_LAUNCHED("k_transpose(dx)");
   }
-  const bool need_om = grad_offset || grad_mask_logits;
   if (grad_weight || need_om) {
     // weight gradient, and the offset / mask gradients from the same corner samples (C / 64
-    // channel-block partials added into zeroed outputs)
-    const size_t ob = static_cast<size_t>(s.M) * s.N * 4;
-    if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob, hs) != hipSuccess) return launch_status("memset");
-    if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob, hs) != hipSuccess) return launch_status("memset");
-    if (grad_weight && hipMemsetAsync(w.gwp, 0, static_cast<size_t>(O) * s.K * 4, hs) != hipSuccess)
-      return launch_status("hipMemsetAsync(dcn dw)");
+    // channel-block partials added into the zeroed outputs)
     const int gx = s.N * ((s.C + kWC - 1) / kWC), gz = grad_weight ? (s.O + 255) / 256 : 1;
     // one round of resident blocks (256 CUs x 2): a partial second round would double the time
     int slices = std::max(1, 512 / (gx * gz));
@@ -957,12 +1002,11 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
     slices = (s.M + m_slice - 1) / m_slice;
     const dim3 grid(gx, slices, gz);
     const bool avec = (s.Ho * s.Wo) % kWMs == 0;   // 32-pixel chunks never straddle images
-    float *gwp = grad_weight ? w.gwp : nullptr;
-    const float *dc = need_om ? w.dcols : nullptr;
+    const float *dc = need_om ? sc.dcols : nullptr;
     {
       KernelTimer kt("k_dcn_bwd_weight", hs);
       auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, dim3(kDcnThreads), 0, hs, s, w.xt, w.coef, grad_out, gwp, m_slice, dc,
+        hipLaunchKernelGGL(kern, grid, dim3(kDcnThreads), 0, hs, s, st.xt, st.coef, grad_out, grad_weight, m_slice, dc,
                            grad_offset, grad_mask_logits);
       };
       if (dc) {
@@ -976,12 +1020,118 @@ int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logi
       }
     }
     SBOD_LAUNCHED("k_dcn_bwd_weight");
-    if (grad_weight) {
-      launch_transpose(w.gwp, grad_weight, s.O, s.N, s.C, hs);   // [O][N][C] -> [O][C][N]
-      SBOD_LAUNCHED("k_transpose(dw)");
-    }
   }
   return SBOD_OK;
+}
+
+extern "C" {
+
+size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  return shape_ok(s) ? carve_all(s, nullptr, nullptr, nullptr) : 0;
+}
+
+size_t sbod_dcn_fwd_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  return shape_ok(s) ? carve_state(s, nullptr, nullptr, false) : 0;
+}
+
+size_t sbod_dcn_state_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  return shape_ok(s) ? carve_state(s, nullptr, nullptr, true) : 0;
+}
+
+size_t sbod_dcn_scratch_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  return shape_ok(s) ? carve_scratch(s, nullptr, nullptr) : 0;
+}
+
+int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logits,
+                     const float *weight, int B, int C, int H, int W, int O, int k, int stride,
+                     int pad, float *out, void *workspace, size_t workspace_bytes, void *stream) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  int st = dcn_check(s, x, offset, weight);
+  if (st != SBOD_OK) return st;
+  SBOD_REQUIRE(out != nullptr, "sbod_dcn_fwd_f32: out is NULL");
+  const size_t need = carve_state(s, nullptr, nullptr, false);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("sbod_dcn_fwd_f32: workspace %zu < %zu", workspace_bytes, need);
+    return SBOD_E_WORKSPACE;
+  }
+  hipStream_t hs = as_stream(stream);
+  DcnState w;
+  carve_state(s, workspace, &w, false);
+  const int split = fwd_split(s);
+  st = dcn_derive(s, x, offset, mask_logits, weight, w, false, split > 1 ? out : nullptr,
+                  split > 1 ? static_cast<int64_t>(s.M) * s.O : 0, hs);
+  if (st != SBOD_OK) return st;
+  return dcn_forward(s, w, out, split, hs);
+}
+
+int sbod_dcn_fwd_train_f32(const float *x, const float *offset, const float *mask_logits,
+                           const float *weight, int B, int C, int H, int W, int O, int k, int stride,
+                           int pad, float *out, void *state, size_t state_bytes, void *stream) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  int st = dcn_check(s, x, offset, weight);
+  if (st != SBOD_OK) return st;
+  SBOD_REQUIRE(out != nullptr, "sbod_dcn_fwd_train_f32: out is NULL");
+  const size_t need = carve_state(s, nullptr, nullptr, true);
+  if (state == nullptr || state_bytes < need) {
+    set_error("sbod_dcn_fwd_train_f32: state %zu < %zu", state_bytes, need);
+    return SBOD_E_WORKSPACE;
+  }
+  hipStream_t hs = as_stream(stream);
+  DcnState w;
+  carve_state(s, state, &w, true);
+  const int split = fwd_split(s);
+  st = dcn_derive(s, x, offset, mask_logits, weight, w, true, split > 1 ? out : nullptr,
+                  split > 1 ? static_cast<int64_t>(s.M) * s.O : 0, hs);
+  if (st != SBOD_OK) return st;
+  return dcn_forward(s, w, out, split, hs);
+}
+
+int sbod_dcn_bwd_state_f32(const float *grad_out, int B, int C, int H, int W, int O, int k, int stride,
+                           int pad, float *grad_x, float *grad_offset, float *grad_mask_logits,
+                           float *grad_weight, const void *state, size_t state_bytes, void *scratch,
+                           size_t scratch_bytes, void *stream) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  SBOD_REQUIRE(shape_ok(s) && s.N <= kMaxN, "sbod_dcn_bwd_state_f32: bad sizes");
+  SBOD_REQUIRE(grad_out != nullptr, "sbod_dcn_bwd_state_f32: grad_out is NULL");
+  const size_t need_st = carve_state(s, nullptr, nullptr, true), need_sc = carve_scratch(s, nullptr, nullptr);
+  if (state == nullptr || state_bytes < need_st || scratch == nullptr || scratch_bytes < need_sc) {
+    set_error("sbod_dcn_bwd_state_f32: state %zu < %zu or scratch %zu < %zu", state_bytes, need_st, scratch_bytes,
+              need_sc);
+    return SBOD_E_WORKSPACE;
+  }
+  DcnState w;
+  DcnScratch t;
+  carve_state(s, const_cast<void *>(state), &w, true);
+  carve_scratch(s, scratch, &t);
+  return dcn_backward(s, w, t, grad_out, grad_x, grad_offset, grad_mask_logits, grad_weight, as_stream(stream));
+}
+
+int sbod_dcn_bwd_f32(const float *x, const float *offset, const float *mask_logits,
+                     const float *weight, const float *grad_out, int B, int C, int H, int W,
+                     int O, int k, int stride, int pad, float *grad_x, float *grad_offset,
+                     float *grad_mask_logits, float *grad_weight, void *workspace,
+                     size_t workspace_bytes, void *stream) {
+  const DcnShape s = make_shape(B, C, H, W, O, k, stride, pad);
+  int st = dcn_check(s, x, offset, weight);
+  if (st != SBOD_OK) return st;
+  SBOD_REQUIRE(grad_out != nullptr, "sbod_dcn_bwd_f32: grad_out is NULL");
+  const size_t need = carve_all(s, nullptr, nullptr, nullptr);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("sbod_dcn_bwd_f32: workspace %zu < %zu", workspace_bytes, need);
+    return SBOD_E_WORKSPACE;
+  }
+  hipStream_t hs = as_stream(stream);
+  DcnState w;
+  DcnScratch t;
+  carve_all(s, workspace, &w, &t);
+  st = dcn_derive(s, x, offset, mask_logits, weight, w, true, nullptr, 0, hs);   // the state, re-derived
+  if (st != SBOD_OK) return st;
+  if (!mask_logits) grad_mask_logits = nullptr;
+  return dcn_backward(s, w, t, grad_out, grad_x, grad_offset, grad_mask_logits, grad_weight, hs);
 }
 
 }  // extern "C"

@@ -192,3 +192,9 @@ def test_workspace_layout_queries():
     assert lib.sbod_match_ssd_workspace_bytes(0, 8732) == 0
     assert 0 < lib.sbod_dcn_fwd_workspace_bytes(2, 8, 9, 9, 8, 3, 1, 1) < lib.sbod_dcn_workspace_bytes(2, 8, 9, 9, 8, 3, 1, 1)
     assert lib.sbod_dcn_workspace_bytes(2, 8, 9, 9, 8, 3, 0, 1) == 0      # stride 0: invalid, no SIGFPE
+    # the training form: forward-only workspace < state; the stateless backward's workspace is
+    # exactly the state followed by the scratch
+    d = (16, 256, 64, 64, 256, 3, 1, 1)
+    assert lib.sbod_dcn_fwd_workspace_bytes(*d) < lib.sbod_dcn_state_bytes(*d)
+    assert lib.sbod_dcn_state_bytes(*d) + lib.sbod_dcn_scratch_bytes(*d) == lib.sbod_dcn_workspace_bytes(*d)
+    assert lib.sbod_dcn_state_bytes(2, 8, 9, 9, 8, 3, 0, 1) == lib.sbod_dcn_scratch_bytes(2, 8, 9, 9, 8, 3, 0, 1) == 0

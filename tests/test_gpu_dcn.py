@@ -206,3 +206,36 @@ def test_partial_gradients_match_full_backward(which):
                                        err_msg='partial ' + n)
         else:
             assert pp.grad is None
+
+
+def test_state_backward_stateless_backward_and_retained_graph():
+    """The training form (forward state kept by autograd, sbod_dcn_bwd_state_f32) against the
+    C-ABI's stateless sbod_dcn_bwd_f32 (state re-derived in its own workspace), a retained graph's
+    second backward (the backward only reads the state) against its first, and the inference
+    forward (no state) against the training forward.  The dx entries and the weight / offset
+    partials are combined by atomics in arbitrary order: equal within fp32 rounding, not bitwise."""
+    from shape_based_object_detection_amd import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(21)
+    B, C, O, H, ks = 2, 40, 48, 11, 3
+    x = torch.randn(B, C, H, H, device=DEV, generator=g).requires_grad_(True)
+    off = torch.randn(B, 2 * ks * ks, H, H, device=DEV, generator=g).requires_grad_(True)
+    ml = torch.randn(B, ks * ks, H, H, device=DEV, generator=g).requires_grad_(True)
+    w = (torch.randn(O, C, ks, ks, device=DEV, generator=g) / 20).requires_grad_(True)
+    gout = torch.randn(B, O, H, H, device=DEV, generator=g)
+    ins = (x, off, ml, w)
+    out = core.deform_conv2d(x, off, ml, w, ks, 1, 1)
+    first = torch.autograd.grad(out, ins, gout, retain_graph=True)
+    second = torch.autograd.grad(out, ins, gout)
+    with torch.no_grad():
+        inf = core.deform_conv2d(x, off, ml, w, ks, 1, 1)
+    dims = (B, C, H, H, O, ks, 1, 1)
+    nb = L.lib().sbod_dcn_workspace_bytes(*dims)
+    ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    stateless = [torch.empty_like(t) for t in ins]
+    L.call('sbod_dcn_bwd_f32', *[L.ptr(t) for t in ins], L.ptr(gout), *dims, *[L.ptr(t) for t in stateless],
+           L.ptr(ws), nb, L.stream_of(gout))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(inf), _np(out), rtol=1e-5, atol=1e-6 * _amax(out), err_msg='inference fwd')
+    for n, a, b, c in zip(('x', 'offset', 'mask', 'weight'), first, second, stateless):
+        np.testing.assert_allclose(_np(b), _np(a), rtol=1e-5, atol=1e-6 * _amax(a), err_msg='retained ' + n)
+        np.testing.assert_allclose(_np(c), _np(a), rtol=1e-5, atol=1e-6 * _amax(a), err_msg='stateless ' + n)
