@@ -914,7 +914,7 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
                       hipStream_t hs) {
   const int64_t npix = static_cast<int64_t>(s.B) * s.H * s.W;
   const int HW = s.H * s.W;
-  hipLaunchKernelGGL(k_transpose, dim3((s.C + 63) / 64, (HW + 63) / 64, s.B), dim3(256), 0, hs, x, st.xt, s.C, HW,
+  hipLaunchKernelGGL(k_transpose, dim3((HW + 63) / 64, (s.C + 63) / 64, s.B), dim3(256), 0, hs, x, st.xt, s.C, HW,
                      train ? reinterpret_cast<float *>(st.tcount) : nullptr, train ? npix + 1 : 0);
   SBOD_LAUNCHED("k_transpose(x)");   // x [B][C][HW] -> xt [B][HW][C]
   const int64_t nc = static_cast<int64_t>(s.M) * s.N;
