@@ -192,6 +192,34 @@ def cpu_baseline(B, threads_all, det_images_one=8):
                            'detect_s': round(d_one, 3), 'detect_images': n_one}}
 
 
+def dcn_cpu_baseline(threads, H=64, B=4, C=256, O=256):
+    """The DCN leg of the CPU baseline (BASELINE.md's timed CPU path includes DeformConv2d): the
+    oracle (oracle/dcn_ref.py, the reference's forward restated in torch-CPU, autograd backward)
+    forward + the four input gradients on a bounded C4 sample (B images at HxH, 256 -> 256, 3x3,
+    modulated) on host cores; TF/s of the same three contractions the GPU figure counts.  Second
+    of two runs (the first warms the allocator / thread pool).  kind = 'port'."""
+    from oracle import dcn_ref as DR
+    g = torch.Generator().manual_seed(H)
+    x = torch.randn(B, C, H, H, generator=g).requires_grad_(True)
+    off = torch.randn(B, 18, H, H, generator=g).requires_grad_(True)
+    ml = torch.randn(B, 9, H, H, generator=g).requires_grad_(True)
+    w = (torch.randn(O, C, 3, 3, generator=g) / 48).requires_grad_(True)
+    gout = torch.randn(B, O, H, H, generator=g)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    ts = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        out = DR.deform_conv2d(x, off, torch.sigmoid(ml), w, 3, 1, 1)
+        torch.autograd.grad(out, (x, off, ml, w), gout)
+        ts.append(time.perf_counter() - t0)
+    torch.set_num_threads(prev)
+    fl = 3 * 2.0 * B * H * H * O * C * 9
+    return {'tflops': round(fl / ts[-1] / 1e12, 4), 'unit': 'TF/s', 'cores': threads, 'kind': 'port',
+            'sample': 'oracle DeformConv2d fwd + 4 input gradients, B=%d %dx%d 256->256 3x3 modulated: %.3f s '
+                      '(second of two runs)' % (B, H, H, ts[-1])}
+
+
 # ----------------------------------------------------------------------------- DCN (config C4)
 def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
     """DeformConv2d (a14) forward+backward at one of config C4's maps: TF/s of the three
@@ -744,6 +772,10 @@ def main():
                                         'mfma_frac': round(tot_tf / F32_MFMA_PEAK_TFS, 4)})
     if not a.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(B, min(os.cpu_count() or 1, 16))
+        if not a.no_dcn:   # the DCN leg: TF/s of the oracle beside the GPU figure in line['dcn']
+            line['cpu_baseline']['dcn'] = dcn_cpu_baseline(min(os.cpu_count() or 1, 16))
+            if 'dcn' in line:
+                line['dcn']['cpu_baseline_tflops'] = line['cpu_baseline']['dcn']['tflops']
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
