@@ -74,6 +74,10 @@ def parse(argv=None):
                     help='graph mode: which of the two streams gets the high HIP stream priority')
     ap.add_argument('--order', choices=('criterion_first', 'detect_first', 'detect_early'), default='criterion_first',
                     help='graph mode: which graph of a step is submitted first')
+    ap.add_argument('--crit-form', choices=('two', 'one'), default='two',
+                    help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
+    ap.add_argument('--det-form', choices=('two', 'one'), default='two',
+                    help='detect: per-class NMS and per-image merge as two launches or one (k_det_nms)')
     ap.add_argument('--det-streams', type=int, default=2,
                     help='graph mode: streams the detect graphs alternate over (1 = one detect stream)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -280,7 +284,7 @@ class Step:
     buffer and the two-deep pipeline (submit step k, then collect step k-1) needs no copies."""
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
-                 dtype=torch.float32, order='criterion_first', det_streams=2):
+                 dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two'):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -289,6 +293,8 @@ class Step:
                        cls_loss='focal', focal_type='softmax', model={'box_type': 'offset'})
         self.crit = CR.MultiBoxLoss512(priors_cxcy=self.priors, config=self.cfg)
         self.crit.distributed = world > 1
+        self.crit.one_launch = crit_form == 'one'
+        self.det_two_pass = det_form == 'two'
         self.batches = [Batch(B, 1000 * rank + 100 * i, dev, dtype) for i in range(max(1, n_batches))]
         cap = max(int(b.shape[0]) for bt in self.batches for b in bt.boxes)
         self.capacity = max(16, (cap + 15) // 16 * 16)
@@ -327,7 +333,8 @@ class Step:
 
     def detect(self, bt, capture):
         return core.detect(bt.locs.detach(), bt.det_scores, 0.01, 0.45, 200, self.priors,
-                           box_type='offset', act='softmax', async_=True, capture=capture)
+                           box_type='offset', act='softmax', async_=True, capture=capture,
+                           two_pass=self.det_two_pass)
 
     def body(self, bt, gt):
         """One stream, in stream order: criterion forward, detect (lists collected later),
@@ -616,7 +623,8 @@ def main():
     L.lib()
     B = a.batch
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
-              n_batches=a.batches, order=a.order, det_streams=a.det_streams)
+              n_batches=a.batches, order=a.order, det_streams=a.det_streams, crit_form=a.crit_form,
+              det_form=a.det_form)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -728,7 +736,7 @@ def main():
         'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
-        'detect_streams': len(st.det_streams),
+        'detect_streams': len(st.det_streams), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }

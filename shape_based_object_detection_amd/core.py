@@ -482,7 +482,8 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
         ws = workspace(nb, dev, 'criterion')
         zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion')
         _CLEAN.pop(ws.data_ptr(), None)
-        flags = (spec.flags & L.LOSS_FOCAL_NORM) | zflag | (L.CRIT_TWO_LAUNCH if two_launch else 0)
+        flags = ((spec.flags & (L.LOSS_FOCAL_NORM | L.LOSS_UNFUSED_FINISH)) | zflag |
+                 (L.CRIT_TWO_LAUNCH if two_launch else 0))
         L.call('sbod_criterion_focal', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy), L.ptr(pxy),
                L.ptr(gt.boxes), L.ptr(gt.labels), L.ptr(gt.offsets), gmax, float(threshold), float(neg_threshold),
                spec.reg, flags, float(spec.reg_weight), float(spec.alpha), float(spec.gamma), L.ptr(obj), L.ptr(ovl),
@@ -698,16 +699,23 @@ def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overl
     _CLEAN[ws.data_ptr()] = need
 
 
+# The per-class NMS and the per-image merge as two launches (k_det_segment_w4, k_det_merge with
+# its inline second window) or as one (k_det_nms, the image's last class merges): the default of
+# ``detect(two_pass=None)``, chosen by the same-box A/B in DESIGN.md round 4.
+DETECT_TWO_PASS = True
+
+
 def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='offset',
            act='softmax', pos_mask=None, final_nms=None, debug=False, window=0, async_=False,
-           capture=False, two_pass=False):
+           capture=False, two_pass=None):
     """Batched decode + per-class NMS + top-k.  Returns (boxes, labels, scores) lists of per-image
     tensors (views of batched device outputs).  ONE host sync: the per-image counts (waited on
     through an event).  ``async_=True`` returns a ``DetectHandle`` instead (``.wait()`` gives the
     lists), so a caller can overlap the detect kernels with later host work.  ``capture=True``
     (inside hipGraph capture) returns a persistent handle: call ``.replayed()`` after each replay,
-    then ``.wait()``.  ``two_pass`` keeps the per-class NMS and the per-image merge as two launches
-    (with the inline second window) where they would be one (A/B, tests)."""
+    then ``.wait()``.  ``two_pass`` (None: the module default
+    ``DETECT_TWO_PASS``) runs the per-class NMS and the per-image merge as two launches (with the
+    inline second window) or, False, as one (k_det_nms)."""
     L.require_device(locs, scores, what='detect')
     B, P, C = scores.shape
     if top_k <= 0:
@@ -722,7 +730,7 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
         sc = scores.contiguous().float()
         lc = locs if (locs.is_contiguous() and locs.dtype == torch.float32) else locs.contiguous().float()
         in_flags = 0
-    if two_pass:
+    if DETECT_TWO_PASS if two_pass is None else two_pass:
         in_flags |= L.DETECT_TWO_PASS
     pri = priors_cxcy.contiguous().float() if priors_cxcy is not None else None
     pm = pos_mask.contiguous().to(torch.uint8) if pos_mask is not None else None

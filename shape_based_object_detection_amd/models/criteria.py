@@ -56,7 +56,11 @@ class _AnchorCriterion(nn.Module):
         self.process_group = None
         self.grad_reduction = 'mean'
         self.force_collectives = False   # run the collectives even in a one-rank group (tests)
-        self.two_launch = False          # focal on one device: matcher and loss as two launches (A/B)
+        # focal on one device: the matcher and the loss pass as separate launches (default), or as
+        # ONE launch (opt-in: its workgroups wait for each other, so it needs the whole device —
+        # with kernels of other streams sharing the CUs the grid is not co-resident and the
+        # bounded wait ends in a NaN loss; measured slower alone too)
+        self.one_launch = False
         self.last_components = None
 
     def increase_threshold(self, increment=0.1):
@@ -103,10 +107,11 @@ class _AnchorCriterion(nn.Module):
         gt = core.pack_gt(boxes, labels)
         spec = self._spec()
         if spec.cls == L.CLS['focal'] and not self.distributed:
-            # one device, no mining: the matcher, the normaliser and the loss pass in one launch
+            # one device, no mining: the matcher and the loss pass in one C call (the matcher's
+            # launches then the loss launch; ONE launch with ``one_launch``)
             loss, comps, _ = core.criterion_focal(predicted_locs, predicted_scores, gt, self.priors_cxcy,
                                                   self.priors_xy, spec, self.threshold, self.threshold - 0.1,
-                                                  two_launch=self.two_launch)
+                                                  two_launch=not self.one_launch)
             self.last_components = comps
             return loss
         obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold)

@@ -105,14 +105,15 @@ def test_one_launch_forced_collisions():
 
 
 def test_criterion_class_uses_one_launch_and_captures():
-    """MultiBoxLoss512(focal) on one device takes the one-launch form; replayed from a hipGraph it
-    gives the eager results."""
+    """MultiBoxLoss512(focal) with ``one_launch`` set takes the one-launch form; replayed from a
+    hipGraph (nothing else running beside it) it gives the eager results."""
     P = torch.from_numpy(prior_table('SSD512')).to(DEV)
     B = 8
     boxes, labels = synth.make_gt(B, seed=77)
     locs, scores = synth.make_preds(B, P.shape[0], 21, seed=77)
     crit = CR.MultiBoxLoss512(priors_cxcy=P, config=Cfg(reg_weights=1.0, device=DEV, n_classes=21, reg_loss='diou',
                                                         cls_loss='focal'))
+    crit.one_launch = True   # opt-in (the default is the matcher and loss launches)
     bx, lb = [b.to(DEV) for b in boxes], [l.to(DEV) for l in labels]
     stage = core.GtStaging(B, 16, DEV)
     lo = locs.to(DEV).requires_grad_(True)

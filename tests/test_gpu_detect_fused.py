@@ -22,14 +22,14 @@ def test_one_launch_equals_two_launches(B, bg, top_k):
     P = torch.from_numpy(Pn).to(DEV)
     locs, scores = synth.make_preds(B, Pn.shape[0], 21, seed=100 + B, bg_shift=bg)
     l, s = locs.to(DEV), scores.to(DEV)
-    one = core.detect(l, s, 0.01, 0.45, top_k, P)
+    one = core.detect(l, s, 0.01, 0.45, top_k, P, two_pass=False)
     two = core.detect(l, s, 0.01, 0.45, top_k, P, two_pass=True)
     for a, b in zip(one, two):
         assert len(a) == len(b) == B
         for x, y in zip(a, b):
             assert torch.equal(x, y)
     if B <= 5:   # and the oracle on the kernels' own activations / decodes
-        (ob, ol, os_), probs, bxs = core.detect(l, s, 0.01, 0.45, top_k, P, debug=True)
+        (ob, ol, os_), probs, bxs = core.detect(l, s, 0.01, 0.45, top_k, P, debug=True, two_pass=False)
         rb, rl, rs = M.detect(probs.cpu().numpy(), bxs.cpu().numpy(), 0.01, 0.45, top_k, nms_variant='tv')
         for i in range(B):
             np.testing.assert_array_equal(ol[i].cpu().numpy(), rl[i])
@@ -44,7 +44,8 @@ def test_one_launch_counters_left_zero_and_repeatable():
     P = torch.from_numpy(Pn).to(DEV)
     locs, scores = synth.make_preds(6, Pn.shape[0], 21, seed=7, bg_shift=6.0)
     l, s = locs.to(DEV), scores.to(DEV)
-    res = [core.detect(l[:B].contiguous(), s[:B].contiguous(), 0.01, 0.45, 200, P) for B in (6, 3, 6)]
+    res = [core.detect(l[:B].contiguous(), s[:B].contiguous(), 0.01, 0.45, 200, P, two_pass=False)
+           for B in (6, 3, 6)]
     for a, b in zip(res[0], res[2]):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
@@ -65,9 +66,10 @@ def test_counter_prefix_clean_across_batch_sizes():
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        seq = [core.detect(l[:B].contiguous(), s[:B].contiguous(), 0.01, 0.45, 200, P) for B in (3, 6, 8)]
+        seq = [core.detect(l[:B].contiguous(), s[:B].contiguous(), 0.01, 0.45, 200, P, two_pass=tp)
+               for tp in (False, True) for B in (3, 6, 8)]
     torch.cuda.current_stream().wait_stream(side)
-    for B, got in zip((3, 6, 8), seq):
+    for B, got in zip((3, 6, 8) * 2, seq):
         fresh = torch.cuda.Stream()
         fresh.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(fresh):

@@ -213,8 +213,7 @@ def test_workspace_allocation_under_capture_refused():
 
 def test_graph_span_timing():
     """A timed kernel captured into a graph overwrites its own span record on every replay; the host
-    reads the latest launch without writing anything between replays.  (MultiBoxLoss512's focal
-    criterion on one device is the one-launch form, timed as k_criterion.)"""
+    reads the latest launch without writing anything between replays."""
     B = 4
     P, crit, locs, scores, det = _setup(B, seed=5)
     gt = _gt(B, 7)
@@ -227,7 +226,7 @@ def test_graph_span_timing():
             crit(locs, scores, stage.stage(*gt), None).backward()
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
-    L.timing_enable('k_criterion')
+    L.timing_enable('k_multibox')
     g = torch.cuda.CUDAGraph()
     locs.grad = None
     scores.grad = None
@@ -235,12 +234,12 @@ def test_graph_span_timing():
         loss = crit(locs, scores, stage.stage(*gt), None)
         loss.backward()
     L.timing_enable(None)
-    assert L.timing_query('k_criterion')[0] == 0          # never replayed yet
+    assert L.timing_query('k_multibox')[0] == 0          # never replayed yet
     times = []
     for _ in range(3):
         g.replay()
         torch.cuda.synchronize()
-        n, ms = L.timing_query('k_criterion')
+        n, ms = L.timing_query('k_multibox')
         assert n == 1
         times.append(ms)
     assert all(0.0005 < t < 5.0 for t in times), times
