@@ -906,7 +906,7 @@ class _DeformConv(torch.autograd.Function):
     A training forward (any input needs a gradient) runs ``sbod_dcn_fwd_train_f32`` into a
     per-call STATE buffer that autograd keeps until the backward: the coefficients, channels-last
     x, both weight layouts and the per-input-pixel sample counts, so ``sbod_dcn_bwd_state_f32``
-    re-derives none of them (five launches for all four gradients; the state is read-only there,
+    re-derives none of them (six launches for all four gradients; the state is read-only there,
     so a retained graph's second backward sees the same state).  An inference forward takes the
     forward-only workspace (no state kept)."""
 

@@ -8,7 +8,7 @@
 // (a permutation of conv.weight's c*N + n, applied to the weight copies below):
 //   forward      out[o, m]   = sum_K' Wf[o, K'] * cols[K', m]
 //   backward     dcols[m, c] = sum_o dout[o, m] * Wb[n, o, c]   (per n) -> dx, d_offset, d_mask
-//                dW[o,c,n]   = sum_m dout[o, m] * cols[(n,c), m]
+//                dWp[o,n,c]  = sum_m dout[o, m] * cols[(n,c), m]
 // cols[(n,c), m] = sigmoid(mask) * sum_q g_q * x[corner_q] is never materialised: it is built per
 // 32-channel K'-tile into LDS from per-(pixel, kernel point) coefficients computed once
 // (k_dcn_coef), reading x channels-last (xt) so the four corner gathers of a pixel are
@@ -567,8 +567,9 @@ __global__ __launch_bounds__(64 * kGxPix) void k_dcn_dx_gather(int C, int HW, in
 
 // ----------------------------------------------------------------------------- backward (weight)
 // Block: one kernel point n x 64 channels (blockIdx.x), a slice of pixels (blockIdx.y), 256
-// output channels (blockIdx.z): dW[o, c, n] += sum_m dout[o, m] cols[(n, c), m] (conv.weight's
-// own layout: no transpose after).  The mirror of
+// output channels (blockIdx.z): dWp[o, n, c] += sum_m dout[o, m] cols[(n, c), m], transposed to
+// conv.weight's [O][C][k][k] after (accumulating in that layout directly puts the 32 lanes of an
+// atomic on 32 lines, k² floats apart: the C4 8x8 backward took 0.31 ms instead of 0.17).  The mirror of
 // the forward kernel: dout rows go straight from HBM into the MFMA A registers (float4 when a
 // 32-pixel chunk never straddles two images), the columns are re-sampled channels-last into
 // double-buffered LDS, and the next chunk's gathers are in flight during the current MFMAs.
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.C + c) * s.N + n, acc[a][bq][r]);
+        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.N + n) * s.C + c, acc[a][bq][r]);
       }
     }
 }
@@ -821,10 +822,11 @@ struct DcnState {
   float *wb;          // training: Wb [N][O][C]
 };
 
-// Backward scratch (sbod_dcn_scratch_bytes): dcols rows [M][N][C], the per-input-pixel entry
-// cursors and entries of the dx gather, the scan's temporary storage.
+// Backward scratch (sbod_dcn_scratch_bytes): dcols rows [M][N][C], the weight-gradient
+// accumulator dWp [O][N][C], the per-input-pixel entry cursors and entries of the dx gather, the
+// scan's temporary storage.
 struct DcnScratch {
-  float *dcols;
+  float *dcols, *gwp;
   uint32_t *cur;
   DxEnt *ent;
   void *scan_tmp;
@@ -866,6 +868,7 @@ size_t carve_scratch(const DcnShape &s, void *base, DcnScratch *w) {
   const size_t npix = static_cast<size_t>(s.B) * s.H * s.W;
   DcnScratch t{};
   t.dcols = reinterpret_cast<float *>(take(rows * s.C * 4));
+  t.gwp = reinterpret_cast<float *>(take(static_cast<size_t>(s.O) * s.K * 4));
   t.cur = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
   t.ent = reinterpret_cast<DxEnt *>(take(rows * 4 * sizeof(DxEnt)));
   t.scan_bytes = dcn_scan_bytes(static_cast<int64_t>(npix) + 1);
@@ -947,7 +950,7 @@ static int dcn_forward(const DcnShape &s, const DcnState &st, float *out, int sp
 // The backward from a training state: with dx wanted, scan (the pixels' entry ranges) -> dx_fill
 // (which also zeroes the offset / mask / weight gradients) -> bwd_data (dcols rows) -> dx gather
 // (straight into [B][C][H][W]) -> bwd_weight (weight gradient into [O][C][k][k] and the offset /
-// mask gradients); five launches for all four gradients.
+// mask gradients) -> transpose of dWp; six launches for all four gradients.
 static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch &sc, const float *grad_out,
                         float *grad_x, float *grad_offset, float *grad_mask_logits, float *grad_weight, hipStream_t hs) {
   const int npix = s.B * s.H * s.W;
@@ -964,12 +967,12 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
       return launch_status("DeviceScan(dcn dx offsets)");
     hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hs, s, st.coef, sc.cur, sc.ent,
                        grad_offset, grad_offset ? 2 * ob : 0, grad_mask_logits, grad_mask_logits ? ob : 0,
-                       grad_weight, grad_weight ? wn : 0);
+                       grad_weight ? sc.gwp : nullptr, grad_weight ? wn : 0);
     SBOD_LAUNCHED("k_dcn_dx_fill");
   } else {
     if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob * 4, hs) != hipSuccess) return launch_status("memset");
     if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob * 4, hs) != hipSuccess) return launch_status("memset");
-    if (grad_weight && hipMemsetAsync(grad_weight, 0, wn * 4, hs) != hipSuccess) return launch_status("memset");
+    if (grad_weight && hipMemsetAsync(sc.gwp, 0, wn * 4, hs) != hipSuccess) return launch_status("memset");
   }
   if (need_cols) {
     KernelTimer kt("k_dcn_bwd_data", hs);
@@ -1006,7 +1009,7 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
     {
       KernelTimer kt("k_dcn_bwd_weight", hs);
       auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, dim3(kDcnThreads), 0, hs, s, st.xt, st.coef, grad_out, grad_weight, m_slice, dc,
+        hipLaunchKernelGGL(kern, grid, dim3(kDcnThreads), 0, hs, s, st.xt, st.coef, grad_out, grad_weight ? sc.gwp : nullptr, m_slice, dc,
                            grad_offset, grad_mask_logits);
       };
       if (dc) {
@@ -1020,6 +1023,11 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
       }
     }
     SBOD_LAUNCHED("k_dcn_bwd_weight");
+    if (grad_weight) {   // dWp [O][N][C] -> conv.weight's [O][C][N]
+      hipLaunchKernelGGL(k_transpose, dim3((s.C + 63) / 64, (s.N + 63) / 64, s.O), dim3(256), 0, hs, sc.gwp,
+                         grad_weight, s.N, s.C, nullptr, int64_t(0));
+      SBOD_LAUNCHED("k_transpose(dw)");
+    }
   }
   return SBOD_OK;
 }
