@@ -78,6 +78,8 @@ def parse(argv=None):
                     help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
     ap.add_argument('--det-form', choices=('two', 'one'), default='two',
                     help='detect: per-class NMS and per-image merge as two launches or one (k_det_nms)')
+    ap.add_argument('--crit-streams', type=int, default=2,
+                    help='graph mode: streams the criterion graphs alternate over (1 = one criterion stream)')
     ap.add_argument('--det-streams', type=int, default=2,
                     help='graph mode: streams the detect graphs alternate over (1 = one detect stream)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -279,12 +281,14 @@ class Step:
     """Criterion forward+backward and detect on one batch; eager or captured in hipGraphs.
 
     ``n_batches`` resident batches are rotated (step k uses batch k mod n): in graph mode each
-    batch has its own pair of graphs (criterion on ``cap_stream``, detect on ``det_stream``)
-    that own its gradients and detections, so consecutive steps never share an input or output
-    buffer and the two-deep pipeline (submit step k, then collect step k-1) needs no copies."""
+    batch has its own pair of graphs (criterion on criterion stream k mod ``crit_streams``, detect
+    on detect stream k mod ``det_streams``) and its own GT staging buffers, and the graphs own its
+    gradients and detections, so consecutive steps never share an input, output or workspace and
+    the two-deep pipeline (submit step k, then collect step k-1) needs no copies."""
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
-                 dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two'):
+                 dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
+                 crit_streams=2):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -298,14 +302,22 @@ class Step:
         self.batches = [Batch(B, 1000 * rank + 100 * i, dev, dtype) for i in range(max(1, n_batches))]
         cap = max(int(b.shape[0]) for bt in self.batches for b in bt.boxes)
         self.capacity = max(16, (cap + 15) // 16 * 16)
-        self.stage = core.GtStaging(B, self.capacity, dev)
+        # GT staging per resident batch: step k's packing never overwrites buffers that step k-1's
+        # criterion (possibly on the other criterion stream) is still reading
+        for bt in self.batches:
+            bt.stage = core.GtStaging(B, self.capacity, dev)
         # the warm-up runs on the capture streams, so every workspace the captured calls use
         # (cached per stream in core.workspace) already exists: nothing large is allocated
         # under capture.  Graph mode: the criterion and detect are two graphs replayed on two
         # streams, so their kernels (several latency-bound, few workgroups) run concurrently;
         # a fork/join INSIDE one graph costs ~30 us per edge on this runtime
         # (scripts/probe_graph_launch.py), two graphs on two streams need no edge at all.
-        self.cap_stream = torch.cuda.Stream(dev, priority=-1 if priority == 'criterion' else 0)
+        # criterion graphs alternate over `crit_streams` streams the same way (each stream has its
+        # own cached workspaces): step k's matcher need not wait for step k-1's loss pass
+        self.cap_streams = [torch.cuda.Stream(dev, priority=-1 if priority == 'criterion' else 0)
+                            for _ in range(max(1, crit_streams))]
+        self.cap_stream = self.cap_streams[0]
+        self._cap_warm = set()
         # detect graphs alternate over `det_streams` streams (batch i on stream i mod n): step k's
         # prepare need not wait for step k-1's segment / merge (latency-bound, few workgroups),
         # so the two overlap instead of the detect chain setting the step period
@@ -331,6 +343,12 @@ class Step:
         self.k += 1
         return bt
 
+    def cs_of(self, i):
+        return self.cap_streams[i % len(self.batches) % len(self.cap_streams)]
+
+    def ds_of(self, i):
+        return self.det_streams[i % len(self.batches) % len(self.det_streams)]
+
     def detect(self, bt, capture):
         return core.detect(bt.locs.detach(), bt.det_scores, 0.01, 0.45, 200, self.priors,
                            box_type='offset', act='softmax', async_=True, capture=capture,
@@ -348,7 +366,7 @@ class Step:
         bt = self._next_batch()
         bt.locs.grad = None
         bt.scores.grad = None
-        gt = self.stage.stage(bt.boxes, bt.labels)
+        gt = bt.stage.stage(bt.boxes, bt.labels)
         return self.body(bt, gt)
 
     def eager(self):
@@ -357,23 +375,25 @@ class Step:
 
     def eager_split(self):
         """The two-stream form eagerly (also warms both capture streams' workspaces): GT
-        packing, criterion forward and backward on cap_stream, detect on det_stream."""
+        packing, criterion forward and backward on the batch's criterion stream, detect on its
+        detect stream."""
         bt = self._next_batch()
         bt.locs.grad = None
         bt.scores.grad = None
-        ds = self.det_streams[(self.k - 1) % len(self.batches) % len(self.det_streams)]
-        self.cap_stream.wait_stream(torch.cuda.current_stream(self.dev))
+        cs, ds = self.cs_of(self.k - 1), self.ds_of(self.k - 1)
+        cs.wait_stream(torch.cuda.current_stream(self.dev))
         ds.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.stream(self.cap_stream):
-            gt = self.stage.stage(bt.boxes, bt.labels)
+        with torch.cuda.stream(cs):
+            gt = bt.stage.stage(bt.boxes, bt.labels)
             loss = self.crit(bt.locs, bt.scores, gt, None)
         with torch.cuda.stream(ds):
             h = self.detect(bt, False)
         self._det_warm.add(ds.cuda_stream)
-        with torch.cuda.stream(self.cap_stream):
+        with torch.cuda.stream(cs):
             loss.backward(self.one)
+        self._cap_warm.add(cs.cuda_stream)
         out = loss, h.wait()
-        torch.cuda.current_stream(self.dev).wait_stream(self.cap_stream)
+        torch.cuda.current_stream(self.dev).wait_stream(cs)
         return out
 
     def eager_half(self, part):
@@ -390,19 +410,27 @@ class Step:
                 self.detect(bt, False).wait()
             torch.cuda.current_stream(self.dev).wait_stream(ds)
             return
-        self.cap_stream.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.stream(self.cap_stream):
-            gt = self.stage.stage(bt.boxes, bt.labels)
+        cs = self.cs_of(self.k - 1)
+        cs.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(cs):
+            gt = bt.stage.stage(bt.boxes, bt.labels)
             loss = self.crit(bt.locs, bt.scores, gt, None)
             loss.backward(self.one)
-        torch.cuda.current_stream(self.dev).wait_stream(self.cap_stream)
+        torch.cuda.current_stream(self.dev).wait_stream(cs)
 
     def capture(self, after_first=None):
         """Capture one graph pair per resident batch (the usual torch pattern: warm-up already
         done on the capture streams; gradients set to None so the captured backward owns
         them).  ``after_first`` runs after the first batch's capture."""
-        gt = self.stage.stage(self.batches[0].boxes, self.batches[0].labels)
         n = len(self.batches)
+        for cs in self.cap_streams:   # every criterion stream's workspaces exist before capture
+            if cs.cuda_stream not in self._cap_warm:
+                bt = self.batches[0]
+                cs.wait_stream(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(cs):
+                    self.crit(bt.locs, bt.scores, bt.stage.stage(bt.boxes, bt.labels), None).backward(self.one)
+                torch.cuda.current_stream(self.dev).wait_stream(cs)
+                self._cap_warm.add(cs.cuda_stream)
         for ds in self.det_streams:   # every detect stream's workspace exists before capture
             if ds.cuda_stream not in self._det_warm:
                 ds.wait_stream(torch.cuda.current_stream(self.dev))
@@ -415,17 +443,19 @@ class Step:
         for bi, bt in enumerate(self.batches):
             bt.locs.grad = None
             bt.scores.grad = None
+            gt = bt.stage.stage(bt.boxes, bt.labels)   # the batch's own staging buffers
+            torch.cuda.synchronize()
             if self.two:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga, stream=self.cap_stream):
+                with torch.cuda.graph(ga, stream=self.cs_of(bi)):
                     loss = self.crit(bt.locs, bt.scores, gt, None)
                     loss.backward(self.one)
-                with torch.cuda.graph(gb, stream=self.det_streams[bi % len(self.det_streams)]):
+                with torch.cuda.graph(gb, stream=self.ds_of(bi)):
                     h = self.detect(bt, True)
                 self.slots.append((ga, gb, loss, h))
             else:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=self.cap_stream):
+                with torch.cuda.graph(g, stream=self.cs_of(bi)):
                     loss = self.crit(bt.locs, bt.scores, gt, None)
                     h = self.detect(bt, True)
                     loss.backward(self.one)
@@ -439,15 +469,15 @@ class Step:
         if self.two and L.host_ext is not None:
             self.fast = []
             for bi, (ga, gb, _, h) in enumerate(self.slots):
-                ds = self.det_streams[bi % len(self.det_streams)]
+                ds, cs = self.ds_of(bi), self.cs_of(bi)
                 h.replayed(ds)          # creates the event (recorded once here)
-                pairs = [(ga, self.cap_stream), (gb, ds)]
+                pairs = [(ga, cs), (gb, ds)]
                 if self.detect_first:
                     pairs.reverse()
                 early = None
                 if self.detect_early:   # the detect graph alone first, then packing + criterion
                     early = core.graph_launches([(gb, ds)])[0]
-                    pairs = [(ga, self.cap_stream)]
+                    pairs = [(ga, cs)]
                 self.fast.append((core.graph_launches(pairs), h._event.cuda_event, ds.cuda_stream, early))
             torch.cuda.synchronize()
         self.k = 0
@@ -462,19 +492,23 @@ class Step:
             launches, ev, ev_stream, early = self.fast[i]
             if early is not None:
                 L.call('sbod_graph_launch', early[0], early[1])
-            # GT packing on the criterion's stream, whichever graph is submitted first
-            if self.stage.stage_and_replay(bt.boxes, bt.labels, launches, ev, ev_stream,
-                                           pack_stream=self.cap_stream.cuda_stream) is not None:
+            # GT packing on the criterion's stream, whichever graph is submitted first.  The
+            # lists are resident device tensors written (and synchronised) before any step, so
+            # the packing needs no wait on the stream that made them (src_stream = its own)
+            cs = self.cs_of(i).cuda_stream
+            if bt.stage.stage_and_replay(bt.boxes, bt.labels, launches, ev, ev_stream, pack_stream=cs,
+                                         src_stream=cs) is not None:
                 return loss, h.rearmed()
+        cs = self.cs_of(i)
         if gb is None:
-            with torch.cuda.stream(self.cap_stream):
-                self.stage.stage(bt.boxes, bt.labels)
+            with torch.cuda.stream(cs):
+                bt.stage.stage(bt.boxes, bt.labels)
                 ga.replay()
-                return loss, h.replayed(self.cap_stream)
-        with torch.cuda.stream(self.cap_stream):
-            self.stage.stage(bt.boxes, bt.labels)
+                return loss, h.replayed(cs)
+        with torch.cuda.stream(cs):
+            bt.stage.stage(bt.boxes, bt.labels)
             ga.replay()
-        ds = self.det_streams[i % len(self.det_streams)]
+        ds = self.ds_of(i)
         with torch.cuda.stream(ds):
             gb.replay()
             return loss, h.replayed(ds)
@@ -624,7 +658,7 @@ def main():
     B = a.batch
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
               n_batches=a.batches, order=a.order, det_streams=a.det_streams, crit_form=a.crit_form,
-              det_form=a.det_form)
+              det_form=a.det_form, crit_streams=a.crit_streams)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -736,7 +770,7 @@ def main():
         'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
-        'detect_streams': len(st.det_streams), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
+        'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }

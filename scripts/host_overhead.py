@@ -45,12 +45,12 @@ def t(fn, n=N, sync_every=8):
 
 ga, gb, loss, h = st.slots[0]
 out = {}
-out['stage_device_lists'] = t(lambda: st.stage.stage(st.boxes, st.labels))
+out['stage_device_lists'] = t(lambda: st.batches[0].stage.stage(st.boxes, st.labels))
 out['as_rows'] = t(lambda: core._as_rows(st.boxes, st.labels))
 bx, lb, _ = core._as_rows(st.boxes, st.labels)
 counts = [b.shape[0] for b in st.boxes]
-out['launch_pack_only'] = t(lambda: core._launch_pack(bx, lb, counts, st.stage.boxes.shape[0], st.stage.boxes,
-                                                      st.stage.labels, st.stage.offsets))
+out['launch_pack_only'] = t(lambda: core._launch_pack(bx, lb, counts, st.batches[0].stage.boxes.shape[0], st.batches[0].stage.boxes,
+                                                      st.batches[0].stage.labels, st.batches[0].stage.offsets))
 out['graph_replay_criterion'] = t(ga.replay)
 out['graph_replay_detect'] = t(gb.replay)
 

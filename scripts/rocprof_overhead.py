@@ -59,7 +59,7 @@ def measure(out, reps=60, replays=300):
     L.timing_enable(None)
     # graph: [k_null, criterion] per resident batch, replayed back to back
     graphs = []
-    gt = st.stage.stage(st.batches[0].boxes, st.batches[0].labels)
+    gt = st.batches[0].stage.stage(st.batches[0].boxes, st.batches[0].labels)
     for bt in st.batches:
         bt.locs.grad = None
         bt.scores.grad = None

@@ -74,7 +74,7 @@ def main():
         hs.clear()
         ext = L.host_ext
         bt = st.batches[0]
-        stg = st.stage
+        stg = bt.stage
         res['pack_only'] = timed_idle(lambda: ext.pack_device_lists(
             bt.boxes, bt.labels, stg.boxes.shape[0], stg.capacity, 0, stg.boxes.data_ptr(), stg.labels.data_ptr(),
             stg.offsets.data_ptr(), st.cap_stream.cuda_stream, False), a.n)

@@ -176,7 +176,7 @@ class GtStaging:
         return GtPack(self.boxes, self.labels, self.offsets, counts, gmax=self.capacity)
 
     def stage_and_replay(self, boxes, labels, launches, event=0, event_stream=0, allow_empty=False,
-                         pack_stream=None):
+                         pack_stream=None, src_stream=None):
         """One-call submit of a captured step: ``stage`` of device lists on ``pack_stream`` (a raw
         hipStream_t; default the first launch's stream — the graph that reads the GT must be on
         it), then every (graph exec, stream) of ``launches`` (from ``graph_launches``), then
@@ -187,7 +187,9 @@ class GtStaging:
         Ordering: the lists may have been produced on the CURRENT stream (e.g. a non_blocking
         ``.to(device)``).  The packing stream waits for it first, and the current stream waits
         for the packing launch afterwards (not for the graphs), so the pack never reads a copy
-        in flight and the caching allocator cannot recycle the lists' memory under it."""
+        in flight and the caching allocator cannot recycle the lists' memory under it.
+        ``src_stream`` (a raw hipStream_t) names the stream the lists were produced on when it is
+        not the current one; passing the packing stream itself says they are ready (no wait)."""
         ext = L.host_ext
         if (ext is None or type(boxes) is not list or type(labels) is not list or not launches
                 or len(boxes) != self.batch or not boxes[0].is_cuda):
@@ -199,7 +201,8 @@ class GtStaging:
                                    self.labels.data_ptr(), self.offsets.data_ptr())
         r = ext.stage_and_replay(boxes, labels, fixed[0], fixed[1], fixed[2], fixed[3], fixed[4], fixed[5],
                                  pack_stream if pack_stream is not None else launches[0][1], allow_empty,
-                                 launches, event or None, event_stream or None, L._raw_stream(fixed[2]) or None)
+                                 launches, event or None, event_stream or None,
+                                 (src_stream if src_stream is not None else L._raw_stream(fixed[2])) or None)
         if r is None:
             return None
         if type(r) is int:

@@ -15,10 +15,8 @@
 // contiguous channel vectors, and it is shared by every output channel of the tile.
 // dx is a gather, not a scatter: the backward-data kernel writes the dcols rows, and one wave
 // per input pixel sums the rows whose bilinear corners land on it (lists built by a counting sort
-// on integer counters), channels-last, then transposed back.  Roofline: MFMA-bound (2*M*O*C*N
+// on integer counters), written back as NCHW rows.  Roofline: MFMA-bound (2*M*O*C*N
 // flops forward, 2x backward).
-#include <hipcub/hipcub.hpp>
-
 #include "sbod_common.h"
 
 namespace sbod {
@@ -466,6 +464,46 @@ __global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
 // counters, and k_dcn_dx_gather (one wave per input pixel) sums its rows in registers and stores
 // dx once: no float atomics (the per-pixel entry order is arbitrary; fp32 sums stay within the
 // tests' tolerance, as with the atomics they replace).
+// Exclusive scan of the per-input-pixel sample counts into the entry cursors, in ONE launch of one
+// 1024-thread block: each thread sums a contiguous segment (its loads independent, in flight
+// together), the block scans the 1024 sums (wave shuffles + 16 wave totals in LDS), and each
+// thread writes its segment's running offsets.  At C4's largest map (65,537 counters) that is 64
+// per thread; one block replaces the library scan's two launches.
+__global__ __launch_bounds__(1024) void k_dcn_scan(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int n) {
+  __shared__ uint32_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int per = (n + 1023) >> 10;
+  const int b0 = min(tid * per, n), b1 = min(b0 + per, n);
+  uint32_t sum = 0;
+#pragma unroll 8
+  for (int i = b0; i < b1; ++i) sum += in[i];
+  uint32_t incl = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  if (lane == 63) s_w[wv] = incl;
+  __syncthreads();
+  if (wv == 0) {
+    uint32_t w = lane < 16 ? s_w[lane] : 0u, wi = w;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      const uint32_t v = __shfl_up(wi, off, 64);
+      if (lane >= off) wi += v;
+    }
+    if (lane < 16) s_w[lane] = wi - w;   // exclusive: the waves before
+  }
+  __syncthreads();
+  uint32_t run = s_w[wv] + incl - sum;
+#pragma unroll 8
+  for (int i = b0; i < b1; ++i) {
+    const uint32_t c = in[i];
+    out[i] = run;
+    run += c;
+  }
+}
+
 struct DxEnt {
   uint32_t row;   // m * N + n
   float w;        // g_q * mask
@@ -823,24 +861,12 @@ struct DcnState {
 };
 
 // Backward scratch (sbod_dcn_scratch_bytes): dcols rows [M][N][C], the weight-gradient
-// accumulator dWp [O][N][C], the per-input-pixel entry cursors and entries of the dx gather, the
-// scan's temporary storage.
+// accumulator dWp [O][N][C], the per-input-pixel entry cursors and entries of the dx gather.
 struct DcnScratch {
   float *dcols, *gwp;
   uint32_t *cur;
   DxEnt *ent;
-  void *scan_tmp;
-  size_t scan_bytes;
 };
-
-size_t dcn_scan_bytes(int64_t n) {
-  size_t b = 0;
-  // size query only; a failed query makes the workspace requirement unsatisfiable (loud)
-  if (hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<uint32_t *>(nullptr), static_cast<uint32_t *>(nullptr),
-                                       static_cast<int>(n)) != hipSuccess)
-    return SIZE_MAX / 4;
-  return b;
-}
 
 size_t carve_state(const DcnShape &s, void *base, DcnState *w, bool train) {
   char *p = static_cast<char *>(base);
@@ -871,8 +897,6 @@ size_t carve_scratch(const DcnShape &s, void *base, DcnScratch *w) {
   t.gwp = reinterpret_cast<float *>(take(static_cast<size_t>(s.O) * s.K * 4));
   t.cur = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
   t.ent = reinterpret_cast<DxEnt *>(take(rows * 4 * sizeof(DxEnt)));
-  t.scan_bytes = dcn_scan_bytes(static_cast<int64_t>(npix) + 1);
-  t.scan_tmp = take(t.scan_bytes);
   if (w) *w = t;
   return off;
 }
@@ -962,9 +986,8 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
   const int64_t ob = static_cast<int64_t>(s.M) * s.N;
   const int64_t wn = static_cast<int64_t>(s.O) * s.K;
   if (grad_x) {   // the input pixels' entry ranges (scan of the counts the forward made)
-    size_t tb = sc.scan_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, tb, st.tcount, sc.cur, npix + 1, hs) != hipSuccess)
-      return launch_status("DeviceScan(dcn dx offsets)");
+    hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, hs, st.tcount, sc.cur, npix + 1);
+    SBOD_LAUNCHED("k_dcn_scan");
     hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hs, s, st.coef, sc.cur, sc.ent,
                        grad_offset, grad_offset ? 2 * ob : 0, grad_mask_logits, grad_mask_logits ? ob : 0,
                        grad_weight ? sc.gwp : nullptr, grad_weight ? wn : 0);
