@@ -34,6 +34,7 @@ RCCL communicator and overlapped with the step.
                     [--no-cpu-baseline] [--no-dcn]
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -78,6 +79,8 @@ def parse(argv=None):
                     help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
     ap.add_argument('--det-form', choices=('two', 'one'), default='two',
                     help='detect: per-class NMS and per-image merge as two launches or one (k_det_nms)')
+    ap.add_argument('--depth', type=int, default=2,
+                    help='graph mode: steps in flight (submit step k, then collect step k - depth + 1)')
     ap.add_argument('--crit-streams', type=int, default=2,
                     help='graph mode: streams the criterion graphs alternate over (1 = one criterion stream)')
     ap.add_argument('--det-streams', type=int, default=2,
@@ -288,7 +291,7 @@ class Step:
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
-                 crit_streams=2):
+                 crit_streams=2, depth=2):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -333,7 +336,8 @@ class Step:
         self.capture_error = None
         self.fast = None
         self.k = 0
-        self.pending = None
+        self.pending = collections.deque()
+        self.depth = max(2, int(depth))
         self.host_submit = self.host_collect = 0.0
         # the read-only unit upstream gradient: no ones-fill and no scale launch in the step
         self.one = core.unit_grad(dev)
@@ -481,7 +485,7 @@ class Step:
                 self.fast.append((core.graph_launches(pairs), h._event.cuda_event, ds.cuda_stream, early))
             torch.cuda.synchronize()
         self.k = 0
-        self.pending = None
+        self.pending.clear()
         self.host_submit = self.host_collect = 0.0
 
     def launch_replay(self):
@@ -518,25 +522,28 @@ class Step:
         return loss, h.wait()
 
     def pipelined(self):
-        """One step, pipelined two deep: launch step k (GT packing + graph replays), then collect
-        step k-1's per-image detection lists (its host sync overlaps step k on the GPU)."""
+        """One step, pipelined ``depth`` deep: launch step k (GT packing + graph replays), then
+        collect step k-depth+1's per-image detection lists (its host sync overlaps the steps
+        still on the GPU).  Returns that step's (loss, lists), or None while the pipe fills."""
         t0 = time.perf_counter()
         nxt = self.launch_replay()
         t1 = time.perf_counter()
         self.host_submit += t1 - t0
-        prev, self.pending = self.pending, nxt
-        if prev is not None:
+        self.pending.append(nxt)
+        if len(self.pending) >= self.depth:
+            prev = self.pending.popleft()
             out = prev[0], prev[1].wait()
             self.host_collect += time.perf_counter() - t1
             return out
         return None
 
     def drain(self):
-        """Collect the last launched step's detections."""
-        if self.pending is not None:
-            prev, self.pending = self.pending, None
-            return prev[0], prev[1].wait()
-        return None
+        """Collect every launched step not collected yet (oldest first)."""
+        out = []
+        while self.pending:
+            prev = self.pending.popleft()
+            out.append((prev[0], prev[1].wait()))
+        return out
 
     def __call__(self):
         return self.replay() if self.graph is not None else self.eager()
@@ -658,7 +665,7 @@ def main():
     B = a.batch
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
               n_batches=a.batches, order=a.order, det_streams=a.det_streams, crit_form=a.crit_form,
-              det_form=a.det_form, crit_streams=a.crit_streams)
+              det_form=a.det_form, crit_streams=a.crit_streams, depth=a.depth)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -770,7 +777,8 @@ def main():
         'step_GBps_algorithmic': round(step_bytes / (ms_step * 1e-3) / 1e9, 1),
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
-        'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
+        'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams),
+        'pipeline_depth': st.depth, 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }

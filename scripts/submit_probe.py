@@ -94,7 +94,7 @@ def main():
                 coll.append(time.perf_counter() - t)
         res['collect_ready'] = med(coll)
         # the pipelined step back to back
-        st.pending = None
+        st.pending.clear()
         for _ in range(20):
             st.pipelined()
         st.drain()

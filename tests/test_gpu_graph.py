@@ -247,16 +247,19 @@ def test_graph_span_timing():
     L.call('sbod_timing_reset_graphs')
 
 
-def test_bench_pipelined_step_equals_eager():
-    """bench.Step as the bench runs it: per-batch criterion graphs on one stream, detect graphs
-    alternating over two streams, submitted by the one-call C++ path, pipelined two deep, with the
-    criterion's stream current.  Every step's loss, gradients and per-image detections equal the
-    eager two-stream step on the same batch, across two rotations of the resident batches."""
+@pytest.mark.parametrize('depth', [2, 3])
+def test_bench_pipelined_step_equals_eager(depth):
+    """bench.Step as the bench runs it: per-batch criterion and detect graphs, each alternating over
+    two streams, submitted by the one-call C++ path with ``depth`` steps in flight and a criterion
+    stream current.  Every step's loss, gradients and
+    per-image detections equal the eager two-stream step on the same batch, across two rotations
+    of the resident batches."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    st = bench.Step(DEV, 4, 0, 1, graph=True, two_streams=True, priority='detect', n_batches=4, det_streams=2)
+    st = bench.Step(DEV, 4, 0, 1, graph=True, two_streams=True, priority='detect', n_batches=4, det_streams=2,
+                    crit_streams=2, depth=depth)
     ref = []
     for bt in st.batches:          # eager reference per batch (also warms both detect streams)
         loss, dets = st.eager_split()
@@ -272,7 +275,7 @@ def test_bench_pipelined_step_equals_eager():
             out = st.pipelined()
             if out is not None:
                 got.append(out)
-        got.append(st.drain())
+        got.extend(st.drain())
     torch.cuda.synchronize()
     assert len(got) == 2 * len(st.batches)
     for k, (loss, dets) in enumerate(got):
