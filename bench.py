@@ -435,7 +435,9 @@ class Step:
                     self.crit(bt.locs, bt.scores, bt.stage.stage(bt.boxes, bt.labels), None).backward(self.one)
                 torch.cuda.current_stream(self.dev).wait_stream(cs)
                 self._cap_warm.add(cs.cuda_stream)
-        for ds in self.det_streams:   # every detect stream's workspace exists before capture
+        # every detect stream's workspace exists before capture (one graph per step: detect runs
+        # on the criterion streams)
+        for ds in (self.det_streams if self.two else self.cap_streams):
             if ds.cuda_stream not in self._det_warm:
                 ds.wait_stream(torch.cuda.current_stream(self.dev))
                 with torch.cuda.stream(ds):
@@ -470,10 +472,14 @@ class Step:
         self.graph = self.slots[0][0]
         # raw handles for the one-call submit (C++: GT packing + both replays + detect event)
         self.fast = None
-        if self.two and L.host_ext is not None:
+        if L.host_ext is not None:
             self.fast = []
             for bi, (ga, gb, _, h) in enumerate(self.slots):
                 ds, cs = self.ds_of(bi), self.cs_of(bi)
+                if gb is None:          # one graph per step: criterion then detect on one stream
+                    h.replayed(cs)
+                    self.fast.append((core.graph_launches([(ga, cs)]), h._event.cuda_event, cs.cuda_stream, None))
+                    continue
                 h.replayed(ds)          # creates the event (recorded once here)
                 pairs = [(ga, cs), (gb, ds)]
                 if self.detect_first:

@@ -12,9 +12,10 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_graph.py -m gpu -x -v --tim
 out=gpurun_out/depth_ab_$TAG.jsonl
 : > $out
 for r in 1 2; do
-  for f in "2 1" "2 2" "3 1" "3 2" "4 2"; do
+  for f in "2 1 -" "2 2 -" "3 2 -" "4 2 -" "4 4 --one-stream"; do
     set -- $f
-    timeout -k 10 240 python -u bench.py --steps 400 --no-dcn --no-cpu-baseline --no-c2 --depth $1 --crit-streams $2 \
+    o=$3; [ "$o" = "-" ] && o=
+    timeout -k 10 240 python -u bench.py --steps 400 --no-dcn --no-cpu-baseline --no-c2 --depth $1 --crit-streams $2 $o \
         > gpurun_out/depth_bench.tmp 2>> gpurun_out/depth_ab_$TAG.err || exit 1
     tail -1 gpurun_out/depth_bench.tmp >> $out
   done

@@ -247,18 +247,18 @@ def test_graph_span_timing():
     L.call('sbod_timing_reset_graphs')
 
 
-@pytest.mark.parametrize('depth', [2, 3])
-def test_bench_pipelined_step_equals_eager(depth):
+@pytest.mark.parametrize('depth,two', [(2, True), (3, True), (3, False)])
+def test_bench_pipelined_step_equals_eager(depth, two):
     """bench.Step as the bench runs it: per-batch criterion and detect graphs, each alternating over
-    two streams, submitted by the one-call C++ path with ``depth`` steps in flight and a criterion
-    stream current.  Every step's loss, gradients and
+    two streams (or, ``two`` False, one graph per step holding both), submitted by the one-call C++
+    path with ``depth`` steps in flight and a criterion stream current.  Every step's loss, gradients and
     per-image detections equal the eager two-stream step on the same batch, across two rotations
     of the resident batches."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    st = bench.Step(DEV, 4, 0, 1, graph=True, two_streams=True, priority='detect', n_batches=4, det_streams=2,
+    st = bench.Step(DEV, 4, 0, 1, graph=True, two_streams=two, priority='detect', n_batches=4, det_streams=2,
                     crit_streams=2, depth=depth)
     ref = []
     for bt in st.batches:          # eager reference per batch (also warms both detect streams)
