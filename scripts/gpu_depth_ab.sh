@@ -21,4 +21,12 @@ for r in 1 2; do
   done
 done
 timeout -k 10 180 python -u scripts/submit_probe.py --out gpurun_out/submit_probe_$TAG.json > gpurun_out/submit_probe_$TAG.log 2>&1
-echo done
+# DCN: the tests, then the backward split by requested gradients (one kernel trace per subset)
+[ -n "$DCN" ] || { echo done; exit 0; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dcn.py -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/dcn_tests_$TAG.log 2>&1 || exit 1
+for v in all weight x om; do
+  timeout -k 10 120 rocprofv3 --kernel-trace -d gpurun_out/dv_${TAG}_$v -o run --output-format csv -- \
+      python3 scripts/dcn_variants.py $v > gpurun_out/dv_${TAG}_$v.log 2>&1 || exit 1
+done
+bash scripts/gpu_dcn_r4.sh $TAG nopmc

@@ -55,6 +55,49 @@ __device__ __forceinline__ void zero_fill(float *p, int64_t n) {
   for (int64_t i = 4 * n4 + id; i < n; i += nthr) p[i] = 0.f;
 }
 
+// Wave-aggregated increments of per-input-pixel counters: the 4 corner targets of every active
+// lane (ok[q] false: no sample) are grouped by value and each distinct target gets ONE atomic
+// add from a leader lane.  A wave's 64 (pixel, kernel point) samples land on ~40 distinct pixels
+// for 256 corners (neighbouring pixels' 3x3 neighbourhoods overlap), so the memory side sees ~6x
+// fewer same-address atomics.  With `slot`, each lane also gets the position of each of its
+// corners in the target's range: leader base + its rank among the group (corner-major within the
+// wave).  Must be called by the whole wave's active lanes together (ballots inside).
+template <bool kSlots>
+__device__ __forceinline__ void wave_agg_add(uint32_t *__restrict__ cnt, const uint32_t (&tg)[4], const bool (&ok)[4],
+                                             uint32_t (&slot)[4]) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  unsigned long long act[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) act[q] = __ballot(ok[q]);
+  while (act[0] | act[1] | act[2] | act[3]) {
+    const int q0 = act[0] ? 0 : act[1] ? 1 : act[2] ? 2 : 3;   // wave-uniform
+    const unsigned long long a0 = q0 == 0 ? act[0] : q0 == 1 ? act[1] : q0 == 2 ? act[2] : act[3];
+    const int l = __builtin_ctzll(a0);
+    const uint32_t mine = q0 == 0 ? tg[0] : q0 == 1 ? tg[1] : q0 == 2 ? tg[2] : tg[3];
+    const uint32_t t = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mine), l));
+    unsigned long long m[4];
+    uint32_t total = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      m[q] = __ballot(ok[q] && tg[q] == t) & act[q];
+      total += static_cast<uint32_t>(__popcll(m[q]));
+      act[q] &= ~m[q];
+    }
+    uint32_t base = 0;
+    if (lane == l) base = atomicAdd(cnt + t, total);
+    if constexpr (kSlots) {
+      base = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base), l));
+      uint32_t before = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if ((m[q] >> lane) & 1ull) slot[q] = base + before + static_cast<uint32_t>(__popcll(m[q] & lt));
+        before += static_cast<uint32_t>(__popcll(m[q]));
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__restrict__ offset,
                                                   const float *__restrict__ mlog,
                                                   Coef *__restrict__ coef, uint32_t *__restrict__ tcount,
@@ -103,10 +146,15 @@ __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__res
   c.inr = ((px >= 0.f && px <= hx) ? 1 : 0) | ((py >= 0.f && py <= hy) ? 2 : 0);
   coef[t] = c;
   if (tcount) {   // backward: how many corner samples land on each input pixel (dx gather lists)
-    const int64_t ib = static_cast<int64_t>(b) * s.H * s.W;
+    const uint32_t ib = static_cast<uint32_t>(b) * static_cast<uint32_t>(s.H * s.W);   // B*H*W < 2^31
+    uint32_t tg[4], unused[4];
+    bool ok[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (c.idx[q] >= 0) atomicAdd(tcount + ib + c.idx[q], 1u);
+    for (int q = 0; q < 4; ++q) {
+      ok[q] = c.idx[q] >= 0;
+      tg[q] = ib + static_cast<uint32_t>(max(c.idx[q], 0));
+    }
+    wave_agg_add<false>(tcount, tg, ok, unused);
   }
 }
 
@@ -520,15 +568,20 @@ __global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__r
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= static_cast<int64_t>(s.M) * s.N) return;
   const int m = static_cast<int>(t / s.N);
-  const int64_t ib = static_cast<int64_t>(m / (s.Ho * s.Wo)) * s.H * s.W;
+  const uint32_t ib = static_cast<uint32_t>(m / (s.Ho * s.Wo)) * static_cast<uint32_t>(s.H * s.W);
   const Coef cf = coef[t];
+  // cur starts at each pixel's first entry (exclusive scan of the counts) and ends at its last + 1
+  uint32_t tg[4], k[4];
+  bool ok[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    if (cf.idx[q] < 0) continue;
-    // cur starts at each pixel's first entry (exclusive scan of the counts) and ends at its last + 1
-    const uint32_t k = atomicAdd(cur + ib + cf.idx[q], 1u);
-    ent[k] = DxEnt{static_cast<uint32_t>(t), cf.g[q] * cf.mval};
+    ok[q] = cf.idx[q] >= 0;
+    tg[q] = ib + static_cast<uint32_t>(max(cf.idx[q], 0));
   }
+  wave_agg_add<true>(cur, tg, ok, k);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (ok[q]) ent[k[q]] = DxEnt{static_cast<uint32_t>(t), cf.g[q] * cf.mval};
 }
 
 // One wave per input pixel, kGxPix pixels per block; lanes hold 4 consecutive channels (C % 4 == 0)
