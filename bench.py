@@ -79,6 +79,8 @@ def parse(argv=None):
                     help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
     ap.add_argument('--det-form', choices=('two', 'one'), default='two',
                     help='detect: per-class NMS and per-image merge as two launches or one (k_det_nms)')
+    ap.add_argument('--submit', choices=('graph', 'direct'), default='graph',
+                    help='graph: replay captured hipGraphs; direct: issue the recorded entry-point calls')
     ap.add_argument('--depth', type=int, default=2,
                     help='graph mode: steps in flight (submit step k, then collect step k - depth + 1)')
     ap.add_argument('--crit-streams', type=int, default=2,
@@ -291,7 +293,7 @@ class Step:
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
-                 crit_streams=2, depth=2):
+                 crit_streams=2, depth=2, submit='graph'):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -338,6 +340,7 @@ class Step:
         self.k = 0
         self.pending = collections.deque()
         self.depth = max(2, int(depth))
+        self.submit = submit
         self.host_submit = self.host_collect = 0.0
         # the read-only unit upstream gradient: no ones-fill and no scale launch in the step
         self.one = core.unit_grad(dev)
@@ -451,6 +454,26 @@ class Step:
             bt.scores.grad = None
             gt = bt.stage.stage(bt.boxes, bt.labels)   # the batch's own staging buffers
             torch.cuda.synchronize()
+            if self.submit == 'direct':
+                # native submit: the step's entry-point calls recorded once (each with its own
+                # outputs, the streams' warm workspaces and zero-on-entry flags set), then issued
+                # again every step from the fast wrappers — the same launches a graph would replay,
+                # without the graph launch (scripts/submit_probe.py: hipGraphLaunch ~8 us each)
+                cs, ds = self.cs_of(bi), self.ds_of(bi)
+                crit_calls, det_calls = [], []
+                cs.wait_stream(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(cs), L.record_calls(crit_calls):
+                    loss = self.crit(bt.locs, bt.scores, gt, None)
+                    loss.backward(self.one)
+                ds.wait_stream(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(ds), L.record_calls(det_calls):
+                    h = self.detect(bt, True)     # persistent handle: its outputs are the slot's
+                torch.cuda.synchronize()
+                if any(n == 'sbod_gt_pack' for n, _ in crit_calls + det_calls) or not crit_calls or not det_calls:
+                    raise RuntimeError('direct submit: unexpected recorded calls %s'
+                                       % [n for n, _ in crit_calls + det_calls])
+                self.slots.append((crit_calls, det_calls, loss, h))
+                continue
             if self.two:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga, stream=self.cs_of(bi)):
@@ -472,7 +495,13 @@ class Step:
         self.graph = self.slots[0][0]
         # raw handles for the one-call submit (C++: GT packing + both replays + detect event)
         self.fast = None
-        if L.host_ext is not None:
+        if self.submit == 'direct':
+            if L.host_ext is None:
+                raise RuntimeError('direct submit needs the _sbodhost extension')
+            for bi, (_, _, _, h) in enumerate(self.slots):
+                h.replayed(self.ds_of(bi))   # creates the event (recorded once here)
+            torch.cuda.synchronize()
+        elif L.host_ext is not None:
             self.fast = []
             for bi, (ga, gb, _, h) in enumerate(self.slots):
                 ds, cs = self.ds_of(bi), self.cs_of(bi)
@@ -498,6 +527,20 @@ class Step:
         i = self.k % len(self.slots)
         bt = self._next_batch()
         ga, gb, loss, h = self.slots[i]
+        if self.submit == 'direct':
+            # GT packing (C++ list checks + one launch) on the criterion stream, the recorded
+            # criterion and detect calls on their streams, the detect event
+            cs, ds = self.cs_of(i).cuda_stream, self.ds_of(i).cuda_stream
+            stg = bt.stage
+            r = L.host_ext.pack_device_lists(bt.boxes, bt.labels, stg.boxes.shape[0], stg.capacity,
+                                             self.dev.index or 0, stg.boxes.data_ptr(), stg.labels.data_ptr(),
+                                             stg.offsets.data_ptr(), cs, False)
+            if type(r) is not list:
+                raise RuntimeError('direct submit: GT packing failed (%r)' % (r,))
+            L.replay_calls(ga)
+            L.replay_calls(gb)
+            L.call('sbod_event_record', h._event.cuda_event, ds)
+            return loss, h.rearmed()
         if self.fast is not None:
             launches, ev, ev_stream, early = self.fast[i]
             if early is not None:
@@ -671,7 +714,7 @@ def main():
     B = a.batch
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
               n_batches=a.batches, order=a.order, det_streams=a.det_streams, crit_form=a.crit_form,
-              det_form=a.det_form, crit_streams=a.crit_streams, depth=a.depth)
+              det_form=a.det_form, crit_streams=a.crit_streams, depth=a.depth, submit=a.submit)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -784,7 +827,7 @@ def main():
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
         'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams),
-        'pipeline_depth': st.depth, 'criterion_form': a.crit_form, 'detect_form': a.det_form,
+        'pipeline_depth': st.depth, 'submit': st.submit, 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }

@@ -178,8 +178,40 @@ def fastcall_names():
     return sorted(_fast)
 
 
+_recorder = []   # recording stack: (list to append (name, args) to) — see record_calls()
+
+
+def record_calls(into):
+    """Context manager: every sbod_* call made inside also appends (name, args) to ``into`` (and
+    still runs).  A caller can then replay the same launches with ``replay_calls`` — e.g. a
+    native-submit step: the calls' pointers (outputs, workspaces, streams) are the recording
+    call's, so the caller keeps those buffers alive and unchanged, as a captured graph would."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def cm():
+        _recorder.append(into)
+        try:
+            yield into
+        finally:
+            _recorder.pop()
+    return cm()
+
+
+def replay_calls(calls):
+    """Issue recorded (name, args) calls again, in order, through the fast wrappers."""
+    for name, args in calls:
+        f = _fast.get(name)
+        st = f(*args) if f is not None else getattr(lib(), name)(*args)
+        if st != 0:
+            msg = lib().sbod_last_error().decode(errors='replace')
+            raise SbodError('%s failed (%d): %s' % (name, st, msg))
+
+
 def call(name, *args):
     """Invoke an sbod_* entry point; raise SbodError with sbod_last_error() on failure."""
+    if _recorder:
+        _recorder[-1].append((name, args))
     f = _fast.get(name)
     st = f(*args) if f is not None else getattr(lib(), name)(*args)
     if st != 0:

@@ -17,6 +17,8 @@
 // per input pixel sums the rows whose bilinear corners land on it (lists built by a counting sort
 // on integer counters), written back as NCHW rows.  Roofline: MFMA-bound (2*M*O*C*N
 // flops forward, 2x backward).
+#include <hipcub/hipcub.hpp>
+
 #include "sbod_common.h"
 
 namespace sbod {
@@ -53,49 +55,6 @@ __device__ __forceinline__ void zero_fill(float *p, int64_t n) {
   float4 *p4 = reinterpret_cast<float4 *>(p);
   for (int64_t i = id; i < n4; i += nthr) p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t i = 4 * n4 + id; i < n; i += nthr) p[i] = 0.f;
-}
-
-// Wave-aggregated increments of per-input-pixel counters: the 4 corner targets of every active
-// lane (ok[q] false: no sample) are grouped by value and each distinct target gets ONE atomic
-// add from a leader lane.  A wave's 64 (pixel, kernel point) samples land on ~40 distinct pixels
-// for 256 corners (neighbouring pixels' 3x3 neighbourhoods overlap), so the memory side sees ~6x
-// fewer same-address atomics.  With `slot`, each lane also gets the position of each of its
-// corners in the target's range: leader base + its rank among the group (corner-major within the
-// wave).  Must be called by the whole wave's active lanes together (ballots inside).
-template <bool kSlots>
-__device__ __forceinline__ void wave_agg_add(uint32_t *__restrict__ cnt, const uint32_t (&tg)[4], const bool (&ok)[4],
-                                             uint32_t (&slot)[4]) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  unsigned long long act[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) act[q] = __ballot(ok[q]);
-  while (act[0] | act[1] | act[2] | act[3]) {
-    const int q0 = act[0] ? 0 : act[1] ? 1 : act[2] ? 2 : 3;   // wave-uniform
-    const unsigned long long a0 = q0 == 0 ? act[0] : q0 == 1 ? act[1] : q0 == 2 ? act[2] : act[3];
-    const int l = __builtin_ctzll(a0);
-    const uint32_t mine = q0 == 0 ? tg[0] : q0 == 1 ? tg[1] : q0 == 2 ? tg[2] : tg[3];
-    const uint32_t t = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mine), l));
-    unsigned long long m[4];
-    uint32_t total = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      m[q] = __ballot(ok[q] && tg[q] == t) & act[q];
-      total += static_cast<uint32_t>(__popcll(m[q]));
-      act[q] &= ~m[q];
-    }
-    uint32_t base = 0;
-    if (lane == l) base = atomicAdd(cnt + t, total);
-    if constexpr (kSlots) {
-      base = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base), l));
-      uint32_t before = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if ((m[q] >> lane) & 1ull) slot[q] = base + before + static_cast<uint32_t>(__popcll(m[q] & lt));
-        before += static_cast<uint32_t>(__popcll(m[q]));
-      }
-    }
-  }
 }
 
 __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__restrict__ offset,
@@ -146,15 +105,10 @@ __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__res
   c.inr = ((px >= 0.f && px <= hx) ? 1 : 0) | ((py >= 0.f && py <= hy) ? 2 : 0);
   coef[t] = c;
   if (tcount) {   // backward: how many corner samples land on each input pixel (dx gather lists)
-    const uint32_t ib = static_cast<uint32_t>(b) * static_cast<uint32_t>(s.H * s.W);   // B*H*W < 2^31
-    uint32_t tg[4], unused[4];
-    bool ok[4];
+    const int64_t ib = static_cast<int64_t>(b) * s.H * s.W;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ok[q] = c.idx[q] >= 0;
-      tg[q] = ib + static_cast<uint32_t>(max(c.idx[q], 0));
-    }
-    wave_agg_add<false>(tcount, tg, ok, unused);
+    for (int q = 0; q < 4; ++q)
+      if (c.idx[q] >= 0) atomicAdd(tcount + ib + c.idx[q], 1u);
   }
 }
 
@@ -515,8 +469,11 @@ __global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
 // Exclusive scan of the per-input-pixel sample counts into the entry cursors, in ONE launch of one
 // 1024-thread block: each thread sums a contiguous segment (its loads independent, in flight
 // together), the block scans the 1024 sums (wave shuffles + 16 wave totals in LDS), and each
-// thread writes its segment's running offsets.  At C4's largest map (65,537 counters) that is 64
-// per thread; one block replaces the library scan's two launches.
+// thread writes its segment's running offsets.  Used up to kScanOneBlock counters (8 per thread),
+// where it replaces the library scan's two launches; beyond, its per-thread segments are long
+// strided walks (C4 64x64: 36 us vs 2 x 4.8 us, profiles/r4_dcn_variants_b3) and hipCUB scans.
+constexpr int kScanOneBlock = 8192;
+
 __global__ __launch_bounds__(1024) void k_dcn_scan(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int n) {
   __shared__ uint32_t s_w[16];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -568,20 +525,15 @@ __global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__r
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= static_cast<int64_t>(s.M) * s.N) return;
   const int m = static_cast<int>(t / s.N);
-  const uint32_t ib = static_cast<uint32_t>(m / (s.Ho * s.Wo)) * static_cast<uint32_t>(s.H * s.W);
+  const int64_t ib = static_cast<int64_t>(m / (s.Ho * s.Wo)) * s.H * s.W;
   const Coef cf = coef[t];
-  // cur starts at each pixel's first entry (exclusive scan of the counts) and ends at its last + 1
-  uint32_t tg[4], k[4];
-  bool ok[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    ok[q] = cf.idx[q] >= 0;
-    tg[q] = ib + static_cast<uint32_t>(max(cf.idx[q], 0));
+    if (cf.idx[q] < 0) continue;
+    // cur starts at each pixel's first entry (exclusive scan of the counts) and ends at its last + 1
+    const uint32_t k = atomicAdd(cur + ib + cf.idx[q], 1u);
+    ent[k] = DxEnt{static_cast<uint32_t>(t), cf.g[q] * cf.mval};
   }
-  wave_agg_add<true>(cur, tg, ok, k);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (ok[q]) ent[k[q]] = DxEnt{static_cast<uint32_t>(t), cf.g[q] * cf.mval};
 }
 
 // One wave per input pixel, kGxPix pixels per block; lanes hold 4 consecutive channels (C % 4 == 0)
@@ -919,7 +871,19 @@ struct DcnScratch {
   float *dcols, *gwp;
   uint32_t *cur;
   DxEnt *ent;
+  void *scan_tmp;      // hipCUB scan storage (more than kScanOneBlock counters)
+  size_t scan_bytes;
 };
+
+size_t dcn_scan_bytes(int64_t n) {
+  if (n <= kScanOneBlock) return 0;
+  size_t b = 0;
+  // size query only; a failed query makes the workspace requirement unsatisfiable (loud)
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<uint32_t *>(nullptr), static_cast<uint32_t *>(nullptr),
+                                       static_cast<int>(n)) != hipSuccess)
+    return SIZE_MAX / 4;
+  return b;
+}
 
 size_t carve_state(const DcnShape &s, void *base, DcnState *w, bool train) {
   char *p = static_cast<char *>(base);
@@ -950,6 +914,8 @@ size_t carve_scratch(const DcnShape &s, void *base, DcnScratch *w) {
   t.gwp = reinterpret_cast<float *>(take(static_cast<size_t>(s.O) * s.K * 4));
   t.cur = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
   t.ent = reinterpret_cast<DxEnt *>(take(rows * 4 * sizeof(DxEnt)));
+  t.scan_bytes = dcn_scan_bytes(static_cast<int64_t>(npix) + 1);
+  t.scan_tmp = take(t.scan_bytes);
   if (w) *w = t;
   return off;
 }
@@ -1039,8 +1005,14 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
   const int64_t ob = static_cast<int64_t>(s.M) * s.N;
   const int64_t wn = static_cast<int64_t>(s.O) * s.K;
   if (grad_x) {   // the input pixels' entry ranges (scan of the counts the forward made)
-    hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, hs, st.tcount, sc.cur, npix + 1);
-    SBOD_LAUNCHED("k_dcn_scan");
+    if (npix + 1 <= kScanOneBlock) {
+      hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, hs, st.tcount, sc.cur, npix + 1);
+      SBOD_LAUNCHED("k_dcn_scan");
+    } else {
+      size_t tb = sc.scan_bytes;
+      if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, tb, st.tcount, sc.cur, npix + 1, hs) != hipSuccess)
+        return launch_status("DeviceScan(dcn dx offsets)");
+    }
     hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hs, s, st.coef, sc.cur, sc.ent,
                        grad_offset, grad_offset ? 2 * ob : 0, grad_mask_logits, grad_mask_logits ? ob : 0,
                        grad_weight ? sc.gwp : nullptr, grad_weight ? wn : 0);

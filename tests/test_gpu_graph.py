@@ -247,11 +247,13 @@ def test_graph_span_timing():
     L.call('sbod_timing_reset_graphs')
 
 
-@pytest.mark.parametrize('depth,two', [(2, True), (3, True), (3, False)])
-def test_bench_pipelined_step_equals_eager(depth, two):
+@pytest.mark.parametrize('depth,two,submit', [(2, True, 'graph'), (3, True, 'graph'), (3, False, 'graph'),
+                                               (4, True, 'direct')])
+def test_bench_pipelined_step_equals_eager(depth, two, submit):
     """bench.Step as the bench runs it: per-batch criterion and detect graphs, each alternating over
     two streams (or, ``two`` False, one graph per step holding both), submitted by the one-call C++
-    path with ``depth`` steps in flight and a criterion stream current.  Every step's loss, gradients and
+    path — or, ``submit='direct'``, the recorded entry-point calls issued again without graphs —
+    with ``depth`` steps in flight and a criterion stream current.  Every step's loss, gradients and
     per-image detections equal the eager two-stream step on the same batch, across two rotations
     of the resident batches."""
     import os
@@ -259,7 +261,7 @@ def test_bench_pipelined_step_equals_eager(depth, two):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     st = bench.Step(DEV, 4, 0, 1, graph=True, two_streams=two, priority='detect', n_batches=4, det_streams=2,
-                    crit_streams=2, depth=depth)
+                    crit_streams=2, depth=depth, submit=submit)
     ref = []
     for bt in st.batches:          # eager reference per batch (also warms both detect streams)
         loss, dets = st.eager_split()
