@@ -11,9 +11,15 @@ One step = one pass of the hot path over one batch of SSD512 synthetic input res
   3. detect on the same batch (softmax, offset decode + clamp, per-class NMS at IoU 0.45,
      min_score 0.01, top_k 200 — models.utils.detect's work) up to its per-image lists, which
      need one device->host sync.
-Steps 2-3 are captured into hipGraphs (criterion and detect, two streams) and replayed every
-step.  Every kernel still runs every step; the graph removes the per-launch host work.  ``--eager``
-runs the same calls without the graph; the line also carries the eager step time.
+Every kernel runs every step.  By default (``--submit direct``) the step's entry-point calls are
+recorded once per resident batch (its own outputs, the streams' warm workspaces) and issued
+again each step from the fast C wrappers; ``--submit graph`` captures them into hipGraphs
+(criterion and detect) and replays those instead (a hipGraphLaunch costs ~8 us of host time, two
+per step, more than the launches it replaces).  Criterion and detect each alternate over two
+streams, and ``--depth`` (default 4) steps are in flight: step k is submitted before step
+k-3's per-image lists are collected.  ``--eager`` runs the Python API calls every step; the line
+also carries the eager step time.  Data-parallel runs always replay graphs (the RCCL exchange of
+the loss normaliser is a torch.distributed call the recorder does not see).
 
 Inputs come from HBM, not from the 256 MiB Infinity Cache (MI355X_MICROARCH.md, "Infinity
 Cache": FETCH_SIZE and kernel time both count its hits): the bench holds ``--batches`` (default
@@ -79,9 +85,9 @@ def parse(argv=None):
                     help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
     ap.add_argument('--det-form', choices=('two', 'one'), default='two',
                     help='detect: per-class NMS and per-image merge as two launches or one (k_det_nms)')
-    ap.add_argument('--submit', choices=('graph', 'direct'), default='graph',
+    ap.add_argument('--submit', choices=('graph', 'direct'), default='direct',
                     help='graph: replay captured hipGraphs; direct: issue the recorded entry-point calls')
-    ap.add_argument('--depth', type=int, default=2,
+    ap.add_argument('--depth', type=int, default=4,
                     help='graph mode: steps in flight (submit step k, then collect step k - depth + 1)')
     ap.add_argument('--crit-streams', type=int, default=2,
                     help='graph mode: streams the criterion graphs alternate over (1 = one criterion stream)')
@@ -293,7 +299,7 @@ class Step:
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
-                 crit_streams=2, depth=2, submit='graph'):
+                 crit_streams=2, depth=4, submit='direct'):
         self.dev, self.B = dev, B
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -340,7 +346,9 @@ class Step:
         self.k = 0
         self.pending = collections.deque()
         self.depth = max(2, int(depth))
-        self.submit = submit
+        # the recorder sees sbod entry points only: with ranks, the normaliser's RCCL all-reduce
+        # (torch.distributed) must be in the replayed work, so data-parallel steps replay graphs
+        self.submit = submit if world == 1 else 'graph'
         self.host_submit = self.host_collect = 0.0
         # the read-only unit upstream gradient: no ones-fill and no scale launch in the step
         self.one = core.unit_grad(dev)
