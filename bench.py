@@ -506,8 +506,21 @@ class Step:
         if self.submit == 'direct':
             if L.host_ext is None:
                 raise RuntimeError('direct submit needs the _sbodhost extension')
-            for bi, (_, _, _, h) in enumerate(self.slots):
-                h.replayed(self.ds_of(bi))   # creates the event (recorded once here)
+            self.programs = []
+            for bi, (crit_calls, det_calls, _, h) in enumerate(self.slots):
+                ds, cs = self.ds_of(bi), self.cs_of(bi)
+                h.replayed(ds)   # creates the event (recorded once here)
+                prog = None
+                if (hasattr(L.host_ext, 'make_step_program') and len(crit_calls) == 1 and len(det_calls) == 1
+                        and crit_calls[0][0] == 'sbod_criterion_focal' and det_calls[0][0] == 'sbod_detect_f32'):
+                    # the whole submit in one native call (list checks + packing, the two recorded
+                    # entry points, the event)
+                    stg = self.batches[bi].stage
+                    prog = L.host_ext.make_step_program(
+                        (stg.boxes.shape[0], stg.capacity, self.dev.index or 0, stg.boxes.data_ptr(),
+                         stg.labels.data_ptr(), stg.offsets.data_ptr(), cs.cuda_stream),
+                        tuple(crit_calls[0][1]), tuple(det_calls[0][1]), h._event.cuda_event, ds.cuda_stream)
+                self.programs.append(prog)
             torch.cuda.synchronize()
         elif L.host_ext is not None:
             self.fast = []
@@ -536,6 +549,13 @@ class Step:
         bt = self._next_batch()
         ga, gb, loss, h = self.slots[i]
         if self.submit == 'direct':
+            prog = self.programs[i]
+            if prog is not None:
+                r = L.host_ext.submit_step_program(prog, bt.boxes, bt.labels)
+                if r is not True:
+                    raise RuntimeError('direct submit failed (%r): %s' % (
+                        r, L.lib().sbod_last_error().decode(errors='replace') if type(r) is int else 'lists'))
+                return loss, h.rearmed()
             # GT packing (C++ list checks + one launch) on the criterion stream, the recorded
             # criterion and detect calls on their streams, the detect event
             cs, ds = self.cs_of(i).cuda_stream, self.ds_of(i).cuda_stream

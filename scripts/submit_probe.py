@@ -53,7 +53,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
-    st = BM.Step(dev, a.B, 0, 1, graph=True, n_batches=6)
+    st = BM.Step(dev, a.B, 0, 1, graph=True, n_batches=6, submit='graph', depth=2)
     for _ in range(3):
         st.eager_split()
     torch.cuda.synchronize()

@@ -162,7 +162,157 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
   return counts_list(cnt);
 }
 
+// ---------------------------------------------------------------------------- step programs
+// A recorded step, submitted natively: the GT packing's fixed destination, the criterion's and
+// detect's entry-point calls with the arguments recorded from one eager call
+// (_lib.record_calls: their outputs, the streams' warm workspaces, the zero-on-entry flags), and
+// detect's event.  One C++ call per step then does the list checks + sbod_gt_pack,
+// sbod_criterion_focal, sbod_detect_f32 and sbod_event_record — what a hipGraph replay does,
+// without two hipGraphLaunch calls and without Python between the launches.
+//   make_step_program(pack, crit_args, det_args, event, event_stream) -> capsule
+//     pack = (capacity, per_image_cap, device, out_boxes, out_labels, out_offsets, stream);
+//     crit_args / det_args = the recorded argument tuples of sbod_criterion_focal /
+//     sbod_detect_f32 (include/sbod.h order; pointers as int or None).
+//   submit_step_program(capsule, boxes, labels) -> True | None | int
+//     None: the lists need the Python path (nothing launched); int: a failing sbod status.
+//   The lists are taken as ready on the packing stream (resident device tensors).
+struct StepProgram {
+  long long capacity, per_image;
+  int dev;
+  void *ob, *ol, *oo, *pack_stream;
+  // sbod_criterion_focal
+  const void *c_locs, *c_scores;
+  int c_dtype, c_B, c_P, c_C;
+  const float *c_pcxcy, *c_pxy, *c_gtb;
+  const int64_t *c_gtl;
+  const int32_t *c_gto;
+  int c_Gmax;
+  float c_thr, c_nthr;
+  int c_reg, c_flags;
+  float c_rw, c_fa, c_fg;
+  int32_t *c_obj;
+  float *c_ovl;
+  int32_t *c_npos;
+  void *c_gl, *c_gs;
+  float *c_out;
+  void *c_ws;
+  size_t c_wsb;
+  void *c_stream;
+  // sbod_detect_f32
+  void *d_locs;
+  const void *d_scores;
+  int d_B, d_P, d_C;
+  const float *d_pri;
+  const uint8_t *d_pm;
+  int d_box, d_act;
+  float d_min, d_ovl;
+  int d_topk;
+  float d_fnms;
+  int d_window, d_flags;
+  float *d_boxes;
+  int64_t *d_labels;
+  float *d_scores_out;
+  int32_t *d_count, *d_count_host;
+  float *d_dbg_p, *d_dbg_b;
+  void *d_ws;
+  size_t d_wsb;
+  void *d_stream;
+  void *event, *ev_stream;
+};
+
+struct ArgReader {   // the recorded tuple, item by item, in signature order
+  PyObject *t;
+  Py_ssize_t i = 0;
+  PyObject *next() { return i < PyTuple_GET_SIZE(t) ? PyTuple_GET_ITEM(t, i++) : nullptr; }
+  void *ptr() { PyObject *o = next(); return (o == nullptr || o == Py_None) ? nullptr : PyLong_AsVoidPtr(o); }
+  int i32() { PyObject *o = next(); return o ? static_cast<int>(PyLong_AsLong(o)) : 0; }
+  float f32() { PyObject *o = next(); return o ? static_cast<float>(PyFloat_AsDouble(o)) : 0.f; }
+  size_t sz() { PyObject *o = next(); return o ? PyLong_AsSize_t(o) : 0; }
+};
+
+void free_program(PyObject *cap) { delete static_cast<StepProgram *>(PyCapsule_GetPointer(cap, "sbod.StepProgram")); }
+
+PyObject *make_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
+  if (n != 5 || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) != 7 || !PyTuple_Check(a[1]) ||
+      PyTuple_GET_SIZE(a[1]) != 28 || !PyTuple_Check(a[2]) || PyTuple_GET_SIZE(a[2]) != 25) {
+    PyErr_SetString(PyExc_TypeError,
+                    "make_step_program(pack[7], criterion_focal args[28], detect_f32 args[25], event, event_stream)");
+    return nullptr;
+  }
+  auto *p = new StepProgram();
+  ArgReader k{a[0]};
+  p->capacity = PyLong_AsLongLong(k.next());
+  p->per_image = PyLong_AsLongLong(k.next());
+  p->dev = k.i32();
+  p->ob = k.ptr(); p->ol = k.ptr(); p->oo = k.ptr(); p->pack_stream = k.ptr();
+  ArgReader c{a[1]};
+  p->c_locs = c.ptr(); p->c_scores = c.ptr();
+  p->c_dtype = c.i32(); p->c_B = c.i32(); p->c_P = c.i32(); p->c_C = c.i32();
+  p->c_pcxcy = static_cast<const float *>(c.ptr()); p->c_pxy = static_cast<const float *>(c.ptr());
+  p->c_gtb = static_cast<const float *>(c.ptr()); p->c_gtl = static_cast<const int64_t *>(c.ptr());
+  p->c_gto = static_cast<const int32_t *>(c.ptr());
+  p->c_Gmax = c.i32(); p->c_thr = c.f32(); p->c_nthr = c.f32(); p->c_reg = c.i32(); p->c_flags = c.i32();
+  p->c_rw = c.f32(); p->c_fa = c.f32(); p->c_fg = c.f32();
+  p->c_obj = static_cast<int32_t *>(c.ptr()); p->c_ovl = static_cast<float *>(c.ptr());
+  p->c_npos = static_cast<int32_t *>(c.ptr()); p->c_gl = c.ptr(); p->c_gs = c.ptr();
+  p->c_out = static_cast<float *>(c.ptr()); p->c_ws = c.ptr(); p->c_wsb = c.sz(); p->c_stream = c.ptr();
+  ArgReader d{a[2]};
+  p->d_locs = d.ptr(); p->d_scores = d.ptr();
+  p->d_B = d.i32(); p->d_P = d.i32(); p->d_C = d.i32();
+  p->d_pri = static_cast<const float *>(d.ptr()); p->d_pm = static_cast<const uint8_t *>(d.ptr());
+  p->d_box = d.i32(); p->d_act = d.i32(); p->d_min = d.f32(); p->d_ovl = d.f32(); p->d_topk = d.i32();
+  p->d_fnms = d.f32(); p->d_window = d.i32(); p->d_flags = d.i32();
+  p->d_boxes = static_cast<float *>(d.ptr()); p->d_labels = static_cast<int64_t *>(d.ptr());
+  p->d_scores_out = static_cast<float *>(d.ptr()); p->d_count = static_cast<int32_t *>(d.ptr());
+  p->d_count_host = static_cast<int32_t *>(d.ptr()); p->d_dbg_p = static_cast<float *>(d.ptr());
+  p->d_dbg_b = static_cast<float *>(d.ptr()); p->d_ws = d.ptr(); p->d_wsb = d.sz(); p->d_stream = d.ptr();
+  p->event = opt_ptr(a[3]);
+  p->ev_stream = opt_ptr(a[4]);
+  if (PyErr_Occurred()) {
+    delete p;
+    return nullptr;
+  }
+  PyObject *cap = PyCapsule_New(p, "sbod.StepProgram", free_program);
+  if (!cap) delete p;
+  return cap;
+}
+
+PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
+  if (n != 3) {
+    PyErr_SetString(PyExc_TypeError, "submit_step_program(program, boxes, labels)");
+    return nullptr;
+  }
+  auto *p = static_cast<StepProgram *>(PyCapsule_GetPointer(a[0], "sbod.StepProgram"));
+  if (!p) return nullptr;
+  std::vector<int32_t> cnt;
+  const int r = pack_lists(a[1], a[2], p->capacity, p->per_image, p->dev, p->ob, p->ol, p->oo, p->pack_stream, 0,
+                           cnt, p->pack_stream);
+  if (r == 0) Py_RETURN_NONE;
+  if (r < 0) return PyLong_FromLong(r);
+  int st = sbod_criterion_focal(p->c_locs, p->c_scores, p->c_dtype, p->c_B, p->c_P, p->c_C, p->c_pcxcy, p->c_pxy,
+                                p->c_gtb, p->c_gtl, p->c_gto, p->c_Gmax, p->c_thr, p->c_nthr, p->c_reg, p->c_flags,
+                                p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl, p->c_gs, p->c_out,
+                                p->c_ws, p->c_wsb, p->c_stream);
+  if (st != SBOD_OK) return PyLong_FromLong(st);
+  st = sbod_detect_f32(p->d_locs, p->d_scores, p->d_B, p->d_P, p->d_C, p->d_pri, p->d_pm, p->d_box, p->d_act,
+                       p->d_min, p->d_ovl, p->d_topk, p->d_fnms, p->d_window, p->d_flags, p->d_boxes, p->d_labels,
+                       p->d_scores_out, p->d_count, p->d_count_host, p->d_dbg_p, p->d_dbg_b, p->d_ws, p->d_wsb,
+                       p->d_stream);
+  if (st != SBOD_OK) return PyLong_FromLong(st);
+  if (p->event) {
+    st = sbod_event_record(p->event, p->ev_stream);
+    if (st != SBOD_OK) return PyLong_FromLong(st);
+  }
+  Py_RETURN_TRUE;
+}
+
 PyMethodDef methods[] = {
+    {"make_step_program",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(make_step_program)),
+     METH_FASTCALL, "Parse a recorded step (GT packing target, criterion and detect calls, event) once."},
+    {"submit_step_program",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(submit_step_program)),
+     METH_FASTCALL, "GT packing + the recorded criterion and detect calls + the event, natively."},
     {"pack_device_lists",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(pack_device_lists)),
      METH_FASTCALL, "Check and pack per-image device GT lists with one sbod_gt_pack launch."},
