@@ -85,6 +85,9 @@ def parse(argv=None):
                     help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
     ap.add_argument('--det-form', choices=('two', 'one'), default='two',
                     help='detect: per-class NMS and per-image merge as two launches or one (k_det_nms)')
+    ap.add_argument('--hw-queues', type=int, default=None,
+                    help='HIP hardware queues per process (GPU_MAX_HW_QUEUES, <= 32; the runtime default is 4): '
+                         'more streams than queues share a queue and serialise')
     ap.add_argument('--submit', choices=('graph', 'direct'), default='direct',
                     help='graph: replay captured hipGraphs; direct: issue the recorded entry-point calls')
     ap.add_argument('--depth', type=int, default=4,
@@ -722,6 +725,8 @@ def grad_allreduce_figure(step, a, dist, dev, world):
 
 def main():
     a = parse()
+    if a.hw_queues is not None:   # before the first HIP call (torch initialises HIP lazily)
+        os.environ['GPU_MAX_HW_QUEUES'] = str(max(1, min(32, a.hw_queues)))
     if 'WORLD_SIZE' not in os.environ and a.gpus > 1:
         # one process per GPU: start the ranks now, before anything touches the GPU
         from shape_based_object_detection_amd.launch import spawn_ranks
@@ -855,7 +860,8 @@ def main():
         'step_hbm_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
         'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams),
-        'pipeline_depth': st.depth, 'submit': st.submit, 'criterion_form': a.crit_form, 'detect_form': a.det_form,
+        'pipeline_depth': st.depth, 'submit': st.submit,
+        'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
     }
