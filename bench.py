@@ -639,6 +639,19 @@ def c2_figure(dev, steps, warmup, B=16, n_batches=12):
     for _ in range(max(warmup - 1, 1)):
         st.eager_split()
     torch.cuda.synchronize()
+    # the bf16 criterion's loss-pass kernel, event-timed over eager criterion halves alone (as the
+    # headline roofline): locs + scores read and their gradients written at 2 B/element, the
+    # matcher's obj + overlap (8 B) read per anchor-image, the priors (16 B) once
+    st.eager_half('criterion')
+    torch.cuda.synchronize()
+    L.timing_enable('k_multibox')
+    for _ in range(12):
+        st.eager_half('criterion')
+    torch.cuda.synchronize()
+    n_mb, ms_mb = L.timing_query('k_multibox')
+    L.timing_enable(None)
+    mb_bytes = B * st.P * (2 * 2 * (4 + N_CLASSES) + 8) + 16 * st.P
+    mb_us = ms_mb * 1e3 / n_mb if n_mb else float('nan')
     st.capture()
     for _ in range(len(st.slots) + 1):
         st.replay()
@@ -656,7 +669,12 @@ def c2_figure(dev, steps, warmup, B=16, n_batches=12):
                       '(bf16 activations read in place), captured, %d resident batches' % (B, n_batches),
             'ms_per_step': round(ms, 4), 'images_per_s': round(B / (ms * 1e-3), 1),
             'criterion_algorithmic_bytes': crit_b, 'steps': steps,
-            'runs_ms_per_step': [round(r, 4) for r in runs]}
+            'runs_ms_per_step': [round(r, 4) for r in runs],
+            'roofline': {'bound': 'hbm', 'kernel': 'k_multibox<bf16>', 'avg_us': round(mb_us, 2),
+                         'launches_timed': n_mb, 'algorithmic_bytes_per_launch': mb_bytes,
+                         'achieved': round(mb_bytes / (mb_us * 1e-6) / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(mb_bytes / (mb_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                         'timing': 'HIP events attached to each dispatch, 12 eager criterion halves alone'}}
 
 
 def timed(fn, steps, dist, dev, per_step=None, finish=None):

@@ -37,7 +37,7 @@ def measure(out, reps=60, replays=300):
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     L.lib()
-    st = BM.Step(dev, 32, 0, 1, graph=False, n_batches=6)
+    st = BM.Step(dev, 32, 0, 1, graph=False, n_batches=6, submit='graph', depth=2)
     for _ in range(4):
         st.eager_half('criterion')
     torch.cuda.synchronize()
