@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build an A/B variant of libsbod_hip.so from THIS tree with extra compile flags into
+# shape_based_object_detection_amd/lib/variants/libsbod_hip_<name>.so (travels with the tree to
+# the GPU box; loaded only when SBOD_LIB names it).   EXTRA="-D..." bash scripts/build_lib_variant.sh NAME
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1
+OUT=gpurun_out/vbuild_$NAME
+LIBV=shape_based_object_detection_amd/lib/variants
+mkdir -p $OUT $LIBV
+for f in shape_based_object_detection_amd/csrc/*.hip; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -munsafe-fp-atomics $EXTRA \
+    -Iinclude -Ishape_based_object_detection_amd/csrc -c $f -o $OUT/$(basename $f).o &
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $LIBV/libsbod_hip_$NAME.so $OUT/*.o
+echo built $LIBV/libsbod_hip_$NAME.so

@@ -624,7 +624,10 @@ __global__ __launch_bounds__(64 * kGxPix) void k_dcn_dx_gather(int C, int HW, in
 constexpr int kWC = 64, kWMs = 32, kWLD = kWC + 2;
 
 template <int VEC, bool AVEC, bool DOFS>   // (the scalar-channel form needs more registers: one block per CU)
-__global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weight(
+#ifndef SBOD_DCN_WGRAD_WAVES
+#define SBOD_DCN_WGRAD_WAVES 2
+#endif
+__global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_WGRAD_WAVES : 1) void k_dcn_bwd_weight(
     DcnShape s, const float *__restrict__ xt, const Coef *__restrict__ coef,
     const float *__restrict__ gout, float *__restrict__ gwp, int m_slice,
     const float *__restrict__ dcols, float *__restrict__ goff, float *__restrict__ gmlog) {
@@ -793,7 +796,9 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
       const int mn = ms0 + min(i + 1, nch - 1) * kWMs;   // the last pass re-gathers its own chunk
       cf = cn;
       gather(mn, cf);
+#ifndef SBOD_DCN_WGRAD_SINGLE_A
       load_a(mn, anext);
+#endif
       cn = load_cf(ms0 + min(i + 2, nch - 1) * kWMs);
       __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
 #pragma unroll
@@ -806,11 +811,16 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? 2 : 1) void k_dcn_bwd_weigh
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[1][st], b1, acc[1][1], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
+#ifdef SBOD_DCN_WGRAD_SINGLE_A
+      load_a(mn, acur);   // (A/B variant) the next chunk's dout rows, once these MFMAs read theirs
+      store_cols(buf ^ 1, cf, mn, i + 1 < nch);
+#else
       store_cols(buf ^ 1, cf, mn, i + 1 < nch);
 #pragma unroll
       for (int ri = 0; ri < 2; ++ri)
 #pragma unroll
         for (int v = 0; v < 16; ++v) acur[ri][v] = anext[ri][v];
+#endif
       __syncthreads();
     }
   }
