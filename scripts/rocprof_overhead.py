@@ -6,7 +6,8 @@ the committed rocprofv3 traces report longer dispatches for the same kernel.  Th
 SAME measurements once plainly and once under the profiler, in one process layout:
 
   * eager: an empty kernel (k_null, one workgroup) and the criterion half of the bench step
-    (GT packing + the one-launch criterion), each dispatch carrying attached HIP events;
+    (GT packing + matcher + the fused loss pass k_multibox), each dispatch carrying attached HIP
+    events;
   * graph: one hipGraph per resident batch holding [k_null, criterion forward + backward],
     replayed back to back; the wall time per replay from HIP events around the whole run.
 
@@ -41,7 +42,7 @@ def measure(out, reps=60, replays=300):
     for _ in range(4):
         st.eager_half('criterion')
     torch.cuda.synchronize()
-    res = {'workload': 'SSD512 B=32 criterion half (GT packing + one-launch criterion fwd+bwd)'}
+    res = {'workload': 'SSD512 B=32 criterion half (GT packing + matcher + fused loss pass fwd+bwd)'}
     # eager, attached events
     s = st.cap_stream.cuda_stream
     L.timing_enable('k_null')
@@ -50,12 +51,12 @@ def measure(out, reps=60, replays=300):
     torch.cuda.synchronize()
     n, ms = L.timing_query('k_null')
     res['event_us'] = {'k_null': ms * 1e3 / n}
-    L.timing_enable('k_criterion')
+    L.timing_enable('k_multibox')
     for _ in range(reps):
         st.eager_half('criterion')
     torch.cuda.synchronize()
-    n, ms = L.timing_query('k_criterion')
-    res['event_us']['k_criterion'] = ms * 1e3 / n
+    n, ms = L.timing_query('k_multibox')
+    res['event_us']['k_multibox'] = ms * 1e3 / n
     L.timing_enable(None)
     # graph: [k_null, criterion] per resident batch, replayed back to back
     graphs = []
@@ -79,7 +80,7 @@ def measure(out, reps=60, replays=300):
             graphs[i % len(graphs)].replay()
         e1.record()
     torch.cuda.synchronize()
-    res['graph'] = {'replays': replays, 'dispatches_per_replay': 2,
+    res['graph'] = {'replays': replays, 'dispatches_per_replay': 4,
                     'us_per_replay': e0.elapsed_time(e1) * 1e3 / replays}
     with open(out, 'w') as f:
         json.dump(res, f, indent=1)
@@ -88,10 +89,11 @@ def measure(out, reps=60, replays=300):
 
 def combine(plain, prof, trace, out):
     a, b = json.load(open(plain)), json.load(open(prof))
-    durs = {'k_null': [], 'k_criterion': []}
+    durs = {'k_null': [], 'k_multibox': []}
     for r in csv.DictReader(open(trace)):
         name = r['Kernel_Name']
-        key = 'k_null' if 'k_null' in name else ('k_criterion' if ('k_multibox<' in name and 'true>' in name) else None)
+        key = ('k_null' if 'k_null' in name else
+               ('k_multibox' if ('k_multibox<float' in name and 'false>' in name) else None))
         if key and int(r['Grid_Size_Y']) in (1, 32):
             durs[key].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
     res = {'workload': a['workload'], 'kernels': {}}
@@ -103,7 +105,7 @@ def combine(plain, prof, trace, out):
     res['graph'] = {'us_per_replay_plain': round(ga['us_per_replay'], 3),
                     'us_per_replay_profiled': round(gb['us_per_replay'], 3),
                     'added_us_per_dispatch': round((gb['us_per_replay'] - ga['us_per_replay']) / per, 3)}
-    kc = res['kernels']['k_criterion']
+    kc = res['kernels']['k_multibox']
     if kc['trace_us']:
         kc['trace_over_event_plain'] = round(kc['trace_us'] / kc['event_us_plain'] - 1.0, 4)
     txt = json.dumps(res, indent=1)
