@@ -90,6 +90,9 @@ def parse(argv=None):
                          'more streams than queues share a queue and serialise')
     ap.add_argument('--submit', choices=('graph', 'direct'), default='direct',
                     help='graph: replay captured hipGraphs; direct: issue the recorded entry-point calls')
+    ap.add_argument('--gt-fold', type=int, choices=(0, 1), default=1,
+                    help='direct submit: 1 = the GT packing folded into the matcher\'s first launch '
+                         '(sbod_criterion_focal_lists), 0 = a separate sbod_gt_pack launch')
     ap.add_argument('--depth', type=int, default=4,
                     help='graph mode: steps in flight (submit step k, then collect step k - depth + 1)')
     ap.add_argument('--crit-streams', type=int, default=2,
@@ -302,8 +305,9 @@ class Step:
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
-                 crit_streams=2, depth=4, submit='direct'):
+                 crit_streams=2, depth=4, submit='direct', gt_fold=True):
         self.dev, self.B = dev, B
+        self.gt_fold = bool(gt_fold)
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
         self.priors = torch.from_numpy(Pn).to(dev)
@@ -522,7 +526,8 @@ class Step:
                     prog = L.host_ext.make_step_program(
                         (stg.boxes.shape[0], stg.capacity, self.dev.index or 0, stg.boxes.data_ptr(),
                          stg.labels.data_ptr(), stg.offsets.data_ptr(), cs.cuda_stream),
-                        tuple(crit_calls[0][1]), tuple(det_calls[0][1]), h._event.cuda_event, ds.cuda_stream)
+                        tuple(crit_calls[0][1]), tuple(det_calls[0][1]), h._event.cuda_event, ds.cuda_stream,
+                        self.gt_fold)
                 self.programs.append(prog)
             torch.cuda.synchronize()
         elif L.host_ext is not None:
@@ -765,7 +770,8 @@ def main():
     B = a.batch
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
               n_batches=a.batches, order=a.order, det_streams=a.det_streams, crit_form=a.crit_form,
-              det_form=a.det_form, crit_streams=a.crit_streams, depth=a.depth, submit=a.submit)
+              det_form=a.det_form, crit_streams=a.crit_streams, depth=a.depth, submit=a.submit,
+              gt_fold=a.gt_fold)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -879,6 +885,7 @@ def main():
         'graph': st.use_graph, 'stream_priority': a.priority, 'submit_order': a.order,
         'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams),
         'pipeline_depth': st.depth, 'submit': st.submit,
+        'gt_fold': st.gt_fold if st.submit == 'direct' else None,
         'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,

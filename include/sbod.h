@@ -140,6 +140,17 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
                    const float *arm_scores, int P, float threshold, float theta, int flags,
                    int32_t *obj, float *ovl, int32_t *n_pos, void *workspace,
                    size_t workspace_bytes, void *stream);
+/* The list form: sbod_gt_pack + sbod_match_f32 in the matcher's two launches.  The first launch
+ * reads each image's rows in place from the collate_fn lists (box_ptrs / label_ptrs / counts as
+ * for sbod_gt_pack: HOST arrays of device pointers, carried in the kernel arguments) and also
+ * writes them packed into gt_boxes / gt_labels / gt_offsets (capacity rows) for the loss pass
+ * that follows.  B <= 64; every image has 1..Gmax objects; boxes 16-B and labels 8-B aligned
+ * (what torch's allocator gives).  Callers with other batches use the two calls. */
+int sbod_match_lists_f32(const void *const *box_ptrs, const void *const *label_ptrs, const int32_t *counts,
+                         int64_t capacity, float *gt_boxes, int64_t *gt_labels, int32_t *gt_offsets, int B,
+                         int Gmax, const float *anchors, const float *priors_cxcy, const float *arm_scores, int P,
+                         float threshold, float theta, int flags, int32_t *obj, float *ovl, int32_t *n_pos,
+                         void *workspace, size_t workspace_bytes, void *stream);
 
 /* Expand matcher outputs to the reference's tensors (for parity tests and the iou_utils API):
  * cls [B,P] int64 (labels[obj], 0 where ovl < threshold; binary -> 0/1),
@@ -269,6 +280,18 @@ int sbod_criterion_focal(const void *locs, const void *scores, int dtype, int B,
                          float focal_gamma, int32_t *obj, float *ovl, int32_t *n_pos, void *grad_locs,
                          void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
                          void *stream);
+/* The focal criterion reading the collate_fn lists: sbod_gt_pack + sbod_criterion_focal's
+ * two-launch form (sbod_match_lists_f32, then the fused focal pass) — one launch fewer per step.
+ * List arguments and limits as sbod_match_lists_f32; gt_boxes / gt_labels / gt_offsets are the
+ * packed OUTPUT (capacity rows); the rest as sbod_criterion_focal (SBOD_CRIT_TWO_LAUNCH implied). */
+int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *label_ptrs, const int32_t *counts,
+                               int64_t capacity, const void *locs, const void *scores, int dtype, int B, int P,
+                               int C, const float *priors_cxcy, const float *priors_xy, float *gt_boxes,
+                               int64_t *gt_labels, int32_t *gt_offsets, int Gmax, float threshold,
+                               float neg_threshold, int reg, int flags, float reg_weight, float focal_alpha,
+                               float focal_gamma, int32_t *obj, float *ovl, int32_t *n_pos, void *grad_locs,
+                               void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
+                               void *stream);
 int sbod_criterion_status(const void *workspace, void *stream);
 
 /* grad *= (*scale) in place unless *scale == 1 (decided on the device: no host sync).

@@ -30,6 +30,8 @@ SIGNATURES = {
     'sbod_match_workspace_bytes': (SZ, [I32, I32]),
     'sbod_match_workspace_bytes_p': (SZ, [I32, I32, I32]),
     'sbod_match_f32': (I32, [P, P, P, I32, I32, P, P, P, I32, F32, F32, I32, P, P, P, P, SZ, P]),
+    'sbod_match_lists_f32': (I32, [P, P, P, I64, P, P, P, I32, I32, P, P, P, I32, F32, F32, I32, P, P, P, P, SZ,
+                                   P]),
     'sbod_match_expand_f32': (I32, [P, P, P, I32, P, P, P, P, I32, F32, F32, I32, P, P, P, P, P]),
     'sbod_match_ssd_workspace_bytes': (SZ, [I32, I32]),
     'sbod_match_ssd_f32': (I32, [P, P, I32, P, I32, F32, F32, F32, I32, P, P, P, SZ, P]),
@@ -43,6 +45,8 @@ SIGNATURES = {
     'sbod_criterion_zero_bytes': (SZ, [I32, I32, I32]),
     'sbod_criterion_focal': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32, I32, F32, F32, F32,
                                    P, P, P, P, P, P, P, SZ, P]),
+    'sbod_criterion_focal_lists': (I32, [P, P, P, I64, P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32,
+                                         I32, F32, F32, F32, P, P, P, P, P, P, P, SZ, P]),
     'sbod_criterion_status': (I32, [P, P]),
     'sbod_multibox_mine_global': (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, F32, P, I64, I64, P,
                                         P, P, SZ, P]),

@@ -17,14 +17,6 @@ namespace sbod {
 
 SBOD_STAMP_DECL
 
-constexpr int kPackImgs = 64;   // images per launch (kernel-argument table: 1,284 B)
-
-struct GtPackArgs {
-  const float *boxes[kPackImgs];
-  const int64_t *labels[kPackImgs];
-  int32_t off[kPackImgs + 1];    // destination row offsets of this chunk (absolute)
-};
-
 __global__ __launch_bounds__(64) void k_gt_pack(GtPackArgs a, int n_img, int last_chunk,
                                                 float *__restrict__ out_boxes,
                                                 int64_t *__restrict__ out_labels,

@@ -26,15 +26,24 @@
 
 namespace {
 
-// Checks the lists and launches sbod_gt_pack.  Returns 1 on success (cnt filled), 0 when the
-// batch needs the Python path (nothing launched), or a negative sbod status.
+// Row pointers of one checked batch (check_lists' output).
+struct ListRows {
+  std::vector<const void *> bp, lp;
+  std::vector<int32_t> cnt;
+};
+
+// Checks the lists and, with `launch`, launches sbod_gt_pack.  Returns 1 on success (rows
+// filled), 0 when the batch needs the Python path (nothing launched), or a negative sbod status.
 int pack_lists(PyObject *boxes, PyObject *labels, long long capacity, long long per_image,
                int want_dev, void *ob, void *ol, void *oo, void *stream, int allow_empty,
-               std::vector<int32_t> &cnt, void *src_stream) {
+               ListRows &rows, void *src_stream, bool launch = true) {
   if (!PyList_Check(boxes) || !PyList_Check(labels)) return 0;
   const Py_ssize_t B = PyList_GET_SIZE(boxes);
   if (B != PyList_GET_SIZE(labels) || B == 0) return 0;
-  std::vector<const void *> bp(B), lp(B);
+  std::vector<const void *> &bp = rows.bp, &lp = rows.lp;
+  std::vector<int32_t> &cnt = rows.cnt;
+  bp.assign(B, nullptr);
+  lp.assign(B, nullptr);
   cnt.assign(B, 0);
   long long total = 0;
   int dev = want_dev;
@@ -59,6 +68,7 @@ int pack_lists(PyObject *boxes, PyObject *labels, long long capacity, long long 
     total += g;
   }
   if (total > capacity) return 0;
+  if (!launch) return 1;
   if (src_stream != stream) {   // fork: the pack waits for the stream that produced the GT
     const int sw = sbod_stream_wait(stream, src_stream);
     if (sw != SBOD_OK) return sw;
@@ -90,12 +100,12 @@ PyObject *pack_device_lists(PyObject *, PyObject *const *a, Py_ssize_t n) {
   void *stream = opt_ptr(a[8]);
   const int allow_empty = PyObject_IsTrue(a[9]);
   if (PyErr_Occurred()) return nullptr;
-  std::vector<int32_t> cnt;
-  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, cnt,
+  ListRows rows;
+  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, rows,
                            stream);
   if (r == 0) Py_RETURN_NONE;
   if (r < 0) return PyLong_FromLong(r);
-  return counts_list(cnt);
+  return counts_list(rows.cnt);
 }
 
 // stage_and_replay(boxes, labels, capacity, per_image_cap, device, out_boxes, out_labels,
@@ -142,8 +152,8 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
     st[i] = opt_ptr(PyTuple_GET_ITEM(pr, 1));
   }
   if (PyErr_Occurred()) return nullptr;
-  std::vector<int32_t> cnt;
-  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, cnt,
+  ListRows rows;
+  const int r = pack_lists(a[0], a[1], capacity, per_image, want_dev, ob, ol, oo, stream, allow_empty, rows,
                            src_stream);
   if (r == 0) Py_RETURN_NONE;
   if (r < 0) return PyLong_FromLong(r);
@@ -159,7 +169,7 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
     const int s3 = sbod_event_record(event, ev_stream);
     if (s3 != SBOD_OK) return PyLong_FromLong(s3);
   }
-  return counts_list(cnt);
+  return counts_list(rows.cnt);
 }
 
 // ---------------------------------------------------------------------------- step programs
@@ -169,13 +179,16 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
 // detect's event.  One C++ call per step then does the list checks + sbod_gt_pack,
 // sbod_criterion_focal, sbod_detect_f32 and sbod_event_record — what a hipGraph replay does,
 // without two hipGraphLaunch calls and without Python between the launches.
-//   make_step_program(pack, crit_args, det_args, event, event_stream) -> capsule
+//   make_step_program(pack, crit_args, det_args, event, event_stream[, lists]) -> capsule
 //     pack = (capacity, per_image_cap, device, out_boxes, out_labels, out_offsets, stream);
 //     crit_args / det_args = the recorded argument tuples of sbod_criterion_focal /
 //     sbod_detect_f32 (include/sbod.h order; pointers as int or None).
 //   submit_step_program(capsule, boxes, labels) -> True | None | int
 //     None: the lists need the Python path (nothing launched); int: a failing sbod status.
-//   The lists are taken as ready on the packing stream (resident device tensors).
+//   The lists are taken as ready on the packing stream (resident device tensors), which is the
+//   criterion's stream.  With `lists` true the packing is folded into the matcher's first launch
+//   (sbod_criterion_focal_lists) whenever the batch allows it (<= 64 images, each 1..Gmax
+//   objects, aligned rows); other batches take sbod_gt_pack + sbod_criterion_focal.
 struct StepProgram {
   long long capacity, per_image;
   int dev;
@@ -218,6 +231,7 @@ struct StepProgram {
   size_t d_wsb;
   void *d_stream;
   void *event, *ev_stream;
+  bool lists;
 };
 
 struct ArgReader {   // the recorded tuple, item by item, in signature order
@@ -233,7 +247,7 @@ struct ArgReader {   // the recorded tuple, item by item, in signature order
 void free_program(PyObject *cap) { delete static_cast<StepProgram *>(PyCapsule_GetPointer(cap, "sbod.StepProgram")); }
 
 PyObject *make_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
-  if (n != 5 || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) != 7 || !PyTuple_Check(a[1]) ||
+  if ((n != 5 && n != 6) || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) != 7 || !PyTuple_Check(a[1]) ||
       PyTuple_GET_SIZE(a[1]) != 28 || !PyTuple_Check(a[2]) || PyTuple_GET_SIZE(a[2]) != 25) {
     PyErr_SetString(PyExc_TypeError,
                     "make_step_program(pack[7], criterion_focal args[28], detect_f32 args[25], event, event_stream)");
@@ -268,6 +282,7 @@ PyObject *make_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   p->d_dbg_b = static_cast<float *>(d.ptr()); p->d_ws = d.ptr(); p->d_wsb = d.sz(); p->d_stream = d.ptr();
   p->event = opt_ptr(a[3]);
   p->ev_stream = opt_ptr(a[4]);
+  p->lists = n == 6 && PyObject_IsTrue(a[5]) == 1;
   if (PyErr_Occurred()) {
     delete p;
     return nullptr;
@@ -284,15 +299,38 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   }
   auto *p = static_cast<StepProgram *>(PyCapsule_GetPointer(a[0], "sbod.StepProgram"));
   if (!p) return nullptr;
-  std::vector<int32_t> cnt;
+  ListRows rows;
   const int r = pack_lists(a[1], a[2], p->capacity, p->per_image, p->dev, p->ob, p->ol, p->oo, p->pack_stream, 0,
-                           cnt, p->pack_stream);
+                           rows, p->pack_stream, !p->lists);
   if (r == 0) Py_RETURN_NONE;
   if (r < 0) return PyLong_FromLong(r);
-  int st = sbod_criterion_focal(p->c_locs, p->c_scores, p->c_dtype, p->c_B, p->c_P, p->c_C, p->c_pcxcy, p->c_pxy,
-                                p->c_gtb, p->c_gtl, p->c_gto, p->c_Gmax, p->c_thr, p->c_nthr, p->c_reg, p->c_flags,
-                                p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl, p->c_gs, p->c_out,
-                                p->c_ws, p->c_wsb, p->c_stream);
+  bool folded = false;
+  if (p->lists) {
+    const size_t B = rows.cnt.size();
+    folded = B <= 64 && static_cast<int>(B) == p->c_B && p->ob == p->c_gtb && p->pack_stream == p->c_stream;
+    for (size_t i = 0; folded && i < B; ++i)
+      folded = rows.cnt[i] >= 1 && rows.cnt[i] <= p->c_Gmax &&
+               (reinterpret_cast<uintptr_t>(rows.bp[i]) & 15) == 0 && (reinterpret_cast<uintptr_t>(rows.lp[i]) & 7) == 0;
+    if (!folded) {   // this batch takes the packing launch
+      const int sp = sbod_gt_pack(rows.bp.data(), rows.lp.data(), rows.cnt.data(), static_cast<int>(B), p->capacity,
+                                  static_cast<float *>(p->ob), static_cast<int64_t *>(p->ol),
+                                  static_cast<int32_t *>(p->oo), p->pack_stream);
+      if (sp != SBOD_OK) return PyLong_FromLong(sp);
+    }
+  }
+  int st;
+  if (folded)
+    st = sbod_criterion_focal_lists(rows.bp.data(), rows.lp.data(), rows.cnt.data(), p->capacity, p->c_locs,
+                                    p->c_scores, p->c_dtype, p->c_B, p->c_P, p->c_C, p->c_pcxcy, p->c_pxy,
+                                    static_cast<float *>(p->ob), static_cast<int64_t *>(p->ol),
+                                    static_cast<int32_t *>(p->oo), p->c_Gmax, p->c_thr, p->c_nthr, p->c_reg,
+                                    p->c_flags, p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl,
+                                    p->c_gs, p->c_out, p->c_ws, p->c_wsb, p->c_stream);
+  else
+    st = sbod_criterion_focal(p->c_locs, p->c_scores, p->c_dtype, p->c_B, p->c_P, p->c_C, p->c_pcxcy, p->c_pxy,
+                              p->c_gtb, p->c_gtl, p->c_gto, p->c_Gmax, p->c_thr, p->c_nthr, p->c_reg, p->c_flags,
+                              p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl, p->c_gs, p->c_out,
+                              p->c_ws, p->c_wsb, p->c_stream);
   if (st != SBOD_OK) return PyLong_FromLong(st);
   st = sbod_detect_f32(p->d_locs, p->d_scores, p->d_B, p->d_P, p->d_C, p->d_pri, p->d_pm, p->d_box, p->d_act,
                        p->d_min, p->d_ovl, p->d_topk, p->d_fnms, p->d_window, p->d_flags, p->d_boxes, p->d_labels,

@@ -83,13 +83,12 @@ __device__ __forceinline__ void load_gt_tile(GtTile *s, const float *gt, int g0,
 // records, block barriers around it — spent ≈10-12 µs per launch at SSD512 B=32, most of it in
 // the barriers and the LDS table)
 template <bool kOdm, int kFlags>
-__global__ __launch_bounds__(kMThreads) void k_match_tile(
-    const float *__restrict__ gt, const int64_t *__restrict__ labels,
-    const int32_t *__restrict__ off, const float *__restrict__ anchors,
-    const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
-    float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
-    unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt, int32_t *__restrict__ npos,
-    int B, SpanRing *span) {
+__device__ __forceinline__ void match_tile_body(
+    const float *__restrict__ gt, const int64_t *__restrict__ labels, const int32_t *__restrict__ off, int g0_in,
+    int G_in, const float *__restrict__ anchors, const float *__restrict__ priors,
+    const float *__restrict__ arm_scores, int P, int Gmax, float thr, float theta, int32_t *__restrict__ obj,
+    float *__restrict__ ovl, unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt,
+    int32_t *__restrict__ npos, int B, SpanRing *span) {
   __shared__ __attribute__((aligned(16))) uint32_t s_od[kMThreads / 64][kSlots][64];   // per wave
   __shared__ int s_slot[kMThreads / 64][kSlots];
   STAMP_BEGIN();
@@ -101,7 +100,7 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile(
   // their atomics over kKeyShards words per object instead of queueing on one)
   unsigned long long *brow = best_key + (static_cast<int64_t>(b) * kKeyShards + (blockIdx.x & (kKeyShards - 1))) * Gmax;
   const MatchLane m = match_wave<kOdm, kFlags>(gt, labels, off, anchors, priors, arm_scores, P, b, wbase, brow,
-                                               s_od[wv], s_slot[wv]);
+                                               s_od[wv], s_slot[wv], g0_in, G_in);
   if (m.valid) {
     const int64_t i = static_cast<int64_t>(b) * P + m.p;
     obj[i] = m.bi;
@@ -113,6 +112,49 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile(
   if (lane == 0) wcnt[static_cast<int64_t>(b) * (gridDim.x * (kMThreads / 64)) + (wbase >> 6)] = n;
   span_end(span);
   STAMP_END(5, 1);
+}
+
+template <bool kOdm, int kFlags>
+__global__ __launch_bounds__(kMThreads) void k_match_tile(
+    const float *__restrict__ gt, const int64_t *__restrict__ labels,
+    const int32_t *__restrict__ off, const float *__restrict__ anchors,
+    const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
+    float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
+    unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt, int32_t *__restrict__ npos,
+    int B, SpanRing *span) {
+  match_tile_body<kOdm, kFlags>(gt, labels, off, -1, 0, anchors, priors, arm_scores, P, Gmax, thr, theta, obj, ovl,
+                                best_key, wcnt, npos, B, span);
+}
+
+// The list form (B <= kPackImgs): each image's rows are read in place from the collate_fn lists
+// (pointers and row offsets in the kernel arguments), and the image's first workgroup also writes
+// them packed (gt_boxes / gt_labels / gt_offsets) for k_match_final and the loss pass after this
+// launch — the separate sbod_gt_pack launch folded in.  Every image has >= 1 row, 16-B aligned.
+template <bool kOdm, int kFlags>
+__global__ __launch_bounds__(kMThreads) void k_match_tile_lists(
+    GtPackArgs lists, float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
+    int32_t *__restrict__ out_off, const float *__restrict__ anchors, const float *__restrict__ priors,
+    const float *__restrict__ arm_scores, int P, int Gmax, float thr, float theta, int32_t *__restrict__ obj,
+    float *__restrict__ ovl, unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt,
+    int32_t *__restrict__ npos, int B) {
+  const int b = blockIdx.y;
+  const int r0 = lists.off[b], G = lists.off[b + 1] - r0;
+  const float *gtb = lists.boxes[b];
+  const int64_t *lab = lists.labels[b];
+  if (blockIdx.x == 0) {   // the packed copy of this image's rows
+    const float4 *src = reinterpret_cast<const float4 *>(gtb);
+    float4 *dst = reinterpret_cast<float4 *>(out_boxes) + r0;
+    for (int g = threadIdx.x; g < G; g += kMThreads) {
+      dst[g] = src[g];
+      out_labels[r0 + g] = lab[g];
+    }
+    if (threadIdx.x == 0) {
+      out_off[b] = r0;
+      if (b == B - 1) out_off[B] = r0 + G;
+    }
+  }
+  match_tile_body<kOdm, kFlags>(gtb, lab, nullptr, 0, G, anchors, priors, arm_scores, P, Gmax, thr, theta, obj, ovl,
+                                best_key, wcnt, npos, B, nullptr);
 }
 
 // k_match_final: one workgroup per image; 64 threads when Gmax <= 64 (the register form),
@@ -327,25 +369,28 @@ int sbod_iou_pairwise_f32(const float *gt_boxes, const int32_t *gt_offsets, int 
   return SBOD_OK;
 }
 
-int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt_offsets,
-                   int B, int Gmax, const float *anchors, const float *priors_cxcy,
-                   const float *arm_scores, int P, float threshold, float theta, int flags,
-                   int32_t *obj, float *ovl, int32_t *n_pos, void *workspace,
-                   size_t workspace_bytes, void *stream) {
+}  // extern "C"
+
+namespace {
+// The matcher's two launches; `lists` non-null = the list form (k_match_tile_lists, which also
+// writes gt_boxes / gt_labels / gt_offsets).
+int match_run(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt_offsets, int B, int Gmax,
+              const float *anchors, const float *priors_cxcy, const float *arm_scores, int P, float threshold,
+              float theta, int flags, int32_t *obj, float *ovl, int32_t *n_pos, void *workspace,
+              size_t workspace_bytes, hipStream_t s, const GtPackArgs *lists, const char *who) {
   SBOD_REQUIRE(B > 0 && Gmax > 0 && P > 0 && gt_boxes && gt_labels && gt_offsets && anchors &&
                    obj && ovl && n_pos,
-               "sbod_match_f32: bad arguments (B=%d Gmax=%d P=%d)", B, Gmax, P);
-  SBOD_REQUIRE(Gmax <= 4096, "sbod_match_f32: Gmax %d > 4096 unsupported", Gmax);
+               "%s: bad arguments (B=%d Gmax=%d P=%d)", who, B, Gmax, P);
+  SBOD_REQUIRE(Gmax <= 4096, "%s: Gmax %d > 4096 unsupported", who, Gmax);
   SBOD_REQUIRE((flags & ~(SBOD_MATCH_BINARY | SBOD_MATCH_ODM | SBOD_MATCH_WS_ZEROED)) == 0,
-               "sbod_match_f32: unknown flags 0x%x", flags);
+               "%s: unknown flags 0x%x", who, flags);
   const bool odm = (flags & SBOD_MATCH_ODM) != 0;
-  SBOD_REQUIRE(!odm || (priors_cxcy && arm_scores), "sbod_match_f32: ODM needs priors and arm_scores");
+  SBOD_REQUIRE(!odm || (priors_cxcy && arm_scores), "%s: ODM needs priors and arm_scores", who);
   const size_t need = sbod_match_workspace_bytes_p(B, Gmax, P);
   if (workspace_bytes < need) {
-    set_error("sbod_match_f32: workspace %zu < %zu", workspace_bytes, need);
+    set_error("%s: workspace %zu < %zu", who, workspace_bytes, need);
     return SBOD_E_WORKSPACE;
   }
-  hipStream_t s = as_stream(stream);
   const int ntile = (P + kMThreads - 1) / kMThreads;
   MatchWs w = carve_match(workspace, B, Gmax, P);
   // the keys and counts must be zero on entry: every call leaves them so (k_match_final), so
@@ -354,19 +399,25 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
     return launch_status("hipMemsetAsync");
   dim3 grid(ntile, B);
   const int fthreads = Gmax <= 64 ? 64 : kFThreads;
-#define SBOD_MATCH(ODM, FL)                                                                     \
-  do {                                                                                          \
-    {                                                                                           \
-      KernelTimer kt("k_match_tile", s, true);                                                  \
-      tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads), 0, s, gt_boxes, gt_labels,     \
-              gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, ovl, \
-              w.best, w.wcnt, n_pos, B, kt.span());                                              \
-    }                                                                                           \
-    SBOD_LAUNCHED("k_match_tile");                                                              \
-    KernelTimer kt("k_match_final", s, true);                                                   \
-    tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(fthreads),                                   \
-            Gmax <= 64 ? 0 : static_cast<size_t>(Gmax) * 24, s, gt_labels, gt_offsets, w.best,  \
-            w.wcnt, w.nw, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B);           \
+#define SBOD_MATCH(ODM, FL)                                                                          \
+  do {                                                                                               \
+    if (lists) {                                                                                     \
+      hipLaunchKernelGGL((k_match_tile_lists<ODM, FL>), grid, dim3(kMThreads), 0, s, *lists,         \
+                         const_cast<float *>(gt_boxes), const_cast<int64_t *>(gt_labels),            \
+                         const_cast<int32_t *>(gt_offsets), anchors, priors_cxcy, arm_scores, P, Gmax, \
+                         threshold, theta, obj, ovl, w.best, w.wcnt, n_pos, B);                     \
+      SBOD_LAUNCHED("k_match_tile_lists");                                                           \
+    } else {                                                                                         \
+      KernelTimer kt("k_match_tile", s, true);                                                       \
+      tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads), 0, s, gt_boxes, gt_labels,          \
+              gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, ovl,      \
+              w.best, w.wcnt, n_pos, B, kt.span());                                                   \
+      SBOD_LAUNCHED("k_match_tile");                                                                 \
+    }                                                                                                \
+    KernelTimer kt("k_match_final", s, true);                                                        \
+    tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(fthreads),                                        \
+            Gmax <= 64 ? 0 : static_cast<size_t>(Gmax) * 24, s, gt_labels, gt_offsets, w.best,       \
+            w.wcnt, w.nw, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B);                \
   } while (0)
   if (odm)
     SBOD_MATCH(true, SBOD_MATCH_ODM);
@@ -377,6 +428,48 @@ int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_
 #undef SBOD_MATCH
   SBOD_LAUNCHED("k_match_final");
   return SBOD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sbod_match_f32(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt_offsets,
+                   int B, int Gmax, const float *anchors, const float *priors_cxcy,
+                   const float *arm_scores, int P, float threshold, float theta, int flags,
+                   int32_t *obj, float *ovl, int32_t *n_pos, void *workspace,
+                   size_t workspace_bytes, void *stream) {
+  return match_run(gt_boxes, gt_labels, gt_offsets, B, Gmax, anchors, priors_cxcy, arm_scores, P, threshold,
+                   theta, flags, obj, ovl, n_pos, workspace, workspace_bytes, as_stream(stream), nullptr,
+                   "sbod_match_f32");
+}
+
+int sbod_match_lists_f32(const void *const *box_ptrs, const void *const *label_ptrs, const int32_t *counts,
+                         int64_t capacity, float *gt_boxes, int64_t *gt_labels, int32_t *gt_offsets, int B,
+                         int Gmax, const float *anchors, const float *priors_cxcy, const float *arm_scores, int P,
+                         float threshold, float theta, int flags, int32_t *obj, float *ovl, int32_t *n_pos,
+                         void *workspace, size_t workspace_bytes, void *stream) {
+  SBOD_REQUIRE(B > 0 && B <= kPackImgs && box_ptrs && label_ptrs && counts,
+               "sbod_match_lists_f32: bad arguments (B=%d, at most %d images)", B, kPackImgs);
+  GtPackArgs a;
+  int64_t row = 0;
+  for (int i = 0; i < B; ++i) {
+    SBOD_REQUIRE(counts[i] >= 1 && counts[i] <= Gmax,
+                 "sbod_match_lists_f32: image %d has %d objects (1..Gmax=%d)", i, counts[i], Gmax);
+    SBOD_REQUIRE(box_ptrs[i] && label_ptrs[i] && (reinterpret_cast<uintptr_t>(box_ptrs[i]) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(label_ptrs[i]) & 7) == 0,
+                 "sbod_match_lists_f32: image %d: null or misaligned rows", i);
+    a.boxes[i] = static_cast<const float *>(box_ptrs[i]);
+    a.labels[i] = static_cast<const int64_t *>(label_ptrs[i]);
+    a.off[i] = static_cast<int32_t>(row);
+    row += counts[i];
+  }
+  a.off[B] = static_cast<int32_t>(row);
+  SBOD_REQUIRE(row <= capacity, "sbod_match_lists_f32: %lld objects exceed the capacity %lld",
+               static_cast<long long>(row), static_cast<long long>(capacity));
+  SBOD_REQUIRE(reinterpret_cast<uintptr_t>(gt_boxes) % 16 == 0, "sbod_match_lists_f32: gt_boxes not 16-B aligned");
+  return match_run(gt_boxes, gt_labels, gt_offsets, B, Gmax, anchors, priors_cxcy, arm_scores, P, threshold,
+                   theta, flags, obj, ovl, n_pos, workspace, workspace_bytes, as_stream(stream), &a,
+                   "sbod_match_lists_f32");
 }
 
 int sbod_match_expand_f32(const float *gt_boxes, const int64_t *gt_labels,

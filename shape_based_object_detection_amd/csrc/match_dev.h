@@ -92,7 +92,8 @@ __device__ __forceinline__ MatchLane match_wave(const float *__restrict__ gt, co
                                                 const int32_t *__restrict__ off, const float *__restrict__ anchors,
                                                 const float *__restrict__ priors,
                                                 const float *__restrict__ arm_scores, int P, int b, int wbase,
-                                                unsigned long long *brow, uint32_t (*s_od)[64], int *s_slot) {
+                                                unsigned long long *brow, uint32_t (*s_od)[64], int *s_slot,
+                                                int g0_in = -1, int G_in = 0) {
   const int lane = threadIdx.x & 63;
   const int p = wbase + lane;
   const bool valid = p < P;
@@ -102,7 +103,10 @@ __device__ __forceinline__ MatchLane match_wave(const float *__restrict__ gt, co
   const int pc = min(p, P - 1);
   const Box4 araw = ld4(kOdm ? anchors + 4 * (static_cast<int64_t>(b) * P + pc) : anchors + 4 * static_cast<int64_t>(pc));
   const Box4 apri = kOdm ? ld4(priors + 4 * pc) : Box4{0.f, 0.f, 0.f, 0.f};
-  const int g0 = ld_i32_uniform(off + b), G = ld_i32_uniform(off + b + 1) - g0;
+  // the image's object rows: [off[b], off[b+1]) of the packed buffers, or (g0_in >= 0) the
+  // G_in rows the caller points gt / labels at (an image's own list, read in place)
+  const int g0 = g0_in >= 0 ? g0_in : ld_i32_uniform(off + b);
+  const int G = g0_in >= 0 ? G_in : ld_i32_uniform(off + b + 1) - g0;
   const bool has = G > 0;
   GtLane o = load_gt_lane<kFlags>(gt, labels, has ? g0 : 0, 0, has ? min(G, 64) : 1, lane);
   float eas0 = 0.f, eas1 = 0.f;

@@ -298,6 +298,16 @@ __device__ __forceinline__ uint32_t ld_wt_u32(const int32_t *p) {
 // Wait for every outstanding vector-memory operation of the calling wave (stores acknowledged,
 // atomics performed) with a compiler memory barrier: no memory access moves across it (a bare
 // __builtin_amdgcn_s_waitcnt is not a compiler barrier).
+// Per-image ground-truth lists travelling in kernel arguments (the collate_fn batch, one device
+// tensor pair per image): k_gt_pack copies them into the packed layout, the list form of the
+// matcher reads them in place.  kPackImgs images per launch (1,284 B of kernel arguments).
+constexpr int kPackImgs = 64;
+struct GtPackArgs {
+  const float *boxes[kPackImgs];
+  const int64_t *labels[kPackImgs];
+  int32_t off[kPackImgs + 1];    // destination row offsets (absolute)
+};
+
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kCpolSc1 = 16;   // gfx950 cache-policy bit SC1 in the buffer intrinsics' aux word
