@@ -66,19 +66,39 @@ __device__ __forceinline__ void tile_load(float *__restrict__ dst, const uint16_
     for (int i = threadIdx.x; i < n; i += nt) dst[i] = ldf(src + i);
   }
 }
-__device__ __forceinline__ void tile_store(float *dst, const float *src, int n) {
+// LDS -> global, threads [t0, t0 + nt) of the workgroup (the others return at once).
+__device__ __forceinline__ void tile_store(float *dst, const float *src, int n, int t0, int nt) {
+  const int t = static_cast<int>(threadIdx.x) - t0;
+  if (t < 0) return;
   if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
     const int n4 = n >> 2;
     float4 *d4 = reinterpret_cast<float4 *>(dst);
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) st4_nt(reinterpret_cast<float *>(d4 + i), s4[i]);
-    for (int i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    for (int i = t; i < n4; i += nt) st4_nt(reinterpret_cast<float *>(d4 + i), s4[i]);
+    for (int i = (n4 << 2) + t; i < n; i += nt) dst[i] = src[i];
   } else {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    for (int i = t; i < n; i += nt) dst[i] = src[i];
   }
 }
-__device__ __forceinline__ void tile_store(uint16_t *dst, const float *src, int n) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) stf(dst + i, src[i]);
+__device__ __forceinline__ uint32_t bf16_bits(float v) {
+  __hip_bfloat16 h = __float2bfloat16(v);
+  return *reinterpret_cast<uint16_t *>(&h);
+}
+// f32 -> bf16 (round to nearest even, as stf), four per 8-byte store from the first 8-byte
+// boundary on (the head and tail one by one)
+__device__ __forceinline__ void tile_store(uint16_t *dst, const float *src, int n, int t0, int nt) {
+  const int t = static_cast<int>(threadIdx.x) - t0;
+  if (t < 0) return;
+  int h = static_cast<int>((8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7) >> 1;   // elements to the boundary
+  if (h > n) h = n;
+  if (t < h) stf(dst + t, src[t]);
+  const int n4 = (n - h) >> 2;
+  uint2 *d4 = reinterpret_cast<uint2 *>(dst + h);
+  for (int i = t; i < n4; i += nt) {
+    const float *q = src + h + 4 * i;
+    d4[i] = make_uint2(bf16_bits(q[0]) | (bf16_bits(q[1]) << 16), bf16_bits(q[2]) | (bf16_bits(q[3]) << 16));
+  }
+  for (int i = h + (n4 << 2) + t; i < n; i += nt) stf(dst + i, src[i]);
 }
 
 // Score tile split into issue (loads into registers) and commit (LDS stores), so a kernel can
@@ -884,15 +904,16 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   }
   __syncthreads();
   SEG_PHASE(2);
-  if (grad) tile_store(gsc + rbase * C, s_sc, np * C);
+  // the gradient tile: with SBOD_MB_W0_NOSTORE wave 0 (which runs the finish and its drain) stores
+  // none of it, so its drain waits for its own atomics only
+#ifdef SBOD_MB_W0_NOSTORE
+  if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 64, kLTile - 64);
+#else
+  if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
+#endif
   conf_l = block_sum(conf_l, s_red);
   loc_l = block_sum(loc_l, s_red + 8);
   SEG_PHASE(3);
-#ifdef SBOD_PHASE_CLOCKS
-  if (PHASE_PRINT_SEL)
-    printf("multibox x%d b%d: load %lld compute %lld store+sum %lld total %lld\n", blockIdx.x, b,
-           ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[3] - ph[0]);
-#endif
   if (a.fin != nullptr) {
     if (tid < 64) multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, n, a.out);
   } else if (tid == 0) {
@@ -900,6 +921,12 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     a.partials[2 * blk] = conf_l;
     a.partials[2 * blk + 1] = loc_l;
   }
+#ifdef SBOD_PHASE_CLOCKS
+  if (tid == 0) ph[4] = __builtin_amdgcn_s_memrealtime();
+  if (PHASE_PRINT_SEL)
+    printf("PH multibox x%d b%d start %lld load %lld compute %lld store+sum %lld finish %lld\n", blockIdx.x, b,
+           ph[0], ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3]);
+#endif
   span_end(a.span);
   STAMP_END(4, 1);
 }

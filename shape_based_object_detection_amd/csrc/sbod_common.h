@@ -361,9 +361,10 @@ __device__ __forceinline__ void tile_load_f32(float *__restrict__ dst, const flo
 // can be read off one dispatch.  Compiles to nothing otherwise.
 // Debug aid (off by default): -DSBOD_PHASE_CLOCKS prints per-phase cycle stamps of a few blocks.
 #ifdef SBOD_PHASE_CLOCKS
-#define SEG_PHASE(i) do { __syncthreads(); if (threadIdx.x == 0) ph[i] = clock64(); } while (0)
+// (wall clock: s_memrealtime, 100 MHz; every 8th tile of every 4th image)
+#define SEG_PHASE(i) do { __syncthreads(); if (threadIdx.x == 0) ph[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define PHASE_DECL long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define PHASE_PRINT_SEL (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 20) && (blockIdx.y == 0 || blockIdx.y == 5))
+#define PHASE_PRINT_SEL (threadIdx.x == 0 && (blockIdx.x % 8) == 0 && (blockIdx.y % 4) == 0)
 #else
 #define SEG_PHASE(i) do { } while (0)
 #define PHASE_DECL do { } while (0)
