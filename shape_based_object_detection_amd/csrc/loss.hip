@@ -14,6 +14,7 @@
 // Roofline: HBM-bound; algorithmic bytes per launch = B*P*(4+C)*s read + B*P*(4+C)*s written.
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -425,7 +426,14 @@ __device__ __forceinline__ unsigned long long xchg0(unsigned long long *w) {
 }
 // Called by wave 0 of every workgroup (all 64 lanes; conf_l / loc_l uniform).  The partials
 // array holds each workgroup's fp32 {conf, loc} for the double fallback.
-__device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, unsigned nblk, float n, float *out) {
+// fxc / fxl (k_multibox_tiles): the exact sums of the workgroup's per-tile partials, already in
+// fixed point (fx_ok: every partial foldable); conf_l / loc_l are then only the fallback's values.
+__device__ __forceinline__ Fx128 fx128_add(Fx128 x, Fx128 y) {
+  const unsigned long long lo = x.lo + y.lo;
+  return Fx128{lo, x.hi + y.hi + (lo < x.lo ? 1ull : 0ull)};
+}
+__device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, unsigned nblk, float n, float *out,
+                                const Fx128 *fxc = nullptr, const Fx128 *fxl = nullptr, bool fx_ok = true) {
   // accumulators: kFinGroups group lines, then the top line.  Two levels because atomics on one
   // word serialise at the memory side (~10 ns each): ~41 arrivals per group word and 32 on the
   // top word instead of every workgroup on one word.
@@ -436,12 +444,12 @@ __device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, un
   unsigned long long *acc = a.fin + kFinStride * g, *top = a.fin + kFinStride * kFinGroups;
   int last = 0;
   if (lane == 0) {
-    const bool ok = fx_foldable(conf_l) && fx_foldable(loc_l);
+    const bool ok = fxc ? fx_ok : (fx_foldable(conf_l) && fx_foldable(loc_l));
     st_wt_u32(reinterpret_cast<int32_t *>(a.partials) + 2 * blk, __float_as_uint(conf_l));
     st_wt_u32(reinterpret_cast<int32_t *>(a.partials) + 2 * blk + 1, __float_as_uint(loc_l));
     if (ok) {
-      fx_add(acc + kFinConf, to_fx128(conf_l));
-      fx_add(acc + kFinLoc, to_fx128(loc_l));
+      fx_add(acc + kFinConf, fxc ? *fxc : to_fx128(conf_l));
+      fx_add(acc + kFinLoc, fxl ? *fxl : to_fx128(loc_l));
     } else {
       __hip_atomic_fetch_or(acc + kFinFlag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -526,125 +534,17 @@ __device__ __forceinline__ unsigned wait_all_images(unsigned long long *done, in
   }
 }
 
-// CM > 0: class rows of C <= CM in registers (padding slots -inf: no per-slot guards in the
-// max / exp / sum); CM == 0: any C, rows in LDS.
-// kFused (focal criteria, shared priors, one rank): the matcher runs in the same launch — the
-// workgroup first matches its own 256 priors (match_wave, keys into the shards, phase-1 (obj, ovl)
-// written through), counts itself in at its image, and the image's last tile runs the image's
-// forced match (match_final_image) and counts the image in; every workgroup then loads its score
-// tile, waits for all images (the normaliser), applies the forced rewrites of its own priors from
-// the image's list, and goes on with the loss pass on registers it already holds.
-template <typename T, int CM, int CLS, bool kFused>
-__global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs a, const T *__restrict__ locs,
-                                                     const T *__restrict__ scores,
-                                                     T *__restrict__ glocs, T *__restrict__ gsc) {
-  extern __shared__ __attribute__((aligned(16))) float s_sc[];
-  __shared__ float s_red[16];
-  __shared__ int2 s_plist[kLTile];        // positive rows: wave w's at [64 w, 64 w + count)
-  __shared__ int s_wcnt[kLTile / 64];
-  __shared__ int s_misc[16];
-  STAMP_BEGIN();
-  span_begin(a.span);
-  PHASE_DECL;
-  SEG_PHASE(0);
-  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int P = a.P, C = a.C;
-  const int np = min(kLTile, P - p0);
-  const int64_t rbase = static_cast<int64_t>(b) * P + p0;
-  // memory schedule: the row's matcher outputs first, then the score tile, then the loads
-  // that depend on the matcher outputs (label, GT box, and the loc / prior of rows that can
-  // be positive) — all in flight together; the tile is committed to LDS last
-  // (a tile that does not qualify for the register path is staged first, with nothing live)
-  const bool valid = tid < np;
-  const int64_t ic = rbase + (valid ? tid : 0);
-  constexpr int NB = CM / 4;
-  const T *tsrc = scores + rbase * C;
-  const bool fast = fast_tile<T, NB>(tsrc, np * C);
-  int objv, offb;
-  float v, n;
-  int64_t labg;
-  typename TileVec<T>::V tr[NB > 0 ? NB : 1];
-  if constexpr (kFused) {
-    offb = a.off[b];
-    // ---- phase 1: this tile's match (the dynamic LDS holds the waves' key rows until the
-    // score tile is loaded)
-    uint32_t(*s_od)[kSlots][64] = reinterpret_cast<uint32_t(*)[kSlots][64]>(s_sc);
-    int *s_slot = reinterpret_cast<int *>(s_sc) + (kLTile / 64) * kSlots * 64;
-    unsigned long long *brow =
-        a.keys + (static_cast<int64_t>(b) * kKeyShards + (blockIdx.x & (kKeyShards - 1))) * a.Gmax;
-    const MatchLane m = match_wave<false, 0>(a.gt, a.labels, a.off, a.anchors, nullptr, nullptr, P, b,
-                                             p0 + (tid & ~63), brow, s_od[wv], s_slot + wv * kSlots);
-    if (m.valid) {   // phase-1 (obj, ovl), written through: the image's forced match reads them
-      st_wt_u32(a.obj_out + ic, static_cast<uint32_t>(m.bi));
-      st_wt_u32(reinterpret_cast<int32_t *>(a.ovl_out) + ic, __float_as_uint(m.best));
-    }
-    const int n1 = __popcll(__ballot(phase1_positive<false>(m, a.thr, 0.f)));
-    drain_vm();   // this wave's key atomics performed and its (obj, ovl) stores written through
-    if (lane == 0) s_wcnt[wv] = n1;
-    __syncthreads();
-    // ---- the tile counts itself in at its image: (1 << 32) | its phase-1 positives; the image's
-    // last tile gets the count of all of them and runs the image's forced match
-    if (tid == 0) {
-      const unsigned nt = static_cast<unsigned>(s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3]);
-      const unsigned long long old =
-          __hip_atomic_fetch_add(a.arrive + b, (1ull << 32) | nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int last = -1;
-      if ((old >> 32) == static_cast<unsigned long long>(gridDim.x - 1)) {
-        last = static_cast<int>(static_cast<unsigned>(old) + nt);
-        __hip_atomic_store(a.arrive + b, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next call
-      }
-      s_misc[15] = last;
-    }
-    __syncthreads();
-    const int cnt1 = s_misc[15];
-    if (cnt1 >= 0) {
-      match_final_image<0, true>(b, a.labels, a.off, a.keys, nullptr, 0, a.Gmax, P, a.thr, nullptr, 0.f, a.obj_out,
-                                 a.ovl_out, a.npos_out, a.B, cnt1, ForcedOut{a.forced, a.nforced, a.done},
-                                 reinterpret_cast<unsigned char *>(s_sc), s_misc);
-      __syncthreads();
-    }
-    // ---- the score tile -> LDS, in flight while the other images finish
-    if (!fast) tile_load(s_sc, tsrc, np * C);
-    if constexpr (NB > 0)
-      tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (NB > 0)
-      if (fast) tile_commit(s_sc, tr, np * C);
-    // ---- every image counted in: the batch's positives, then this tile's forced rewrites
-    if (tid == 0) s_misc[14] = static_cast<int>(wait_all_images(a.done, a.B, a.status));
-    __syncthreads();
-    n = static_cast<float>(s_misc[14]);
-    objv = m.bi;
-    v = m.best;
-    const int nf = static_cast<int>(ld_wt_u32(a.nforced + b));
-    for (int k = 0; k < nf; ++k) {
-      const unsigned long long e = ld_wt_u64(a.forced + static_cast<int64_t>(b) * a.Gmax + k);
-      if (static_cast<int>(e >> 32) == m.p) {
-        objv = static_cast<int>(static_cast<uint32_t>(e));
-        v = 1.0f;
-      }
-    }
-    labg = a.labels[offb + objv];
-  } else {
-    // memory schedule: the row's matcher outputs first, then the score tile, then the label
-    // that depends on the matcher outputs — all in flight together;
-    // the tile is committed to LDS last (a tile that does not qualify for the register path is
-    // staged first, with nothing live)
-    if (!fast) tile_load(s_sc, tsrc, np * C);
-    objv = a.obj[ic];
-    v = a.ovl[ic];
-    offb = a.off[b];
-    // every load below is unconditional (a tile that is not staged through registers loads an
-    // aligned dummy vector instead): a conditional load makes the wait-count insertion at
-    // the join assume the short path and wait for the whole batch
-    if constexpr (NB > 0)   // (the workspace's partials: 256-byte aligned, whatever `scores` is)
-      tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
-    __builtin_amdgcn_sched_barrier(0);   // keep the tile's loads ahead of the dependent chain
-    labg = a.labels[offb + objv];
-    if constexpr (NB > 0)
-      if (fast) tile_commit(s_sc, tr, np * C);
-    n = static_cast<float>(*a.npos_total);
-  }
+// The tile's rows after their matcher outputs are known: the class decision, the positive
+// list, the box regression of the positives and the classification (loss + gradient row into the
+// LDS tile).  Shared by k_multibox (one tile per workgroup) and k_multibox_tiles (several).
+// Every thread of the workgroup calls it (one barrier inside); conf_l / loc_l accumulate.
+template <typename T, int CM, int CLS>
+__device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__restrict__ locs, T *__restrict__ glocs,
+                                              T *__restrict__ gsc, int p0, int64_t rbase, bool valid, int64_t ic,
+                                              int objv, float v, int64_t labg, int offb, float n, float *s_sc,
+                                              int2 *s_plist, int *s_wcnt, float &conf_l, float &loc_l) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int C = a.C;
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
   const bool grad = gsc != nullptr;
   // The row's class decision before the barrier, so the tile's positive rows can be listed.
@@ -668,8 +568,6 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     if (lane == 0) s_wcnt[wv] = __popcll(bal);
   }
   __syncthreads();
-  SEG_PHASE(1);
-  float conf_l = 0.f, loc_l = 0.f;
   // ---------------- box regression, compacted: positives are ~1-3 % of the rows, yet with one
   // per wave the whole wave would run the DIoU / encode path (a dozen IEEE divisions, exps).
   // The tile's positives are packed 64 per chunk and chunk k runs on wave k % 4 (usually one
@@ -902,6 +800,132 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
       }
     }
   }
+}
+
+// CM > 0: class rows of C <= CM in registers (padding slots -inf: no per-slot guards in the
+// max / exp / sum); CM == 0: any C, rows in LDS.
+// kFused (focal criteria, shared priors, one rank): the matcher runs in the same launch — the
+// workgroup first matches its own 256 priors (match_wave, keys into the shards, phase-1 (obj, ovl)
+// written through), counts itself in at its image, and the image's last tile runs the image's
+// forced match (match_final_image) and counts the image in; every workgroup then loads its score
+// tile, waits for all images (the normaliser), applies the forced rewrites of its own priors from
+// the image's list, and goes on with the loss pass on registers it already holds.
+template <typename T, int CM, int CLS, bool kFused>
+__global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs a, const T *__restrict__ locs,
+                                                     const T *__restrict__ scores,
+                                                     T *__restrict__ glocs, T *__restrict__ gsc) {
+  extern __shared__ __attribute__((aligned(16))) float s_sc[];
+  __shared__ float s_red[16];
+  __shared__ int2 s_plist[kLTile];        // positive rows: wave w's at [64 w, 64 w + count)
+  __shared__ int s_wcnt[kLTile / 64];
+  __shared__ int s_misc[16];
+  STAMP_BEGIN();
+  span_begin(a.span);
+  PHASE_DECL;
+  SEG_PHASE(0);
+  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int P = a.P, C = a.C;
+  const int np = min(kLTile, P - p0);
+  const int64_t rbase = static_cast<int64_t>(b) * P + p0;
+  // memory schedule: the row's matcher outputs first, then the score tile, then the loads
+  // that depend on the matcher outputs (label, GT box, and the loc / prior of rows that can
+  // be positive) — all in flight together; the tile is committed to LDS last
+  // (a tile that does not qualify for the register path is staged first, with nothing live)
+  const bool valid = tid < np;
+  const int64_t ic = rbase + (valid ? tid : 0);
+  constexpr int NB = CM / 4;
+  const T *tsrc = scores + rbase * C;
+  const bool fast = fast_tile<T, NB>(tsrc, np * C);
+  int objv, offb;
+  float v, n;
+  int64_t labg;
+  typename TileVec<T>::V tr[NB > 0 ? NB : 1];
+  if constexpr (kFused) {
+    offb = a.off[b];
+    // ---- phase 1: this tile's match (the dynamic LDS holds the waves' key rows until the
+    // score tile is loaded)
+    uint32_t(*s_od)[kSlots][64] = reinterpret_cast<uint32_t(*)[kSlots][64]>(s_sc);
+    int *s_slot = reinterpret_cast<int *>(s_sc) + (kLTile / 64) * kSlots * 64;
+    unsigned long long *brow =
+        a.keys + (static_cast<int64_t>(b) * kKeyShards + (blockIdx.x & (kKeyShards - 1))) * a.Gmax;
+    const MatchLane m = match_wave<false, 0>(a.gt, a.labels, a.off, a.anchors, nullptr, nullptr, P, b,
+                                             p0 + (tid & ~63), brow, s_od[wv], s_slot + wv * kSlots);
+    if (m.valid) {   // phase-1 (obj, ovl), written through: the image's forced match reads them
+      st_wt_u32(a.obj_out + ic, static_cast<uint32_t>(m.bi));
+      st_wt_u32(reinterpret_cast<int32_t *>(a.ovl_out) + ic, __float_as_uint(m.best));
+    }
+    const int n1 = __popcll(__ballot(phase1_positive<false>(m, a.thr, 0.f)));
+    drain_vm();   // this wave's key atomics performed and its (obj, ovl) stores written through
+    if (lane == 0) s_wcnt[wv] = n1;
+    __syncthreads();
+    // ---- the tile counts itself in at its image: (1 << 32) | its phase-1 positives; the image's
+    // last tile gets the count of all of them and runs the image's forced match
+    if (tid == 0) {
+      const unsigned nt = static_cast<unsigned>(s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3]);
+      const unsigned long long old =
+          __hip_atomic_fetch_add(a.arrive + b, (1ull << 32) | nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int last = -1;
+      if ((old >> 32) == static_cast<unsigned long long>(gridDim.x - 1)) {
+        last = static_cast<int>(static_cast<unsigned>(old) + nt);
+        __hip_atomic_store(a.arrive + b, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next call
+      }
+      s_misc[15] = last;
+    }
+    __syncthreads();
+    const int cnt1 = s_misc[15];
+    if (cnt1 >= 0) {
+      match_final_image<0, true>(b, a.labels, a.off, a.keys, nullptr, 0, a.Gmax, P, a.thr, nullptr, 0.f, a.obj_out,
+                                 a.ovl_out, a.npos_out, a.B, cnt1, ForcedOut{a.forced, a.nforced, a.done},
+                                 reinterpret_cast<unsigned char *>(s_sc), s_misc);
+      __syncthreads();
+    }
+    // ---- the score tile -> LDS, in flight while the other images finish
+    if (!fast) tile_load(s_sc, tsrc, np * C);
+    if constexpr (NB > 0)
+      tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NB > 0)
+      if (fast) tile_commit(s_sc, tr, np * C);
+    // ---- every image counted in: the batch's positives, then this tile's forced rewrites
+    if (tid == 0) s_misc[14] = static_cast<int>(wait_all_images(a.done, a.B, a.status));
+    __syncthreads();
+    n = static_cast<float>(s_misc[14]);
+    objv = m.bi;
+    v = m.best;
+    const int nf = static_cast<int>(ld_wt_u32(a.nforced + b));
+    for (int k = 0; k < nf; ++k) {
+      const unsigned long long e = ld_wt_u64(a.forced + static_cast<int64_t>(b) * a.Gmax + k);
+      if (static_cast<int>(e >> 32) == m.p) {
+        objv = static_cast<int>(static_cast<uint32_t>(e));
+        v = 1.0f;
+      }
+    }
+    labg = a.labels[offb + objv];
+  } else {
+    // memory schedule: the row's matcher outputs first, then the score tile, then the label
+    // that depends on the matcher outputs — all in flight together;
+    // the tile is committed to LDS last (a tile that does not qualify for the register path is
+    // staged first, with nothing live)
+    if (!fast) tile_load(s_sc, tsrc, np * C);
+    objv = a.obj[ic];
+    v = a.ovl[ic];
+    offb = a.off[b];
+    // every load below is unconditional (a tile that is not staged through registers loads an
+    // aligned dummy vector instead): a conditional load makes the wait-count insertion at
+    // the join assume the short path and wait for the whole batch
+    if constexpr (NB > 0)   // (the workspace's partials: 256-byte aligned, whatever `scores` is)
+      tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
+    __builtin_amdgcn_sched_barrier(0);   // keep the tile's loads ahead of the dependent chain
+    labg = a.labels[offb + objv];
+    if constexpr (NB > 0)
+      if (fast) tile_commit(s_sc, tr, np * C);
+    n = static_cast<float>(*a.npos_total);
+  }
+  SEG_PHASE(1);
+  const bool grad = gsc != nullptr;
+  float conf_l = 0.f, loc_l = 0.f;
+  multibox_rows<T, CM, CLS>(a, locs, glocs, gsc, p0, rbase, valid, ic, objv, v, labg, offb, n, s_sc, s_plist, s_wcnt,
+                            conf_l, loc_l);
   __syncthreads();
   SEG_PHASE(2);
   // the gradient tile: with SBOD_MB_W0_NOSTORE wave 0 (which runs the finish and its drain) stores
@@ -927,6 +951,94 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     printf("PH multibox x%d b%d start %lld load %lld compute %lld store+sum %lld finish %lld\n", blockIdx.x, b,
            ph[0], ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3]);
 #endif
+  span_end(a.span);
+  STAMP_END(4, 1);
+}
+
+// The focal loss pass with several tiles per workgroup (tiles blockIdx.x * tpw .. + tpw of image
+// blockIdx.y), software-pipelined: as soon as tile t is committed to LDS, the registers that
+// carried it take tile t+1's scores (and its rows' matcher outputs), so t+1's loads are in flight
+// while t is computed and stored.  One tile per workgroup (k_multibox) puts every workgroup of
+// the launch in the same phase at once — all loading (HBM busy, ALUs idle), then all computing
+// (the reverse) — which is what bounds it at a large batch.  Register-path rows (CM > 0) and the
+// in-kernel finish only (focal, C <= 24: wider rows would spill); results are identical to k_multibox's (same per-row code, and
+// the finish's exact fixed-point sums do not depend on how rows are grouped into workgroups).
+template <typename T, int CM>
+__global__ __launch_bounds__(kLTile, 3) void k_multibox_tiles(LossArgs a, const T *__restrict__ locs,
+                                                              const T *__restrict__ scores, T *__restrict__ glocs,
+                                                              T *__restrict__ gsc, int tpw) {
+  static_assert(CM > 0, "k_multibox_tiles: register-path rows only");
+  extern __shared__ __attribute__((aligned(16))) float s_sc[];
+  __shared__ float s_red[16];
+  __shared__ int2 s_plist[kLTile];
+  __shared__ int s_wcnt[kLTile / 64];
+  STAMP_BEGIN();
+  span_begin(a.span);
+  constexpr int NB = CM / 4;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int P = a.P, C = a.C;
+  const int ntx = (P + kLTile - 1) / kLTile;
+  const int x0 = blockIdx.x * tpw, x1 = min(x0 + tpw, ntx);
+  const int offb = a.off[b];
+  const float n = static_cast<float>(*a.npos_total);
+  const bool grad = gsc != nullptr;
+  const T *dummy = reinterpret_cast<const T *>(a.partials);   // 256-byte aligned workspace
+  float conf_l = 0.f, loc_l = 0.f;   // the workgroup's fp32 sums (the finish's fallback only)
+  Fx128 fxc{0ull, 0ull}, fxl{0ull, 0ull};   // exact sums of the per-tile partials
+  bool fx_ok = true;
+  typename TileVec<T>::V tr[NB];
+  // tile x0's loads (every load unconditional: a tile that does not qualify for the register path
+  // loads the aligned dummy, and is staged through LDS when its turn comes)
+  int p0 = x0 * kLTile;
+  int np = min(kLTile, P - p0);
+  int64_t rbase = static_cast<int64_t>(b) * P + p0;
+  bool fast = fast_tile<T, NB>(scores + rbase * C, np * C);
+  int64_t ic = rbase + (tid < np ? tid : 0);
+  int objv = a.obj[ic];
+  float v = a.ovl[ic];
+  tile_issue<T, NB>(tr, fast ? scores + rbase * C : dummy, fast ? np * C : 4);
+  for (int x = x0; x < x1; ++x) {
+    const bool valid = tid < np;
+    if (!fast) tile_load(s_sc, scores + rbase * C, np * C);
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t labg = a.labels[offb + objv];
+    if (fast) tile_commit(s_sc, tr, np * C);
+    // the next tile's loads into the registers just freed (the last tile loads the dummy)
+    const bool more = x + 1 < x1;
+    const int p0n = more ? p0 + kLTile : p0;
+    const int npn = min(kLTile, P - p0n);
+    const int64_t rbn = static_cast<int64_t>(b) * P + p0n;
+    const bool fastn = more && fast_tile<T, NB>(scores + rbn * C, npn * C);
+    const int64_t icn = rbn + (tid < npn ? tid : 0);
+    const int objn = a.obj[icn];
+    const float vn = a.ovl[icn];
+    tile_issue<T, NB>(tr, fastn ? scores + rbn * C : dummy, fastn ? npn * C : 4);
+    float ct = 0.f, lt = 0.f;
+    multibox_rows<T, CM, SBOD_CLS_FOCAL>(a, locs, glocs, gsc, p0, rbase, valid, ic, objv, v, labg, offb, n, s_sc,
+                                         s_plist, s_wcnt, ct, lt);
+    __syncthreads();
+    if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
+    // the tile's partials exactly as k_multibox's workgroup would report them, summed in fixed
+    // point (exact: the loss equals the one-tile kernel's bit for bit)
+    ct = block_sum(ct, s_red);
+    lt = block_sum(lt, s_red + 8);
+    fx_ok = fx_ok && fx_foldable(ct) && fx_foldable(lt);
+    if (fx_ok) {
+      fxc = fx128_add(fxc, to_fx128(ct));
+      fxl = fx128_add(fxl, to_fx128(lt));
+    }
+    conf_l += ct;
+    loc_l += lt;
+    __syncthreads();   // the tile's LDS rows are read out before the next tile is committed
+    p0 = p0n;
+    np = npn;
+    rbase = rbn;
+    fast = fastn;
+    ic = icn;
+    objv = objn;
+    v = vn;
+  }
+  if (tid < 64) multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, n, a.out, &fxc, &fxl, fx_ok);
   span_end(a.span);
   STAMP_END(4, 1);
 }
@@ -1309,6 +1421,16 @@ int resident_capacity(const void *kernel, size_t lds) {
   cache.push_back(Entry{dev, kernel, lds, per_cu * cus});
   return per_cu * cus;
 }
+// Tiles per workgroup of the focal loss pass: SBOD_MB_TILES (A/B) or, by default, 2 once the
+// launch has at least kMtMinTiles tiles (below that a single round of one-tile workgroups leaves
+// the CUs part-empty, and halving the workgroups would leave more of them empty).
+constexpr int kMtMinTiles = 1024;
+int multibox_tiles_per_wg(int tiles) {
+  const char *e = std::getenv("SBOD_MB_TILES");   // read per call (tests switch it)
+  const int env = e ? std::atoi(e) : 0;
+  if (env > 0) return env < 16 ? env : 16;
+  return tiles >= kMtMinTiles ? 2 : 1;
+}
 }  // namespace
 
 extern "C" {
@@ -1507,6 +1629,27 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   dim3 grid((P + kLTile - 1) / kLTile, B);
   // + 8 floats: the register path's constant-offset row reads may run up to 7 past the last row
   const size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
+  const int tpw = fused && C <= 24 ? multibox_tiles_per_wg(static_cast<int>(grid.x) * B) : 1;
+  if (tpw > 1) {   // several tiles per workgroup, pipelined (k_multibox_tiles)
+    const dim3 g2((grid.x + tpw - 1) / tpw, B);
+    KernelTimer kt("k_multibox", s, true);
+    a.span = kt.span();
+#define SBOD_MBT(T, CM)                                                                                      \
+  tlaunch(kt, (k_multibox_tiles<T, CM>), g2, dim3(kLTile), lds, s, a, static_cast<const T *>(locs),            \
+          static_cast<const T *>(scores), static_cast<T *>(grad_locs), static_cast<T *>(grad_scores), tpw)
+#define SBOD_MBT_C(T)                  \
+  do {                                 \
+    if (C <= 8) SBOD_MBT(T, 8);        \
+    else if (C <= 16) SBOD_MBT(T, 16); \
+    else SBOD_MBT(T, 24);              \
+  } while (0)
+    if (dtype == SBOD_DT_F32) SBOD_MBT_C(float);
+    else SBOD_MBT_C(uint16_t);
+#undef SBOD_MBT_C
+#undef SBOD_MBT
+    SBOD_LAUNCHED("k_multibox_tiles");
+    return SBOD_OK;
+  }
   {
     KernelTimer kt("k_multibox", s, true);
     a.span = kt.span();
