@@ -69,4 +69,7 @@ def test_tiles_default_matches_oracle():
     ref.backward()
     np.testing.assert_allclose(float(got['loss']), ref.item(), rtol=1e-4)
     np.testing.assert_allclose(got['gl'], lo.grad.numpy(), rtol=1e-4, atol=1e-8)
-    np.testing.assert_allclose(got['gs'], sc.grad.numpy(), rtol=1e-4, atol=1e-8)
+    # atol 1e-7 (as the golden-vector tests): the focal derivative's bracket
+    # gamma * q^(gamma-1) * (-log q) - q^(gamma-1) cancels near q = exp(-1 / gamma), where an ulp of
+    # the exp moves a ~1e-4 gradient by a few 1e-8 (seed 77 has one such element in 6.9M)
+    np.testing.assert_allclose(got['gs'], sc.grad.numpy(), rtol=1e-4, atol=1e-7)
