@@ -13,7 +13,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_multibox_tiles.py tests/tes
 out=gpurun_out/tiles_ab_$TAG.jsonl
 : > $out
 for r in 1 2; do
-  for t in 1 2 3; do
+  for t in ${TILES:-1 2 3}; do
     SBOD_MB_TILES=$t timeout -k 10 200 python -u scripts/mb_ab.py tiles$t >> $out 2>> gpurun_out/tiles_ab_$TAG.err || exit 1
     SBOD_MB_TILES=$t timeout -k 10 300 python -u bench.py --steps 400 --no-dcn --no-cpu-baseline \
         > gpurun_out/tiles_bench.tmp 2>> gpurun_out/tiles_ab_$TAG.err || exit 1

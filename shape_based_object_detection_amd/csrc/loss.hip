@@ -538,11 +538,18 @@ __device__ __forceinline__ unsigned wait_all_images(unsigned long long *done, in
 // list, the box regression of the positives and the classification (loss + gradient row into the
 // LDS tile).  Shared by k_multibox (one tile per workgroup) and k_multibox_tiles (several).
 // Every thread of the workgroup calls it (one barrier inside); conf_l / loc_l accumulate.
-template <typename T, int CM, int CLS>
+// before_cls() runs after the last global load of the rows and before the classification (LDS
+// and ALU only): k_multibox_tiles issues the next tile's loads there, so that no wait for this
+// tile's loads (the wait counter is in order) also waits for them.
+struct NoPrefetch {
+  __device__ void operator()() const {}
+};
+template <typename T, int CM, int CLS, typename Pf = NoPrefetch>
 __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__restrict__ locs, T *__restrict__ glocs,
                                               T *__restrict__ gsc, int p0, int64_t rbase, bool valid, int64_t ic,
                                               int objv, float v, int64_t labg, int offb, float n, float *s_sc,
-                                              int2 *s_plist, int *s_wcnt, float &conf_l, float &loc_l) {
+                                              int2 *s_plist, int *s_wcnt, float &conf_l, float &loc_l,
+                                              Pf before_cls = Pf()) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int C = a.C;
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
@@ -635,6 +642,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
       }
     }
   }
+  before_cls();
   if (valid) {
     const int64_t i = ic;
     if (glocs && !pos) {
@@ -1003,19 +1011,23 @@ __global__ __launch_bounds__(kLTile, 3) void k_multibox_tiles(LossArgs a, const 
     __builtin_amdgcn_sched_barrier(0);
     const int64_t labg = a.labels[offb + objv];
     if (fast) tile_commit(s_sc, tr, np * C);
-    // the next tile's loads into the registers just freed (the last tile loads the dummy)
+    // the next tile's loads into the registers just freed (the last tile loads the dummy), issued
+    // by multibox_rows after this tile's own loads
     const bool more = x + 1 < x1;
     const int p0n = more ? p0 + kLTile : p0;
     const int npn = min(kLTile, P - p0n);
     const int64_t rbn = static_cast<int64_t>(b) * P + p0n;
     const bool fastn = more && fast_tile<T, NB>(scores + rbn * C, npn * C);
     const int64_t icn = rbn + (tid < npn ? tid : 0);
-    const int objn = a.obj[icn];
-    const float vn = a.ovl[icn];
-    tile_issue<T, NB>(tr, fastn ? scores + rbn * C : dummy, fastn ? npn * C : 4);
+    int objn;
+    float vn;
     float ct = 0.f, lt = 0.f;
     multibox_rows<T, CM, SBOD_CLS_FOCAL>(a, locs, glocs, gsc, p0, rbase, valid, ic, objv, v, labg, offb, n, s_sc,
-                                         s_plist, s_wcnt, ct, lt);
+                                         s_plist, s_wcnt, ct, lt, [&]() {
+                                           objn = a.obj[icn];
+                                           vn = a.ovl[icn];
+                                           tile_issue<T, NB>(tr, fastn ? scores + rbn * C : dummy, fastn ? npn * C : 4);
+                                         });
     __syncthreads();
     if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
     // the tile's partials exactly as k_multibox's workgroup would report them, summed in fixed
