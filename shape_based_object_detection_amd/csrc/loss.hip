@@ -1433,15 +1433,17 @@ int resident_capacity(const void *kernel, size_t lds) {
   cache.push_back(Entry{dev, kernel, lds, per_cu * cus});
   return per_cu * cus;
 }
-// Tiles per workgroup of the focal loss pass: SBOD_MB_TILES (A/B) or, by default, 2 once the
-// launch has at least kMtMinTiles tiles (below that a single round of one-tile workgroups leaves
-// the CUs part-empty, and halving the workgroups would leave more of them empty).
-constexpr int kMtMinTiles = 1024;
+// Tiles per workgroup of the focal loss pass: SBOD_MB_TILES (A/B), else 1 (k_multibox).  Measured
+// (scripts/gpu_tiles_ab.sh, SSD512 B=32 f32): 2 tiles per workgroup 24.7 us vs 20.3 us, the step
+// 0.0368 vs 0.0352 ms — the pass is VALU-issue-bound in its compute phase, and the prefetch
+// registers (152 VGPRs: 3 workgroups per CU instead of 6) cost more latency hiding than the
+// overlap of one tile's loads with the previous tile's compute gains.
 int multibox_tiles_per_wg(int tiles) {
   const char *e = std::getenv("SBOD_MB_TILES");   // read per call (tests switch it)
   const int env = e ? std::atoi(e) : 0;
+  (void)tiles;
   if (env > 0) return env < 16 ? env : 16;
-  return tiles >= kMtMinTiles ? 2 : 1;
+  return 1;
 }
 }  // namespace
 

@@ -62,7 +62,7 @@ def test_tiles_per_workgroup_bit_identical(kind, arch, B, reg, dtype):
 
 
 def test_tiles_default_matches_oracle():
-    """The bench's shape (SSD512 B=32 f32, 1,312 tiles: two per workgroup by default)."""
+    """The bench's shape (SSD512 B=32 f32, 1,312 tiles) at two tiles per workgroup."""
     P, boxes, labels, locs, scores, got = _run('ssd512', 'SSD512', 32, 'diou', torch.float32, 2, seed=77)
     lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
     ref = LR.criterion('ssd512', P, lo, sc, boxes, labels, 'diou', 'focal')
