@@ -22,8 +22,13 @@ VARIANTS = [
 ]
 
 
-def run(dev, steps, depth=4, gt_fold=True, crit_streams=2, det_streams=2, dtype='bf16', B=16):
-    st = BM.Step(dev, B, 0, 1, graph=True, n_batches=12,
+def run(dev, steps, depth=4, gt_fold=True, crit_streams=2, det_streams=2, dtype='bf16', B=16, n_batches=12,
+        nogc=False):
+    import gc
+    if nogc:
+        gc.collect()
+        gc.disable()
+    st = BM.Step(dev, B, 0, 1, graph=True, n_batches=n_batches,
                  dtype=torch.bfloat16 if dtype == 'bf16' else torch.float32, priority='detect', depth=depth,
                  crit_streams=crit_streams, det_streams=det_streams, gt_fold=gt_fold)
     for _ in range(3):
@@ -50,6 +55,8 @@ def run(dev, steps, depth=4, gt_fold=True, crit_streams=2, det_streams=2, dtype=
             res.append((dt / steps * 1e3, st.host_submit / steps * 1e6, st.host_collect / steps * 1e6))
     res.sort()
     ms, sub, col = res[1]
+    if nogc:
+        gc.enable()
     del st
     torch.cuda.synchronize()
     return {'ms_per_step': round(ms, 4), 'submit_us': round(sub, 1), 'collect_us': round(col, 1),
@@ -60,12 +67,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=400)
     ap.add_argument('--out')
+    ap.add_argument('--variants', help='JSON list of variant dicts (default: the built-in list)')
+    ap.add_argument('--rounds', type=int, default=2)
     a = ap.parse_args()
+    variants = json.loads(a.variants) if a.variants else VARIANTS
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     out = open(a.out, 'w') if a.out else None
-    for rnd in range(2):
-        for v in VARIANTS:
+    for rnd in range(a.rounds):
+        for v in variants:
             r = dict(v, round=rnd, **run(dev, a.steps, **v))
             print(json.dumps(r), flush=True)
             if out:
