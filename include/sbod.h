@@ -293,6 +293,10 @@ int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *l
                                void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
                                void *stream);
 int sbod_criterion_status(const void *workspace, void *stream);
+/* A/B knob of the focal loss pass: tiles per workgroup (1 = k_multibox, the default; 2..16 =
+ * k_multibox_tiles, software-pipelined, bit-identical results).  n < 1 only queries.  Returns the
+ * previous value.  Initialised from the environment variable SBOD_MB_TILES when the library loads. */
+int sbod_set_multibox_tiles(int n);
 
 /* grad *= (*scale) in place unless *scale == 1 (decided on the device: no host sync).
  * Used by backward to apply the upstream gradient to gradients produced by the fused

@@ -14,6 +14,7 @@
 // Roofline: HBM-bound; algorithmic bytes per launch = B*P*(4+C)*s read + B*P*(4+C)*s written.
 #include <hip/hip_bf16.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -1438,12 +1439,14 @@ int resident_capacity(const void *kernel, size_t lds) {
 // 0.0368 vs 0.0352 ms — the pass is VALU-issue-bound in its compute phase, and the prefetch
 // registers (152 VGPRs: 3 workgroups per CU instead of 6) cost more latency hiding than the
 // overlap of one tile's loads with the previous tile's compute gains.
+std::atomic<int> g_mb_tiles{[] {   // SBOD_MB_TILES read once; sbod_set_multibox_tiles() after
+  const char *e = std::getenv("SBOD_MB_TILES");
+  const int v = e ? std::atoi(e) : 1;
+  return v < 1 ? 1 : (v > 16 ? 16 : v);
+}()};
 int multibox_tiles_per_wg(int tiles) {
-  const char *e = std::getenv("SBOD_MB_TILES");   // read per call (tests switch it)
-  const int env = e ? std::atoi(e) : 0;
   (void)tiles;
-  if (env > 0) return env < 16 ? env : 16;
-  return 1;
+  return g_mb_tiles.load(std::memory_order_relaxed);
 }
 }  // namespace
 
@@ -1700,6 +1703,12 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
 }
 
 size_t sbod_loss_zero_prefix_bytes(void) { return kFinBytes; }
+
+int sbod_set_multibox_tiles(int n) {
+  const int prev = g_mb_tiles.load();
+  if (n >= 1) g_mb_tiles.store(n > 16 ? 16 : n);
+  return prev;
+}
 
 size_t sbod_loss_pool_offset(int B, int P) {
   return carve(nullptr, B, P).pool_off;
