@@ -967,8 +967,8 @@ static int dcn_check(const DcnShape &s, const float *x, const float *offset, con
 // A second stream per device for the independent parts of a call (the weight layouts beside the
 // x transpose + coefficients; the dx chain — scan, entry fill, gather — beside bwd_data and
 // bwd_weight): fork on an event recorded on the caller's stream, join before returning, so the
-// call is ordered on the caller's stream exactly as before.  Eager calls only (see side_for);
-// created on first use; if creation fails, calls run serially.
+// call is ordered on the caller's stream exactly as before (and captures as a fork-join graph).
+// Created on first use outside a capture; until then (or if creation fails) calls run serially.
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t ev[4] = {};
@@ -980,14 +980,10 @@ SideStream *side_for(hipStream_t hs) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   SideStream &sd = g_side[dev];
+  if (sd.s) return &sd;
   if (sd.failed) return nullptr;
-  // eager calls only: a fork-join inside a hipGraph capture (event record on the capturing
-  // stream, the side stream joining through it) crashed this runtime's capture_end
-  // (tests/test_gpu_dcn.py::test_fork_join_streams_eager_and_captured), so captured calls stay on
-  // the caller's stream
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(hs, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  if (sd.s) return &sd;
   hipStream_t st = nullptr;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
     sd.failed = true;

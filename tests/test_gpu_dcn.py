@@ -243,11 +243,11 @@ def test_state_backward_stateless_backward_and_retained_graph():
 
 @pytest.mark.parametrize('H', [8, 24])
 def test_fork_join_streams_eager_and_captured(H):
-    """Eager calls run the forward's weight layouts and the backward's dx chain (scan, entry fill,
-    gather) on a second stream forked from and joined back into the caller's: the results equal
-    the oracle-checked serial form (the C-ABI's stateless backward, one stream).  Captured calls
-    stay on the capturing stream (serial): a hipGraph over forward + backward replays to the eager
-    values, also after the inputs change between replays."""
+    """The forward's weight layouts and the backward's dx chain (scan, entry fill, gather) run on a
+    second stream forked from and joined back into the caller's: the results equal the oracle-
+    checked serial form (the C-ABI's stateless backward, one stream) eagerly, and a hipGraph
+    captured over forward + backward (a fork-join graph) replays to the same values, also after the
+    inputs change between replays."""
     from shape_based_object_detection_amd import _lib as L
     g = torch.Generator(device=DEV).manual_seed(H)
     B, C, O, ks = 3, 64, 32, 3
