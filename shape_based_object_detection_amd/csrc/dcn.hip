@@ -19,8 +19,6 @@
 // flops forward, 2x backward).
 #include <hipcub/hipcub.hpp>
 
-#include <mutex>
-
 #include "sbod_common.h"
 
 namespace sbod {
@@ -964,46 +962,6 @@ static int dcn_check(const DcnShape &s, const float *x, const float *offset, con
   return SBOD_OK;
 }
 
-// A second stream per device for the independent parts of a call (the weight layouts beside the
-// x transpose + coefficients; the dx chain — scan, entry fill, gather — beside bwd_data and
-// bwd_weight): fork on an event recorded on the caller's stream, join before returning, so the
-// call is ordered on the caller's stream exactly as before (and captures as a fork-join graph).
-// Created on first use outside a capture; until then (or if creation fails) calls run serially.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t ev[4] = {};
-  bool failed = false;
-};
-std::mutex g_side_mu;   // held while a call enqueues (the events are reused call after call)
-SideStream g_side[64];
-SideStream *side_for(hipStream_t hs) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream &sd = g_side[dev];
-  if (sd.s) return &sd;
-  if (sd.failed) return nullptr;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(hs, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-    sd.failed = true;
-    return nullptr;
-  }
-  for (auto &e : sd.ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      sd.failed = true;
-      return nullptr;
-    }
-  sd.s = st;
-  return &sd;
-}
-// `to` waits for everything enqueued on `from` so far (event `e`)
-int stream_after(hipStream_t to, hipStream_t from, hipEvent_t e) {
-  if (hipEventRecord(e, from) != hipSuccess || hipStreamWaitEvent(to, e, 0) != hipSuccess)
-    return launch_status("dcn fork/join");
-  return SBOD_OK;
-}
-
 // Derives the state from the inputs: x -> channels-last xt (training: the sample counters zeroed
 // on the side), the coefficients (training: the counts; split-K: the output zeroed on the side),
 // the weight layouts.  Three launches.
@@ -1012,15 +970,6 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
                       hipStream_t hs) {
   const int64_t npix = static_cast<int64_t>(s.B) * s.H * s.W;
   const int HW = s.H * s.W;
-  // the weight layouts (independent of x / offset / mask) on the side stream, joined at the end
-  std::unique_lock<std::mutex> lk(g_side_mu);
-  SideStream *sd = side_for(hs);
-  if (!sd) lk.unlock();
-  const hipStream_t hw = sd ? sd->s : hs;
-  if (sd && stream_after(hw, hs, sd->ev[0]) != SBOD_OK) return SBOD_E_HIP;
-  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hw, weight, s.O, s.C, s.N, st.wf,
-                     train ? st.wb : nullptr);
-  SBOD_LAUNCHED("k_weight_layouts");
   hipLaunchKernelGGL(k_transpose, dim3((HW + 63) / 64, (s.C + 63) / 64, s.B), dim3(256), 0, hs, x, st.xt, s.C, HW,
                      train ? reinterpret_cast<float *>(st.tcount) : nullptr, train ? npix + 1 : 0);
   SBOD_LAUNCHED("k_transpose(x)");   // x [B][C][HW] -> xt [B][HW][C]
@@ -1028,7 +977,9 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
   hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, st.coef,
                      train ? st.tcount : nullptr, zero_out, n_zero_out);
   SBOD_LAUNCHED("k_dcn_coef");
-  if (sd && stream_after(hs, hw, sd->ev[1]) != SBOD_OK) return SBOD_E_HIP;   // join
+  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
+                     train ? st.wb : nullptr);
+  SBOD_LAUNCHED("k_weight_layouts");
   return SBOD_OK;
 }
 
@@ -1063,23 +1014,16 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
                "sbod_dcn_bwd: grad_out / weight exceed the 2 GiB buffer-descriptor range");
   const int64_t ob = static_cast<int64_t>(s.M) * s.N;
   const int64_t wn = static_cast<int64_t>(s.O) * s.K;
-  // with dx and the weight / offset / mask gradients both wanted, the dx chain (scan, entry fill,
-  // gather) runs on the side stream: the fill beside bwd_data, the gather beside bwd_weight
-  std::unique_lock<std::mutex> lk(g_side_mu);
-  SideStream *sd = grad_x && (grad_weight || need_om) ? side_for(hs) : nullptr;
-  if (!sd) lk.unlock();
-  const hipStream_t hx = sd ? sd->s : hs;
-  if (sd && stream_after(hx, hs, sd->ev[0]) != SBOD_OK) return SBOD_E_HIP;
   if (grad_x) {   // the input pixels' entry ranges (scan of the counts the forward made)
     if (npix + 1 <= kScanOneBlock) {
-      hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, hx, st.tcount, sc.cur, npix + 1);
+      hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, hs, st.tcount, sc.cur, npix + 1);
       SBOD_LAUNCHED("k_dcn_scan");
     } else {
       size_t tb = sc.scan_bytes;
-      if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, tb, st.tcount, sc.cur, npix + 1, hx) != hipSuccess)
+      if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, tb, st.tcount, sc.cur, npix + 1, hs) != hipSuccess)
         return launch_status("DeviceScan(dcn dx offsets)");
     }
-    hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hx, s, st.coef, sc.cur, sc.ent,
+    hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hs, s, st.coef, sc.cur, sc.ent,
                        grad_offset, grad_offset ? 2 * ob : 0, grad_mask_logits, grad_mask_logits ? ob : 0,
                        grad_weight ? sc.gwp : nullptr, grad_weight ? wn : 0);
     SBOD_LAUNCHED("k_dcn_dx_fill");
@@ -1088,29 +1032,25 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
     if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob * 4, hs) != hipSuccess) return launch_status("memset");
     if (grad_weight && hipMemsetAsync(sc.gwp, 0, wn * 4, hs) != hipSuccess) return launch_status("memset");
   }
-  // the fill zeroed the offset / mask / weight-gradient outputs bwd_weight adds into
-  if (sd && hipEventRecord(sd->ev[1], hx) != hipSuccess) return launch_status("dcn fork/join");
   if (need_cols) {
     KernelTimer kt("k_dcn_bwd_data", hs);
     hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
                        hs, s, st.wb, grad_out, sc.dcols);
   }
   if (need_cols) SBOD_LAUNCHED("k_dcn_bwd_data");
-  if (sd && stream_after(hx, hs, sd->ev[2]) != SBOD_OK) return SBOD_E_HIP;   // the gather reads dcols
   if (grad_x) {
     {
-      KernelTimer kt("k_dcn_dx_gather", hx);
+      KernelTimer kt("k_dcn_dx_gather", hs);
       const dim3 grid((npix + kGxPix - 1) / kGxPix);
       if (s.C % 4 == 0)
-        hipLaunchKernelGGL(k_dcn_dx_gather<4>, grid, dim3(64 * kGxPix), 0, hx, s.C, s.H * s.W, npix, sc.cur, sc.ent,
+        hipLaunchKernelGGL(k_dcn_dx_gather<4>, grid, dim3(64 * kGxPix), 0, hs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
                            sc.dcols, grad_x);
       else
-        hipLaunchKernelGGL(k_dcn_dx_gather<1>, grid, dim3(64 * kGxPix), 0, hx, s.C, s.H * s.W, npix, sc.cur, sc.ent,
+        hipLaunchKernelGGL(k_dcn_dx_gather<1>, grid, dim3(64 * kGxPix), 0, hs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
                            sc.dcols, grad_x);
     }
     SBOD_LAUNCHED("k_dcn_dx_gather");
   }
-  if (sd && hipStreamWaitEvent(hs, sd->ev[1], 0) != hipSuccess) return launch_status("dcn fork/join");
   if (grad_weight || need_om) {
     // weight gradient, and the offset / mask gradients from the same corner samples (C / 64
     // channel-block partials added into the zeroed outputs)
@@ -1147,7 +1087,6 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
       SBOD_LAUNCHED("k_transpose(dw)");
     }
   }
-  if (sd && stream_after(hs, hx, sd->ev[3]) != SBOD_OK) return SBOD_E_HIP;   // join the dx chain
   return SBOD_OK;
 }
 
