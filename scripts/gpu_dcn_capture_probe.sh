@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 log=gpurun_out/dcn_capture_probe_${1:-run}.log
 : > $log
-for cfg in "16 256 256 8 2 0" "3 64 32 8 2 0" "3 256 256 8 2 0" "16 64 32 8 2 0" "3 64 32 8 1 0" "3 64 32 8 1 1"; do
+for cfg in ${CFGS:-"16 256 256 8 2 0"}; do
   timeout -k 10 120 python -u scripts/dcn_capture_probe.py $cfg >> $log 2>&1 || { echo "FAIL $cfg rc $?" >> $log; exit 1; }
 done
 echo done
