@@ -239,3 +239,41 @@ def test_state_backward_stateless_backward_and_retained_graph():
     for n, a, b, c in zip(('x', 'offset', 'mask', 'weight'), first, second, stateless):
         np.testing.assert_allclose(_np(b), _np(a), rtol=1e-5, atol=1e-6 * _amax(a), err_msg='retained ' + n)
         np.testing.assert_allclose(_np(c), _np(a), rtol=1e-5, atol=1e-6 * _amax(a), err_msg='stateless ' + n)
+
+
+@pytest.mark.parametrize('H', [8, 24])
+def test_captured_fwd_bwd_equals_eager(H):
+    """A hipGraph captured over forward + autograd backward (as bench.py times DCN) replays to the
+    eager values, also after the inputs change in place between replays."""
+    g = torch.Generator(device=DEV).manual_seed(H)
+    B, C, O, ks = 3, 64, 32, 3
+    x = torch.randn(B, C, H, H, device=DEV, generator=g).requires_grad_(True)
+    off = torch.randn(B, 2 * ks * ks, H, H, device=DEV, generator=g).requires_grad_(True)
+    ml = torch.randn(B, ks * ks, H, H, device=DEV, generator=g).requires_grad_(True)
+    w = (torch.randn(O, C, ks, ks, device=DEV, generator=g) / 24).requires_grad_(True)
+    gout = torch.randn(B, O, H, H, device=DEV, generator=g)
+    ins = (x, off, ml, w)
+
+    def step():
+        out = core.deform_conv2d(x, off, ml, w, ks, 1, 1)
+        return (out,) + tuple(torch.autograd.grad(out, ins, gout))
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=side):
+        cap = step()
+    for k in range(2):
+        with torch.no_grad():   # new inputs in place: the replay must follow them
+            x.mul_(0.5 if k else 1.0)
+            off.add_(0.25 * k)
+        graph.replay()
+        torch.cuda.synchronize()
+        want = step()
+        for n, a, b in zip(('out', 'x', 'offset', 'mask', 'weight'), cap, want):
+            np.testing.assert_allclose(_np(a), _np(b), rtol=1e-5, atol=1e-6 * _amax(b), err_msg='replay %d %s' % (k, n))
