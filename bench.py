@@ -88,8 +88,10 @@ def parse(argv=None):
     ap.add_argument('--hw-queues', type=int, default=None,
                     help='HIP hardware queues per process (GPU_MAX_HW_QUEUES, <= 32; the runtime default is 4): '
                          'more streams than queues share a queue and serialise')
-    ap.add_argument('--submit', choices=('graph', 'direct'), default='direct',
-                    help='graph: replay captured hipGraphs; direct: issue the recorded entry-point calls')
+    ap.add_argument('--submit', choices=('graph', 'direct', 'fork'), default='direct',
+                    help='graph: replay captured hipGraphs (criterion and detect, two launches); fork: one '
+                         'graph per step with detect forked onto its stream inside it; direct: issue the '
+                         'recorded entry-point calls')
     ap.add_argument('--gt-fold', type=int, choices=(0, 1), default=0,
                     help='direct submit: 1 = the GT packing folded into the matcher\'s first launch '
                          '(sbod_criterion_focal_lists), 0 = a separate sbod_gt_pack launch (the headline default: '
@@ -356,7 +358,7 @@ class Step:
         self.depth = max(2, int(depth))
         # the recorder sees sbod entry points only: with ranks, the normaliser's RCCL all-reduce
         # (torch.distributed) must be in the replayed work, so data-parallel steps replay graphs
-        self.submit = submit if world == 1 else 'graph'
+        self.submit = submit if world == 1 or submit == 'fork' else 'graph'
         self.host_submit = self.host_collect = 0.0
         # the read-only unit upstream gradient: no ones-fill and no scale launch in the step
         self.one = core.unit_grad(dev)
@@ -489,6 +491,22 @@ class Step:
                     raise RuntimeError('direct submit: unexpected recorded calls %s'
                                        % [n for n, _ in crit_calls + det_calls])
                 self.slots.append((crit_calls, det_calls, loss, h))
+                continue
+            if self.submit == 'fork':
+                # ONE graph per step: detect forked onto the detect stream inside the capture and
+                # joined back, so one hipGraphLaunch submits both chains (which stay concurrent)
+                g = torch.cuda.CUDAGraph()
+                cs, ds = self.cs_of(bi), self.ds_of(bi)
+                with torch.cuda.graph(g, stream=cs):
+                    ds.wait_stream(cs)
+                    with torch.cuda.stream(ds):
+                        h = self.detect(bt, True)
+                    loss = self.crit(bt.locs, bt.scores, gt, None)
+                    loss.backward(self.one)
+                    cs.wait_stream(ds)
+                self.slots.append((g, None, loss, h))
+                if after_first is not None and len(self.slots) == 1:
+                    after_first()
                 continue
             if self.two:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -877,6 +895,8 @@ def main():
                                % (B, ((', the recorded criterion and detect entry-point calls issued natively '
                                        'per step (criterion and detect streams, %d steps in flight)' % st.depth)
                                       if st.submit == 'direct' else
+                                      (', one hipGraph per step (detect forked onto its own stream inside it)'
+                                       if st.submit == 'fork' else None) or
                                       (', criterion and detect hipGraphs replayed on two streams per step'
                                        if st.two else ', one hipGraph replay per step'))
                                   if st.use_graph else ', eager launches'),

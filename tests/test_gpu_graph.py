@@ -249,11 +249,12 @@ def test_graph_span_timing():
 
 @pytest.mark.parametrize('depth,two,submit,fold', [(2, True, 'graph', False), (3, True, 'graph', False),
                                                     (3, False, 'graph', False), (4, True, 'direct', True),
-                                                    (4, True, 'direct', False)])
+                                                    (4, True, 'direct', False), (4, True, 'fork', False)])
 def test_bench_pipelined_step_equals_eager(depth, two, submit, fold):
     """bench.Step as the bench runs it: per-batch criterion and detect graphs, each alternating over
     two streams (or, ``two`` False, one graph per step holding both), submitted by the one-call C++
     path — or, ``submit='direct'``, the recorded entry-point calls issued again without graphs —
+    — or, ``submit='fork'``, one graph per step with detect forked onto its stream inside it —
     with ``depth`` steps in flight and a criterion stream current.  Every step's loss, gradients and
     per-image detections equal the eager two-stream step on the same batch, across two rotations
     of the resident batches.  ``fold``: the direct submit's GT packing folded into the matcher's
