@@ -335,6 +335,13 @@ class Step:
         # (scripts/probe_graph_launch.py), two graphs on two streams need no edge at all.
         # criterion graphs alternate over `crit_streams` streams the same way (each stream has its
         # own cached workspaces): step k's matcher need not wait for step k-1's loss pass
+        # with ranks every criterion graph holds the normaliser's RCCL all-reduce: collectives on
+        # one communicator must run in the order they were issued on every rank, which two
+        # criterion streams replaying concurrently would not guarantee (step k+1's all-reduce
+        # could start before step k's on one rank and after it on another: a cross-rank deadlock).
+        # Data-parallel steps therefore keep ONE criterion stream; detect has no collective.
+        if world > 1:
+            crit_streams = 1
         self.cap_streams = [torch.cuda.Stream(dev, priority=-1 if priority == 'criterion' else 0)
                             for _ in range(max(1, crit_streams))]
         self.cap_stream = self.cap_streams[0]
