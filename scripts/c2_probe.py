@@ -23,14 +23,14 @@ VARIANTS = [
 
 
 def run(dev, steps, depth=4, gt_fold=True, crit_streams=2, det_streams=2, dtype='bf16', B=16, n_batches=12,
-        nogc=False):
+        nogc=False, det_form='two'):
     import gc
     if nogc:
         gc.collect()
         gc.disable()
     st = BM.Step(dev, B, 0, 1, graph=True, n_batches=n_batches,
                  dtype=torch.bfloat16 if dtype == 'bf16' else torch.float32, priority='detect', depth=depth,
-                 crit_streams=crit_streams, det_streams=det_streams, gt_fold=gt_fold)
+                 crit_streams=crit_streams, det_streams=det_streams, gt_fold=gt_fold, det_form=det_form)
     for _ in range(3):
         st.eager_split()
     torch.cuda.synchronize()
