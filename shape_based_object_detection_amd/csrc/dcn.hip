@@ -541,7 +541,14 @@ __global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__r
 // consecutive pixels per channel): the channels-last result is never written to HBM and
 // transposed back.  After k_dcn_dx_fill, cur[tp] is the end of pixel tp's entries and cur[tp - 1]
 // its start.
-constexpr int kGxPix = 16;
+#ifndef SBOD_GX_PIX   // A/B knobs: pixels (waves) per block, dcols rows in flight per wave
+#define SBOD_GX_PIX 16
+#endif
+#ifndef SBOD_GX_ROWS
+#define SBOD_GX_ROWS 8
+#endif
+constexpr int kGxPix = SBOD_GX_PIX;
+constexpr int kGxRows = SBOD_GX_ROWS;
 
 template <int VEC>
 __global__ __launch_bounds__(64 * kGxPix) void k_dcn_dx_gather(int C, int HW, int ntarget,
@@ -571,16 +578,16 @@ __global__ __launch_bounds__(64 * kGxPix) void k_dcn_dx_gather(int C, int HW, in
       const int ne = static_cast<int>(min(e1 - eb, 64u));
       const DxEnt mine = lane < ne ? ent[eb + lane] : DxEnt{0u, 0.f};
       int k = 0;
-      for (; k + 8 <= ne; k += 8) {
-        float x[8][VEC], w[8];
+      for (; k + kGxRows <= ne; k += kGxRows) {
+        float x[kGxRows][VEC], w[kGxRows];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < kGxRows; ++u) {
           const uint32_t row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mine.row), k + u));
           w[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mine.w), k + u));
           load_vec<VEC>(dcols + static_cast<int64_t>(row) * C + c0, true, x[u]);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < kGxRows; ++u)
 #pragma unroll
           for (int v = 0; v < VEC; ++v) acc[v] += w[u] * x[u][v];
       }
