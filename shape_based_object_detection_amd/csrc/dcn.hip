@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__r
 // transposed back.  After k_dcn_dx_fill, cur[tp] is the end of pixel tp's entries and cur[tp - 1]
 // its start.
 #ifndef SBOD_GX_PIX   // A/B knobs: pixels (waves) per block, dcols rows in flight per wave
-#define SBOD_GX_PIX 16
+#define SBOD_GX_PIX 8   // 8 (512 threads): 64² 211-213 vs 218-219 us, 8² 8.8 vs 10.6 us (r4_gx_ab_c1.jsonl)
 #endif
 #ifndef SBOD_GX_ROWS
 #define SBOD_GX_ROWS 8
