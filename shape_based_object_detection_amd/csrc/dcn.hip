@@ -548,6 +548,9 @@ __global__ __launch_bounds__(256) void k_dcn_dx_fill(DcnShape s, const Coef *__r
 #define SBOD_GX_ROWS 8
 #endif
 constexpr int kGxPix = SBOD_GX_PIX;
+#ifndef SBOD_WG_TARGET   // A/B knob: k_dcn_bwd_weight's target workgroup count (pixel slices)
+#define SBOD_WG_TARGET 512
+#endif
 constexpr int kGxRows = SBOD_GX_ROWS;
 
 template <int VEC>
@@ -1063,7 +1066,7 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
     // channel-block partials added into the zeroed outputs)
     const int gx = s.N * ((s.C + kWC - 1) / kWC), gz = grad_weight ? (s.O + 255) / 256 : 1;
     // one round of resident blocks (256 CUs x 2): a partial second round would double the time
-    int slices = std::max(1, 512 / (gx * gz));
+    int slices = std::max(1, SBOD_WG_TARGET / (gx * gz));
     slices = std::max(1, std::min(slices, (s.M + kWMs - 1) / kWMs));
     int m_slice = (s.M + slices - 1) / slices;
     m_slice = (m_slice + kWMs - 1) / kWMs * kWMs;
