@@ -345,15 +345,24 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_FWD_WAVES : 2) voi
 // gather over those rows (k_dcn_dx_gather); the offset / mask gradients need the corner values,
 // which k_dcn_bwd_weight already samples, so they are reduced there.
 constexpr int kBM = 64, kBOC = 32, kBLD = kBM + 2;
+#ifndef SBOD_BWD_DATA_MIN_BLOCKS
+#define SBOD_BWD_DATA_MIN_BLOCKS 256
+#endif
+constexpr int kBwdDataMinBlocks = SBOD_BWD_DATA_MIN_BLOCKS;   // below: 32-pixel blocks
 
+// R row halves of 32 pixels per block (R = 2: 64 pixels; R = 1: 32, for maps too small to give
+// every CU a 64-pixel block)
+template <int R>
 __global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
     DcnShape s, const float *__restrict__ wb, const float *__restrict__ gout, float *__restrict__ dcols) {
+  constexpr int kRM = 32 * R;                 // pixels per block
+  constexpr int kLd = kDcnThreads / kRM;      // dout rows (o) per staging pass of the block
   __shared__ float s_dout[2][kBOC][kBLD];     // A operand [o][m]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
   // logical order kernel point fastest: the N tiles of one pixel tile (same dout rows) run
   // back to back on one XCD
   const Tile3 tl = xcd_tile(gridDim.z, gridDim.x, gridDim.y);
-  const int m0 = tl.y * kBM, cgb = tl.z * 256, n = tl.x;
+  const int m0 = tl.y * kRM, cgb = tl.z * 256, n = tl.x;
   const int HWo = s.Ho * s.Wo;
   const int OT = (s.O + kBOC - 1) / kBOC;
   // Operand loads are unconditional, through wave-uniform buffer descriptors (32-bit lane offsets,
@@ -364,32 +373,33 @@ __global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
                                                     static_cast<int>(static_cast<int64_t>(s.M) * s.O * 4), 0x00020000);
   const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(wb), static_cast<short>(0),
                                                     static_cast<int>(static_cast<int64_t>(s.N) * s.O * s.C * 4), 0x00020000);
-  int dvoff[8];   // dout element (o = oc * 32 + ol, m) at byte dvoff + oc * 32 * HWo * 4
-  bool dok[8];
+  constexpr int kSt = kBOC * kRM / kDcnThreads;   // staged dout elements per thread (8 or 4)
+  int dvoff[kSt];   // dout element (o = oc * 32 + ol, m) at byte dvoff + oc * 32 * HWo * 4
+  bool dok[kSt];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < kSt; ++i) {
     const int e = tid + kDcnThreads * i;
-    const int ol = e >> 6, mm = e & 63, m = min(m0 + mm, s.M - 1);
+    const int ol = e / kRM, mm = e % kRM, m = min(m0 + mm, s.M - 1);
     const int b = m / HWo, pix = m - b * HWo;
     dok[i] = m0 + mm < s.M;
     dvoff[i] = ((b * s.O + ol) * HWo + pix) * 4;
   }
-  float dstage[8];
+  float dstage[kSt];
   float bcur[2][16];   // one B buffer: the next chunk's weights load once the MFMAs have read these
   auto load_dout = [&](int oc) {
     const int so = oc * kBOC * HWo * 4;   // wave-uniform: rows o >= O read finite data or 0 (range check)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const bool o_ok = oc * kBOC + ((tid + kDcnThreads * i) >> 6) < s.O;
+    for (int i = 0; i < kSt; ++i) {
+      const bool o_ok = oc * kBOC + (tid + kDcnThreads * i) / kRM < s.O;
       const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, dvoff[i], so, 0));
       dstage[i] = (dok[i] && o_ok) ? v : 0.f;
     }
   };
   auto store_dout = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < kSt; ++i) {
       const int e = tid + kDcnThreads * i;
-      s_dout[buf][e >> 6][e & 63] = dstage[i];
+      s_dout[buf][e / kRM][e % kRM] = dstage[i];
     }
   };
   int bvoff[2];
@@ -427,15 +437,17 @@ __global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       a0[st] = s_dout[buf][16 * h + st][l31];
-      a1[st] = s_dout[buf][16 * h + st][32 + l31];
+      if constexpr (R == 2) a1[st] = s_dout[buf][16 * h + st][32 + l31];
     }
     __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[st], bcur[0][st], acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[st], bcur[1][st], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[st], bcur[0][st], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[st], bcur[1][st], acc[1][1], 0, 0, 0);
+      if constexpr (R == 2) {
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[st], bcur[0][st], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[st], bcur[1][st], acc[1][1], 0, 0, 0);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     load_b(ocn, bcur);   // L2-resident weights, in flight through the dout store and barrier
@@ -444,7 +456,7 @@ __global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
   }
   // epilogue: row m = 32 ri + (r&3) + 8 (r>>2) + 4 h, column c = cgb + 64 wv + 32 ci + l31
 #pragma unroll
-  for (int ri = 0; ri < 2; ++ri)
+  for (int ri = 0; ri < R; ++ri)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + 32 * ri + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -1044,8 +1056,14 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
   }
   if (need_cols) {
     KernelTimer kt("k_dcn_bwd_data", hs);
-    hipLaunchKernelGGL(k_dcn_bwd_data, dim3((s.M + kBM - 1) / kBM, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
-                       hs, s, st.wb, grad_out, sc.dcols);
+    // 64-pixel blocks, or 32 when that leaves fewer blocks than CUs (C4's 8x8 map: 144 -> 288)
+    const int64_t nb64 = static_cast<int64_t>((s.M + kBM - 1) / kBM) * ((s.C + 255) / 256) * s.N;
+    if (nb64 >= kBwdDataMinBlocks)
+      hipLaunchKernelGGL(k_dcn_bwd_data<2>, dim3((s.M + 63) / 64, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
+                         hs, s, st.wb, grad_out, sc.dcols);
+    else
+      hipLaunchKernelGGL(k_dcn_bwd_data<1>, dim3((s.M + 31) / 32, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
+                         hs, s, st.wb, grad_out, sc.dcols);
   }
   if (need_cols) SBOD_LAUNCHED("k_dcn_bwd_data");
   if (grad_x) {
