@@ -865,6 +865,13 @@ def main():
     if st.use_graph:
         for _ in range(len(st.slots) + 1):
             st.replay()
+        # the W warm-up steps of the timed kind: pipelined submits and collects, drained before the
+        # timed region (which starts from an empty pipeline, after its barrier + synchronize)
+        with torch.cuda.stream(st.cap_stream):
+            for _ in range(max(a.warmup, 1)):
+                st.pipelined()
+            st.drain()
+        torch.cuda.synchronize()
         st.host_submit = st.host_collect = 0.0
         # the training loop's current stream is the criterion's: the GT lists it hands over
         # are ordered on the stream that packs them (no cross-stream event pair per step)
