@@ -570,7 +570,10 @@ __global__ __launch_bounds__(64 * kGxPix) void k_dcn_dx_gather(int C, int HW, in
                                                               const uint32_t *__restrict__ cur,
                                                               const DxEnt *__restrict__ ent,
                                                               const float *__restrict__ dcols, float *__restrict__ gx) {
-  __shared__ float s_t[kGxPix][64 * VEC + 1];
+  // row stride 64 * VEC + 8 floats: the float4 row writes stay 16-B aligned and the column reads
+  // (8 pixels x 8 channels per wave) hit 64 distinct banks
+  constexpr int kLd = 64 * VEC + 8;
+  __shared__ __attribute__((aligned(16))) float s_t[kGxPix][kLd];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // neighbouring input pixels (overlapping dcols rows) on one XCD
@@ -615,8 +618,10 @@ __global__ __launch_bounds__(64 * kGxPix) void k_dcn_dx_gather(int C, int HW, in
         for (int v = 0; v < VEC; ++v) acc[v] += w * x[v];
       }
     }
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) s_t[wv][VEC * lane + v] = acc[v];
+    if constexpr (VEC == 4)
+      *reinterpret_cast<float4 *>(&s_t[wv][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    else
+      for (int v = 0; v < VEC; ++v) s_t[wv][VEC * lane + v] = acc[v];
     __syncthreads();
     const int nc = min(64 * VEC, C - cb);
     for (int e = threadIdx.x; e < kGxPix * 64 * VEC; e += 64 * kGxPix) {
