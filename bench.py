@@ -109,6 +109,8 @@ def parse(argv=None):
     ap.add_argument('--timing-steps', type=int, default=12,
                     help='eager steps whose every kernel dispatch carries HIP events')
     ap.add_argument('--no-c2', action='store_true', help='skip the config C2 bf16 B=16 figure')
+    ap.add_argument('--c2-det-form', choices=('two', 'one'), default='two',
+                    help='C2 figure: detect as two launches (segment, merge) or one (k_det_nms)')
     return ap.parse_args(argv)
 
 
@@ -660,13 +662,14 @@ class Step:
         return self.replay() if self.graph is not None else self.eager()
 
 
-def c2_figure(dev, steps, warmup, B=16, n_batches=12):
+def c2_figure(dev, steps, warmup, B=16, n_batches=12, det_form='two'):
     """Config C2 (SSD512 batch=16 bf16 on 1 GPU): the same captured step with bf16 locs / scores
     (and bf16 gradients) for the criterion, and the detect reading the bf16 activations directly
     (SBOD_DETECT_INPUT_BF16: widened exactly on load, no fp32 copies).  ``n_batches`` resident batches
     (~23 MB touched per step) keep the rotation above the Infinity Cache.  Algorithmic bytes of
     the criterion at 2 B/element: SURVEY §8(d) (16.56 MB at B=16)."""
-    st = Step(dev, B, 0, 1, graph=True, n_batches=n_batches, dtype=torch.bfloat16, priority='detect')
+    st = Step(dev, B, 0, 1, graph=True, n_batches=n_batches, dtype=torch.bfloat16, priority='detect',
+              det_form=det_form)
     for _ in range(max(warmup - 1, 1)):
         st.eager_split()
     torch.cuda.synchronize()
@@ -698,6 +701,7 @@ def c2_figure(dev, steps, warmup, B=16, n_batches=12):
     torch.cuda.synchronize()
     return {'config': 'C2 SSD512 batch=%d bf16: MultiBoxLoss512(DIoU+focal) fwd+bwd in bf16 + detect '
                       '(bf16 activations read in place), captured, %d resident batches' % (B, n_batches),
+            'detect_form': det_form,
             'ms_per_step': round(ms, 4), 'images_per_s': round(B / (ms * 1e-3), 1),
             'criterion_algorithmic_bytes': crit_b, 'steps': steps,
             'runs_ms_per_step': [round(r, 4) for r in runs],
@@ -958,7 +962,7 @@ def main():
     if dp is not None:
         line['dp_train_step_with_grad_allreduce'] = dp
     if not a.no_c2 and world == 1:
-        line['c2_bf16'] = c2_figure(dev, a.steps, a.warmup)
+        line['c2_bf16'] = c2_figure(dev, a.steps, a.warmup, det_form=a.c2_det_form)
     if not a.no_dcn:
         maps = [dcn_figure(dev, H=h, iters=5 if h >= 32 else 20) for h in (64, 32, 16, 8)]
         tot_ms = sum(m['ms'] for m in maps)
