@@ -97,8 +97,8 @@ def parse(argv=None):
                          '(sbod_criterion_focal_lists), 0 = a separate sbod_gt_pack launch (the headline default: '
                          'same-box A/B 0.0345 vs 0.0353 ms at B=32; C2 at B=16 takes the fold)')
     ap.add_argument('--crit-split', type=int, choices=(0, 1), default=0,
-                    help='direct submit: 1 = the matcher on high-priority match streams (fork / join '
-                         'events), packing and loss pass on the criterion stream')
+                    help='direct submit: 1 = GT packing + matcher on high-priority match streams, the loss '
+                         'pass on the criterion stream after an event')
     ap.add_argument('--depth', type=int, default=4,
                     help='graph mode: steps in flight (submit step k, then collect step k - depth + 1)')
     ap.add_argument('--crit-streams', type=int, default=2,
@@ -318,8 +318,8 @@ class Step:
                  crit_streams=2, depth=4, submit='direct', gt_fold=True, crit_split=False):
         self.dev, self.B = dev, B
         self.gt_fold = bool(gt_fold)
-        # direct submit: the matcher on high-priority match streams between fork / join events, the
-        # GT packing and the loss pass on the criterion stream (sbod_criterion_focal_split)
+        # direct submit: the GT packing and the matcher on high-priority match streams, the loss pass
+        # on the criterion stream after an event (sbod_criterion_focal_split)
         self.crit_split = bool(crit_split) and submit == 'direct' and world == 1
         self.match_streams = ([torch.cuda.Stream(dev, priority=-1) for _ in range(2)] if self.crit_split else [])
         self._split_events = []
@@ -563,13 +563,12 @@ class Step:
                     stg = self.batches[bi].stage
                     split = ()
                     ps = cs
-                    if self.crit_split:   # the matcher on a high-priority match stream (fork / join events)
-                        ms = self.match_streams[bi % len(self.match_streams)]
-                        evs = [torch.cuda.Event(), torch.cuda.Event()]
-                        for e in evs:
-                            e.record(ms)   # creates the event
-                        self._split_events.extend(evs)
-                        split = (ms.cuda_stream, evs[0].cuda_event, evs[1].cuda_event)
+                    if self.crit_split:   # packing + matcher on a high-priority match stream
+                        ps = self.match_streams[bi % len(self.match_streams)]
+                        ev = torch.cuda.Event()
+                        ev.record(ps)      # creates the event
+                        self._split_events.append(ev)
+                        split = (ps.cuda_stream, ev.cuda_event)
                     prog = L.host_ext.make_step_program(
                         (stg.boxes.shape[0], stg.capacity, self.dev.index or 0, stg.boxes.data_ptr(),
                          stg.labels.data_ptr(), stg.offsets.data_ptr(), ps.cuda_stream),
