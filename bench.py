@@ -96,9 +96,6 @@ def parse(argv=None):
                     help='direct submit: 1 = the GT packing folded into the matcher\'s first launch '
                          '(sbod_criterion_focal_lists), 0 = a separate sbod_gt_pack launch (the headline default: '
                          'same-box A/B 0.0345 vs 0.0353 ms at B=32; C2 at B=16 takes the fold)')
-    ap.add_argument('--crit-split', type=int, choices=(0, 1), default=0,
-                    help='direct submit: 1 = GT packing + matcher on high-priority match streams, the loss '
-                         'pass on the criterion stream after an event')
     ap.add_argument('--depth', type=int, default=4,
                     help='graph mode: steps in flight (submit step k, then collect step k - depth + 1)')
     ap.add_argument('--crit-streams', type=int, default=2,
@@ -315,14 +312,9 @@ class Step:
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
-                 crit_streams=2, depth=4, submit='direct', gt_fold=True, crit_split=False):
+                 crit_streams=2, depth=4, submit='direct', gt_fold=True):
         self.dev, self.B = dev, B
         self.gt_fold = bool(gt_fold)
-        # direct submit: the GT packing and the matcher on high-priority match streams, the loss pass
-        # on the criterion stream after an event (sbod_criterion_focal_split)
-        self.crit_split = bool(crit_split) and submit == 'direct' and world == 1
-        self.match_streams = ([torch.cuda.Stream(dev, priority=-1) for _ in range(2)] if self.crit_split else [])
-        self._split_events = []
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
         self.priors = torch.from_numpy(Pn).to(dev)
@@ -561,19 +553,11 @@ class Step:
                     # the whole submit in one native call (list checks + packing, the two recorded
                     # entry points, the event)
                     stg = self.batches[bi].stage
-                    split = ()
-                    ps = cs
-                    if self.crit_split:   # packing + matcher on a high-priority match stream
-                        ps = self.match_streams[bi % len(self.match_streams)]
-                        ev = torch.cuda.Event()
-                        ev.record(ps)      # creates the event
-                        self._split_events.append(ev)
-                        split = (ps.cuda_stream, ev.cuda_event)
                     prog = L.host_ext.make_step_program(
                         (stg.boxes.shape[0], stg.capacity, self.dev.index or 0, stg.boxes.data_ptr(),
-                         stg.labels.data_ptr(), stg.offsets.data_ptr(), ps.cuda_stream),
+                         stg.labels.data_ptr(), stg.offsets.data_ptr(), cs.cuda_stream),
                         tuple(crit_calls[0][1]), tuple(det_calls[0][1]), h._event.cuda_event, ds.cuda_stream,
-                        self.gt_fold, *split)
+                        self.gt_fold)
                 self.programs.append(prog)
             torch.cuda.synchronize()
         elif L.host_ext is not None:
@@ -819,7 +803,7 @@ def main():
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
               n_batches=a.batches, order=a.order, det_streams=a.det_streams, crit_form=a.crit_form,
               det_form=a.det_form, crit_streams=a.crit_streams, depth=a.depth, submit=a.submit,
-              gt_fold=a.gt_fold, crit_split=a.crit_split)
+              gt_fold=a.gt_fold)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -946,7 +930,6 @@ def main():
         'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams),
         'pipeline_depth': st.depth, 'submit': st.submit,
         'gt_fold': st.gt_fold if st.submit == 'direct' else None,
-        'criterion_split': st.crit_split,
         'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,

@@ -292,17 +292,6 @@ int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *l
                                float focal_gamma, int32_t *obj, float *ovl, int32_t *n_pos, void *grad_locs,
                                void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
                                void *stream);
-/* The two-launch focal criterion with its matcher on a second stream (e.g. a high-priority one,
- * so the latency-bound matcher launches are not queued behind other streams' full-GPU grids):
- * the matcher runs on `match_stream`, `event` (a hipEvent_t the caller owns) is recorded there and
- * waited on by `stream`, which runs the loss pass.  Arguments otherwise as sbod_criterion_focal. */
-int sbod_criterion_focal_split(const void *locs, const void *scores, int dtype, int B, int P, int C,
-                               const float *priors_cxcy, const float *priors_xy, const float *gt_boxes,
-                               const int64_t *gt_labels, const int32_t *gt_offsets, int Gmax, float threshold,
-                               float neg_threshold, int reg, int flags, float reg_weight, float focal_alpha,
-                               float focal_gamma, int32_t *obj, float *ovl, int32_t *n_pos, void *grad_locs,
-                               void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
-                               void *stream, void *match_stream, void *event);
 int sbod_criterion_status(const void *workspace, void *stream);
 /* A/B knob of the focal loss pass: tiles per workgroup (1 = k_multibox, the default; 2..16 =
  * k_multibox_tiles, software-pipelined, bit-identical results).  n < 1 only queries.  Returns the

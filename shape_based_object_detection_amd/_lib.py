@@ -47,8 +47,6 @@ SIGNATURES = {
                                    P, P, P, P, P, P, P, SZ, P]),
     'sbod_criterion_focal_lists': (I32, [P, P, P, I64, P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32,
                                          I32, F32, F32, F32, P, P, P, P, P, P, P, SZ, P]),
-    'sbod_criterion_focal_split': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32, I32, F32, F32,
-                                         F32, P, P, P, P, P, P, P, SZ, P, P, P]),
     'sbod_criterion_status': (I32, [P, P]),
     'sbod_set_multibox_tiles': (I32, [I32]),
     'sbod_multibox_mine_global': (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, F32, P, I64, I64, P,

@@ -179,8 +179,7 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
 // detect's event.  One C++ call per step then does the list checks + sbod_gt_pack,
 // sbod_criterion_focal, sbod_detect_f32 and sbod_event_record — what a hipGraph replay does,
 // without two hipGraphLaunch calls and without Python between the launches.
-//   make_step_program(pack, crit_args, det_args, event, event_stream[, lists[, match_stream,
-//                     match_event]]) -> capsule
+//   make_step_program(pack, crit_args, det_args, event, event_stream[, lists]) -> capsule
 //     pack = (capacity, per_image_cap, device, out_boxes, out_labels, out_offsets, stream);
 //     crit_args / det_args = the recorded argument tuples of sbod_criterion_focal /
 //     sbod_detect_f32 (include/sbod.h order; pointers as int or None).
@@ -189,9 +188,7 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
 //   The lists are taken as ready on the packing stream (resident device tensors), which is the
 //   criterion's stream.  With `lists` true the packing is folded into the matcher's first launch
 //   (sbod_criterion_focal_lists) whenever the batch allows it (<= 64 images, each 1..Gmax
-//   objects, aligned rows); other batches take sbod_gt_pack + sbod_criterion_focal.  With a match
-//   stream (pack[6] should then be it) the criterion is sbod_criterion_focal_split: packing and
-//   matcher there, the loss pass on the recorded stream after match_event.
+//   objects, aligned rows); other batches take sbod_gt_pack + sbod_criterion_focal.
 struct StepProgram {
   long long capacity, per_image;
   int dev;
@@ -235,7 +232,6 @@ struct StepProgram {
   void *d_stream;
   void *event, *ev_stream;
   bool lists;
-  void *m_stream, *m_event;   // split form: the matcher on m_stream (sbod_criterion_focal_split)
 };
 
 struct ArgReader {   // the recorded tuple, item by item, in signature order
@@ -251,7 +247,7 @@ struct ArgReader {   // the recorded tuple, item by item, in signature order
 void free_program(PyObject *cap) { delete static_cast<StepProgram *>(PyCapsule_GetPointer(cap, "sbod.StepProgram")); }
 
 PyObject *make_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
-  if ((n != 5 && n != 6 && n != 8) || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) != 7 || !PyTuple_Check(a[1]) ||
+  if ((n != 5 && n != 6) || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) != 7 || !PyTuple_Check(a[1]) ||
       PyTuple_GET_SIZE(a[1]) != 28 || !PyTuple_Check(a[2]) || PyTuple_GET_SIZE(a[2]) != 25) {
     PyErr_SetString(PyExc_TypeError,
                     "make_step_program(pack[7], criterion_focal args[28], detect_f32 args[25], event, event_stream)");
@@ -286,14 +282,7 @@ PyObject *make_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   p->d_dbg_b = static_cast<float *>(d.ptr()); p->d_ws = d.ptr(); p->d_wsb = d.sz(); p->d_stream = d.ptr();
   p->event = opt_ptr(a[3]);
   p->ev_stream = opt_ptr(a[4]);
-  p->lists = n >= 6 && PyObject_IsTrue(a[5]) == 1;
-  p->m_stream = n == 8 ? opt_ptr(a[6]) : nullptr;
-  p->m_event = n == 8 ? opt_ptr(a[7]) : nullptr;
-  if (p->m_stream && !p->m_event) {
-    delete p;
-    PyErr_SetString(PyExc_TypeError, "make_step_program: a match stream needs its event");
-    return nullptr;
-  }
+  p->lists = n == 6 && PyObject_IsTrue(a[5]) == 1;
   if (PyErr_Occurred()) {
     delete p;
     return nullptr;
@@ -312,11 +301,11 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   if (!p) return nullptr;
   ListRows rows;
   const int r = pack_lists(a[1], a[2], p->capacity, p->per_image, p->dev, p->ob, p->ol, p->oo, p->pack_stream, 0,
-                           rows, p->pack_stream, !(p->lists && !p->m_stream));
+                           rows, p->pack_stream, !p->lists);
   if (r == 0) Py_RETURN_NONE;
   if (r < 0) return PyLong_FromLong(r);
   bool folded = false;
-  if (p->lists && !p->m_stream) {
+  if (p->lists) {
     const size_t B = rows.cnt.size();
     folded = B <= 64 && static_cast<int>(B) == p->c_B && p->ob == p->c_gtb && p->pack_stream == p->c_stream;
     for (size_t i = 0; folded && i < B; ++i)
@@ -337,11 +326,6 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
                                     static_cast<int32_t *>(p->oo), p->c_Gmax, p->c_thr, p->c_nthr, p->c_reg,
                                     p->c_flags, p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl,
                                     p->c_gs, p->c_out, p->c_ws, p->c_wsb, p->c_stream);
-  else if (p->m_stream)
-    st = sbod_criterion_focal_split(p->c_locs, p->c_scores, p->c_dtype, p->c_B, p->c_P, p->c_C, p->c_pcxcy,
-                                    p->c_pxy, p->c_gtb, p->c_gtl, p->c_gto, p->c_Gmax, p->c_thr, p->c_nthr, p->c_reg,
-                                    p->c_flags, p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl,
-                                    p->c_gs, p->c_out, p->c_ws, p->c_wsb, p->c_stream, p->m_stream, p->m_event);
   else
     st = sbod_criterion_focal(p->c_locs, p->c_scores, p->c_dtype, p->c_B, p->c_P, p->c_C, p->c_pcxcy, p->c_pxy,
                               p->c_gtb, p->c_gtl, p->c_gto, p->c_Gmax, p->c_thr, p->c_nthr, p->c_reg, p->c_flags,

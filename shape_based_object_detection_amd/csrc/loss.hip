@@ -1594,42 +1594,6 @@ int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *l
                             grad_locs, grad_scores, loss_out, ws.loss_ws, ws.loss_bytes, stream);
 }
 
-int sbod_criterion_focal_split(const void *locs, const void *scores, int dtype, int B, int P, int C,
-                               const float *priors_cxcy, const float *priors_xy, const float *gt_boxes,
-                               const int64_t *gt_labels, const int32_t *gt_offsets, int Gmax, float threshold,
-                               float neg_threshold, int reg, int flags, float reg_weight, float focal_alpha,
-                               float focal_gamma, int32_t *obj, float *ovl, int32_t *n_pos, void *grad_locs,
-                               void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
-                               void *stream, void *match_stream, void *event) {
-  SBOD_REQUIRE(B > 0 && P > 0 && C >= 2 && Gmax > 0 && locs && scores && priors_cxcy && priors_xy && gt_boxes &&
-                   gt_labels && gt_offsets && obj && ovl && n_pos && loss_out && event,
-               "sbod_criterion_focal_split: bad arguments (B=%d P=%d C=%d Gmax=%d)", B, P, C, Gmax);
-  SBOD_REQUIRE(dtype == SBOD_DT_F32 || dtype == SBOD_DT_BF16, "sbod_criterion_focal_split: dtype %d", dtype);
-  SBOD_REQUIRE(reg >= 0 && reg <= 2, "sbod_criterion_focal_split: reg %d", reg);
-  SBOD_REQUIRE((flags & ~(SBOD_LOSS_FOCAL_NORM | SBOD_CRIT_WS_ZEROED | SBOD_CRIT_TWO_LAUNCH |
-                          SBOD_LOSS_UNFUSED_FINISH)) == 0,
-               "sbod_criterion_focal_split: unknown flags 0x%x", flags);
-  const CritWs ws = carve_crit(workspace, B, Gmax, P);
-  if (workspace_bytes < ws.bytes) {
-    set_error("sbod_criterion_focal_split: workspace %zu < %zu", workspace_bytes, ws.bytes);
-    return SBOD_E_WORKSPACE;
-  }
-  hipStream_t ms = as_stream(match_stream), ls = as_stream(stream);
-  if ((flags & SBOD_CRIT_WS_ZEROED) == 0 && hipMemsetAsync(workspace, 0, ws.zero_bytes, ms) != hipSuccess)
-    return launch_status("hipMemsetAsync(criterion)");
-  const int st = sbod_match_f32(gt_boxes, gt_labels, gt_offsets, B, Gmax, priors_xy, nullptr, nullptr, P, threshold,
-                                0.01f, SBOD_MATCH_WS_ZEROED, obj, ovl, n_pos, ws.match_ws, ws.match_bytes, match_stream);
-  if (st != SBOD_OK) return st;
-  if (ms != ls && (hipEventRecord(static_cast<hipEvent_t>(event), ms) != hipSuccess ||
-                   hipStreamWaitEvent(ls, static_cast<hipEvent_t>(event), 0) != hipSuccess))
-    return launch_status("sbod_criterion_focal_split: event");
-  const int lflags = flags & (SBOD_LOSS_FOCAL_NORM | SBOD_LOSS_UNFUSED_FINISH);
-  return sbod_multibox_loss(locs, scores, dtype, B, P, C, priors_cxcy, nullptr, nullptr, gt_boxes, gt_labels,
-                            gt_offsets, obj, ovl, n_pos, n_pos + B, threshold, neg_threshold, 0.01f, reg,
-                            SBOD_CLS_FOCAL, lflags | SBOD_LOSS_WS_ZEROED, 3, reg_weight, focal_alpha, focal_gamma,
-                            grad_locs, grad_scores, loss_out, ws.loss_ws, ws.loss_bytes, stream);
-}
-
 int sbod_criterion_status(const void *workspace, void *stream) {
   // diagnostics: the one-launch criterion's wait-timeout word (nonzero: a wait gave up), read
   // with a stream synchronisation

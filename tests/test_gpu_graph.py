@@ -247,14 +247,10 @@ def test_graph_span_timing():
     L.call('sbod_timing_reset_graphs')
 
 
-@pytest.mark.parametrize('depth,two,submit,fold,split', [(2, True, 'graph', False, False),
-                                                          (3, True, 'graph', False, False),
-                                                          (3, False, 'graph', False, False),
-                                                          (4, True, 'direct', True, False),
-                                                          (4, True, 'direct', False, False),
-                                                          (4, True, 'direct', False, True),
-                                                          (4, True, 'fork', False, False)])
-def test_bench_pipelined_step_equals_eager(depth, two, submit, fold, split):
+@pytest.mark.parametrize('depth,two,submit,fold', [(2, True, 'graph', False), (3, True, 'graph', False),
+                                                    (3, False, 'graph', False), (4, True, 'direct', True),
+                                                    (4, True, 'direct', False), (4, True, 'fork', False)])
+def test_bench_pipelined_step_equals_eager(depth, two, submit, fold):
     """bench.Step as the bench runs it: per-batch criterion and detect graphs, each alternating over
     two streams (or, ``two`` False, one graph per step holding both), submitted by the one-call C++
     path — or, ``submit='direct'``, the recorded entry-point calls issued again without graphs —
@@ -262,15 +258,13 @@ def test_bench_pipelined_step_equals_eager(depth, two, submit, fold, split):
     with ``depth`` steps in flight and a criterion stream current.  Every step's loss, gradients and
     per-image detections equal the eager two-stream step on the same batch, across two rotations
     of the resident batches.  ``fold``: the direct submit's GT packing folded into the matcher's
-    first launch (sbod_criterion_focal_lists) instead of a separate sbod_gt_pack launch; ``split``:
-    packing + matcher on a high-priority match stream, the loss pass after an event
-    (sbod_criterion_focal_split)."""
+    first launch (sbod_criterion_focal_lists) instead of a separate sbod_gt_pack launch."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     st = bench.Step(DEV, 4, 0, 1, graph=True, two_streams=two, priority='detect', n_batches=4, det_streams=2,
-                    crit_streams=2, depth=depth, submit=submit, gt_fold=fold, crit_split=split)
+                    crit_streams=2, depth=depth, submit=submit, gt_fold=fold)
     ref = []
     for bt in st.batches:          # eager reference per batch (also warms both detect streams)
         loss, dets = st.eager_split()
