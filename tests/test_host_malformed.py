@@ -58,7 +58,7 @@ def _call_all(value):
     lib = L.lib()
     out = {}
     skip = {'sbod_timing_enable', 'sbod_timing_query', 'sbod_timing_every', 'sbod_timing_reset_graphs',
-            'sbod_memcpy_d2h_async', 'sbod_stream_wait'}
+            'sbod_memcpy_d2h_async', 'sbod_stream_wait', 'sbod_set_multibox_tiles'}   # (a knob, not a call)
     for name, (res, args) in L.SIGNATURES.items():
         if name in skip or not args:
             continue
@@ -90,3 +90,33 @@ def test_every_entry_point_validates_null_and_bad_sizes(value):
 
 def test_stream_wait_same_stream_is_a_noop():
     assert L.lib().sbod_stream_wait(None, None) == 0
+
+
+def test_step_program_rejects_malformed_recordings(ext):
+    """make_step_program parses the recorded argument tuples once: wrong arities are TypeErrors,
+    and submit_step_program needs the capsule it made (nothing is launched on either failure)."""
+    def recorded(name):   # a recording of the right types: NULL pointers, zero sizes
+        vals = []
+        for t in L.SIGNATURES[name][1]:
+            vals.append(None if t is ctypes.c_void_p else (0.0 if t in (ctypes.c_float, ctypes.c_double) else 0))
+        return tuple(vals)
+    pack = (64, 16, 0, 0, 0, 0, None)
+    crit = recorded('sbod_criterion_focal')
+    det = recorded('sbod_detect_f32')
+    assert len(crit) == 28 and len(det) == 25
+    with pytest.raises(TypeError):
+        ext.make_step_program(pack[:6], crit, det, None, None)
+    with pytest.raises(TypeError):
+        ext.make_step_program(pack, crit[:27], det, None, None)
+    with pytest.raises(TypeError):
+        ext.make_step_program(pack, crit, det + (None,), None, None)
+    with pytest.raises(TypeError):
+        ext.make_step_program(pack, crit, det, None)                          # argument count
+    prog = ext.make_step_program(pack, crit, det, None, None, True)
+    with pytest.raises((TypeError, ValueError)):
+        ext.submit_step_program(object(), [], [])                            # not the capsule
+    with pytest.raises(TypeError):
+        ext.submit_step_program(prog, [])
+    b = [torch.zeros(3, 4)]
+    l = [torch.zeros(3, dtype=torch.long)]
+    assert ext.submit_step_program(prog, b, l) is None                       # CPU lists: Python path
