@@ -115,11 +115,12 @@ __global__ __launch_bounds__(256) void k_dcn_coef(DcnShape s, const float *__res
 
 // Batched transpose in [nb][R][S] -> out [nb][S][R] (64 x 64 LDS tiles); zeroes `zero` [n_zero]
 // on the side (the sample counters the coefficient pass that follows increments).
-// One 64 x 64 tile (bx, by) of slice bz, through `t` (LDS).
-__device__ __forceinline__ void transpose_tile(const float *__restrict__ in, float *__restrict__ out, int R, int S,
-                                               int bx, int by, int bz, float (*t)[65]) {
-  const int s0 = bx * 64, r0 = by * 64;
-  const int64_t base = static_cast<int64_t>(bz) * R * S;
+__global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ in, float *__restrict__ out,
+                                                   int R, int S, float *__restrict__ zero, int64_t n_zero) {
+  zero_fill(zero, n_zero);
+  __shared__ float t[64][65];
+  const int s0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  const int64_t base = static_cast<int64_t>(blockIdx.z) * R * S;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int r = r0 + i, s = s0 + tx;
@@ -131,20 +132,14 @@ __device__ __forceinline__ void transpose_tile(const float *__restrict__ in, flo
     if (r < R && s < S) out[base + static_cast<int64_t>(s) * R + r] = t[tx][i];
   }
 }
-__global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ in, float *__restrict__ out,
-                                                   int R, int S, float *__restrict__ zero, int64_t n_zero) {
-  zero_fill(zero, n_zero);
-  __shared__ float t[64][65];
-  transpose_tile(in, out, R, S, blockIdx.x, blockIdx.y, blockIdx.z, t);
-}
 
 // conv.weight [O][C][N] -> the forward's Wf [O][N][C] and (training) the backward's Wb [N][O][C]
 // in one pass: one block per (64-channel chunk, output channel), the chunk's 64 x N contiguous
 // weights staged in LDS, each layout's rows written along c.
-__device__ __forceinline__ void weight_layouts_block(const float *__restrict__ w, int O, int C, int N,
-                                                     float *__restrict__ wf, float *__restrict__ wb, int bx, int o,
-                                                     float (*t)[kMaxN + 1]) {
-  const int c0 = bx * 64;
+__global__ __launch_bounds__(256) void k_weight_layouts(const float *__restrict__ w, int O, int C, int N,
+                                                        float *__restrict__ wf, float *__restrict__ wb) {
+  __shared__ float t[64][kMaxN + 1];
+  const int c0 = blockIdx.x * 64, o = blockIdx.y;
   const int nc = min(64, C - c0);
   const float *src = w + (static_cast<int64_t>(o) * C + c0) * N;
   for (int e = threadIdx.x; e < nc * N; e += blockDim.x) t[e / N][e % N] = src[e];
@@ -155,25 +150,6 @@ __device__ __forceinline__ void weight_layouts_block(const float *__restrict__ w
     const float v = t[cl][n];
     wf[(static_cast<int64_t>(o) * N + n) * C + c0 + cl] = v;
     if (wb) wb[(static_cast<int64_t>(n) * O + o) * C + c0 + cl] = v;
-  }
-}
-
-// The state derivation's two independent passes in ONE launch (block ranges): blocks [0, n_t)
-// transpose x [B][C][HW] -> xt [B][HW][C] (tiles t_gx x t_gy per image), the rest build the
-// weight layouts (w_gx chunks x O); every block zeroes its share of `zero` (the sample counters).
-__global__ __launch_bounds__(256) void k_dcn_prep(const float *__restrict__ x, float *__restrict__ xt, int C, int HW,
-                                                  int n_t, int t_gx, int t_gy, const float *__restrict__ w, int O,
-                                                  int N, float *__restrict__ wf, float *__restrict__ wb, int w_gx,
-                                                  float *__restrict__ zero, int64_t n_zero) {
-  zero_fill(zero, n_zero);
-  __shared__ float t[64][65];
-  static_assert(kMaxN + 1 <= 65, "k_dcn_prep: the layouts' LDS rows share the transpose tile");
-  const int id = blockIdx.x;
-  if (id < n_t) {
-    transpose_tile(x, xt, C, HW, id % t_gx, (id / t_gx) % t_gy, id / (t_gx * t_gy), t);
-  } else {
-    const int j = id - n_t;
-    weight_layouts_block(w, O, C, N, wf, wb, j % w_gx, j / w_gx, reinterpret_cast<float (*)[kMaxN + 1]>(t));
   }
 }
 
@@ -1021,18 +997,16 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
                       hipStream_t hs) {
   const int64_t npix = static_cast<int64_t>(s.B) * s.H * s.W;
   const int HW = s.H * s.W;
-  {   // x [B][C][HW] -> xt [B][HW][C] and the two weight layouts, one launch
-    const int t_gx = (HW + 63) / 64, t_gy = (s.C + 63) / 64, w_gx = (s.C + 63) / 64;
-    const int n_t = t_gx * t_gy * s.B, n_w = w_gx * s.O;
-    hipLaunchKernelGGL(k_dcn_prep, dim3(n_t + n_w), dim3(256), 0, hs, x, st.xt, s.C, HW, n_t, t_gx, t_gy, weight,
-                       s.O, s.N, st.wf, train ? st.wb : nullptr, w_gx,
-                       train ? reinterpret_cast<float *>(st.tcount) : nullptr, train ? npix + 1 : 0);
-    SBOD_LAUNCHED("k_dcn_prep");
-  }
+  hipLaunchKernelGGL(k_transpose, dim3((HW + 63) / 64, (s.C + 63) / 64, s.B), dim3(256), 0, hs, x, st.xt, s.C, HW,
+                     train ? reinterpret_cast<float *>(st.tcount) : nullptr, train ? npix + 1 : 0);
+  SBOD_LAUNCHED("k_transpose(x)");   // x [B][C][HW] -> xt [B][HW][C]
   const int64_t nc = static_cast<int64_t>(s.M) * s.N;
   hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, st.coef,
                      train ? st.tcount : nullptr, zero_out, n_zero_out);
   SBOD_LAUNCHED("k_dcn_coef");
+  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
+                     train ? st.wb : nullptr);
+  SBOD_LAUNCHED("k_weight_layouts");
   return SBOD_OK;
 }
 
