@@ -11,7 +11,7 @@ out=gpurun_out/wg_ab_$TAG.jsonl
 : > $out
 for r in 1 2; do
   timeout -k 10 240 python -u scripts/dcn_maps.py --iters 10 >> $out 2>> gpurun_out/wg_ab_$TAG.err || exit 1
-  for v in wg768 wg1024; do
+  for v in ${VARIANTS:-wg768 wg1024}; do
     SBOD_LIB=$V/libsbod_hip_$v.so timeout -k 10 240 python -u scripts/dcn_maps.py --iters 10 >> $out \
         2>> gpurun_out/wg_ab_$TAG.err || exit 1
   done
