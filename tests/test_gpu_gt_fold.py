@@ -97,13 +97,21 @@ def test_criterion_lists_equals_pack_then_criterion(kind, arch, B, reg, dtype, m
     np.testing.assert_array_equal(a['go'].cpu().numpy(), offs)
 
 
-@pytest.mark.parametrize('flags', [0, L.MATCH_BINARY])
+@pytest.mark.parametrize('flags', [0, L.MATCH_BINARY, L.MATCH_ODM])
 def test_match_lists_equals_pack_then_match(flags):
+    """Plain (SSD / RetinaNet), binary (RefineDet ARM) and ODM (RefineDet: anchors = the ARM locs
+    decoded against the priors, easy negatives from the ARM scores) matcher forms."""
     B = 16
     boxes, labels = _lists(B, seed=41, max_objects=40)
     P = torch.from_numpy(prior_table('SSD512')).to(DEV)
     pxy = torch.cat([P[:, :2] - P[:, 2:] / 2, P[:, :2] + P[:, 2:] / 2], 1).contiguous()
     NP = P.shape[0]
+    pri, arm_sc = None, None
+    if flags == L.MATCH_ODM:
+        g = torch.Generator(device=DEV).manual_seed(5)
+        pxy = (torch.randn(B, NP, 4, device=DEV, generator=g) * 0.5).contiguous()    # ARM locs (gcxgcy)
+        pri = P.contiguous()
+        arm_sc = torch.randn(B, NP, 2, device=DEV, generator=g).contiguous()
     cap = sum(b.shape[0] for b in boxes)
     gmax = max(b.shape[0] for b in boxes)
     nb = L.lib().sbod_match_workspace_bytes_p(B, gmax, NP)
@@ -116,8 +124,8 @@ def test_match_lists_equals_pack_then_match(flags):
         ovl = torch.empty(B, NP, dtype=torch.float32, device=DEV)
         npos = torch.empty(B + 1, dtype=torch.int32, device=DEV)
         ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
-        tail = (L.ptr(pxy), None, None, NP, 0.5, 0.01, flags, L.ptr(obj), L.ptr(ovl), L.ptr(npos), L.ptr(ws), nb,
-                stream)
+        tail = (L.ptr(pxy), L.ptr(pri), L.ptr(arm_sc), NP, 0.5, 0.01, flags, L.ptr(obj), L.ptr(ovl), L.ptr(npos),
+                L.ptr(ws), nb, stream)
         if fold:
             L.call('sbod_match_lists_f32', bp, lp, cnt, cap, L.ptr(gb), L.ptr(gl_), L.ptr(go), B, gmax, *tail)
         else:
