@@ -727,17 +727,20 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
               for (int k = 0; k < CM; ++k)
                 if (in_row(k)) row[k] = loss;
             } else {
-              // kq * (onehot - p), p = e * inv (the same values the loss used), two classes per op
+              // kq * (onehot - p), p = e * inv (the same values the loss used), two classes per op:
+              // every slot gets p * (-kq) (= (0 - p) * kq exactly), then the target slot is
+              // rewritten as (1 - p_t) * kq with p_t = q (e_t * inv, the same value) — the one-hot
+              // selects per slot cost a compare and a select each
               const float kq = dq * q * scale;
-              const f2 inv2 = {inv, inv}, kq2 = {kq, kq};
+              const f2 inv2 = {inv, inv}, nkq2 = {-kq, -kq};
 #pragma unroll
               for (int k = 0; k < CM; k += 2) {
                 const f2 pp = f2{in_row(k) ? row[k] : 0.f, in_row(k + 1) ? row[k + 1] : 0.f} * inv2;
-                const f2 oh = {k == c ? 1.f : 0.f, k + 1 == c ? 1.f : 0.f};
-                const f2 g = (oh - pp) * kq2;
+                const f2 g = pp * nkq2;
                 if (in_row(k)) row[k] = g.x;
                 if (in_row(k + 1)) row[k + 1] = g.y;
               }
+              row[c] = (1.f - q) * kq;
             }
           }
         } else if (grad) {
