@@ -667,7 +667,12 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
         const float x = row[k];
         r[k] = in_row(k) ? x : -__builtin_inff();
         m = fmaxf(m, r[k]);                       // a NaN logit gives a NaN loss either way
-        zmin = (in_row(k) && r[k] < zmin) ? r[k] : zmin;
+        // (only the top 8 slots can be padding: the others take one v_min instead of a compare
+        // and a select — same minimum; a NaN logit is skipped either way)
+        if (k < CM - 8)
+          zmin = fminf(zmin, r[k]);
+        else
+          zmin = (in_row(k) && r[k] < zmin) ? r[k] : zmin;
       }
       const float zt = row[c];
       float s = 0.f;
