@@ -740,7 +740,9 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
               const f2 inv2 = {inv, inv}, nkq2 = {-kq, -kq};
 #pragma unroll
               for (int k = 0; k < CM; k += 2) {
-                const f2 pp = f2{in_row(k) ? row[k] : 0.f, in_row(k + 1) ? row[k + 1] : 0.f} * inv2;
+                // constant-offset reads of every slot (a padding slot reads the next row or the 8
+                // floats past the tile, and its value is never stored)
+                const f2 pp = f2{row[k], row[k + 1]} * inv2;
                 const f2 g = pp * nkq2;
                 if (in_row(k)) row[k] = g.x;
                 if (in_row(k + 1)) row[k + 1] = g.y;
