@@ -545,7 +545,10 @@ __device__ __forceinline__ unsigned wait_all_images(unsigned long long *done, in
 struct NoPrefetch {
   __device__ void operator()() const {}
 };
-template <typename T, int CM, int CLS, typename Pf = NoPrefetch>
+// CE > 0: rows of exactly CE classes (CE <= CM; VOC's 21): the per-slot loops run over CE slots,
+// with no padding slots to compute or guard — the same values as the CM-slot form (a padding
+// slot only ever adds exp(-inf) = 0 or an ignored value).
+template <typename T, int CM, int CLS, int CE = 0, typename Pf = NoPrefetch>
 __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__restrict__ locs, T *__restrict__ glocs,
                                               T *__restrict__ gsc, int p0, int64_t rbase, bool valid, int64_t ic,
                                               int objv, float v, int64_t labg, int offb, float n, float *s_sc,
@@ -657,19 +660,20 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
     // ---------------- classification
     float *row = s_sc + tid * C;
     if constexpr (CM > 0) {
+      constexpr int KN = CE > 0 ? CE : CM;   // slots walked
       float r[CM];
       float m = -__builtin_inff(), zmin = __builtin_inff();
       // constant-offset reads (no per-slot index arithmetic; a short last row reads into the 8
       // padding floats after the tile); only the top 8 slots can be padding (C > CM - 8)
-      auto in_row = [&](int k) { return k < CM - 8 || k < C; };
+      auto in_row = [&](int k) { return CE > 0 || k < CM - 8 || k < C; };
 #pragma unroll
-      for (int k = 0; k < CM; ++k) {
+      for (int k = 0; k < KN; ++k) {
         const float x = row[k];
         r[k] = in_row(k) ? x : -__builtin_inff();
         m = fmaxf(m, r[k]);                       // a NaN logit gives a NaN loss either way
         // (only the top 8 slots can be padding: the others take one v_min instead of a compare
         // and a select — same minimum; a NaN logit is skipped either way)
-        if (k < CM - 8)
+        if (CE > 0 || k < CM - 8)
           zmin = fminf(zmin, r[k]);
         else
           zmin = (in_row(k) && r[k] < zmin) ? r[k] : zmin;
@@ -687,19 +691,24 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
         const f2 nm2 = {-m, -m}, l2 = {1.4426950408889634f, 1.4426950408889634f};
         f2 acc2 = {0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < CM; k += 2) {   // CM is a multiple of 8
+        for (int k = 0; k + 1 < KN; k += 2) {   // CM is a multiple of 8
           const f2 t = (f2{r[k], r[k + 1]} + nm2) * l2;
           const f2 ex = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};   // padding: 0
           acc2 += ex;
           if (in_row(k)) row[k] = ex.x;
           if (in_row(k + 1)) row[k + 1] = ex.y;
         }
+        if constexpr (KN % 2 == 1) {   // the last (even) slot: the x lane of its pair
+          const float ex = __builtin_amdgcn_exp2f((r[KN - 1] + nm2.x) * l2.x);
+          acc2.x += ex;
+          row[KN - 1] = ex;
+        }
         s = acc2.x + acc2.y;
       } else {
         // CE feeds the hard-negative selection (a ranking): the accurate exp keeps its values
         // within an ulp of the reference's so near-ties at the top-k boundary do not move
 #pragma unroll
-        for (int k = 0; k < CM; ++k) s += expf(r[k] - m);
+        for (int k = 0; k < KN; ++k) s += expf(r[k] - m);
       }
       const float inv = 1.f / s;
       if constexpr (CLS == SBOD_CLS_FOCAL) {
@@ -729,7 +738,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
           if (grad) {
             if (loss != loss) {
 #pragma unroll
-              for (int k = 0; k < CM; ++k)
+              for (int k = 0; k < KN; ++k)
                 if (in_row(k)) row[k] = loss;
             } else {
               // kq * (onehot - p), p = e * inv (the same values the loss used), two classes per op:
@@ -739,7 +748,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
               const float kq = dq * q * scale;
               const f2 inv2 = {inv, inv}, nkq2 = {-kq, -kq};
 #pragma unroll
-              for (int k = 0; k < CM; k += 2) {
+              for (int k = 0; k + 1 < KN; k += 2) {
                 // constant-offset reads of every slot (a padding slot reads the next row or the 8
                 // floats past the tile, and its value is never stored)
                 const f2 pp = f2{row[k], row[k + 1]} * inv2;
@@ -747,12 +756,13 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
                 if (in_row(k)) row[k] = g.x;
                 if (in_row(k + 1)) row[k + 1] = g.y;
               }
+              if constexpr (KN % 2 == 1) row[KN - 1] = (row[KN - 1] * inv2.x) * nkq2.x;
               row[c] = (1.f - q) * kq;
             }
           }
         } else if (grad) {
 #pragma unroll
-          for (int k = 0; k < CM; ++k)
+          for (int k = 0; k < KN; ++k)
             if (in_row(k)) row[k] = 0.f;
         }
       } else {
@@ -763,7 +773,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
           if (grad) {
             const float sc = 1.f / n;
 #pragma unroll
-            for (int k = 0; k < CM; ++k)
+            for (int k = 0; k < KN; ++k)
               if (in_row(k)) row[k] = (expf(row[k] - m) * inv - (k == c ? 1.f : 0.f)) * sc;
           }
         } else {
@@ -775,7 +785,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
           a.pool[i] = member ? ce : -1.f;
           if (grad) {
 #pragma unroll
-            for (int k = 0; k < CM; ++k)
+            for (int k = 0; k < KN; ++k)
               if (in_row(k)) row[k] = 0.f;
           }
         }
@@ -829,7 +839,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
 // forced match (match_final_image) and counts the image in; every workgroup then loads its score
 // tile, waits for all images (the normaliser), applies the forced rewrites of its own priors from
 // the image's list, and goes on with the loss pass on registers it already holds.
-template <typename T, int CM, int CLS, bool kFused>
+template <typename T, int CM, int CLS, bool kFused, int CE = 0>
 __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs a, const T *__restrict__ locs,
                                                      const T *__restrict__ scores,
                                                      T *__restrict__ glocs, T *__restrict__ gsc) {
@@ -943,8 +953,8 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   SEG_PHASE(1);
   const bool grad = gsc != nullptr;
   float conf_l = 0.f, loc_l = 0.f;
-  multibox_rows<T, CM, CLS>(a, locs, glocs, gsc, p0, rbase, valid, ic, objv, v, labg, offb, n, s_sc, s_plist, s_wcnt,
-                            conf_l, loc_l);
+  multibox_rows<T, CM, CLS, CE>(a, locs, glocs, gsc, p0, rbase, valid, ic, objv, v, labg, offb, n, s_sc, s_plist,
+                                s_wcnt, conf_l, loc_l);
   __syncthreads();
   SEG_PHASE(2);
   // the gradient tile: with SBOD_MB_W0_NOSTORE wave 0 (which runs the finish and its drain) stores
@@ -1683,17 +1693,24 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
 #define SBOD_MB(T, CM, CLS)                                                                       \
   tlaunch(kt, (k_multibox<T, CM, CLS, false>), grid, dim3(kLTile), lds, s, a, static_cast<const T *>(locs), \
                      static_cast<const T *>(scores), static_cast<T *>(grad_locs), static_cast<T *>(grad_scores))
+    // VOC's 21 classes: the exact-width rows (no padding slots)
+#define SBOD_MB21(T, CLS)                                                                          \
+  tlaunch(kt, (k_multibox<T, 24, CLS, false, 21>), grid, dim3(kLTile), lds, s, a,                  \
+          static_cast<const T *>(locs), static_cast<const T *>(scores), static_cast<T *>(grad_locs),    \
+          static_cast<T *>(grad_scores))
     // rows of C <= CM classes in registers; wider rows take the LDS path
 #define SBOD_MB_C(T)                                                  \
   do {                                                                \
     if (cls == SBOD_CLS_FOCAL) {                                      \
-      if (C <= 8) SBOD_MB(T, 8, SBOD_CLS_FOCAL);                      \
+      if (C == 21) SBOD_MB21(T, SBOD_CLS_FOCAL);                      \
+      else if (C <= 8) SBOD_MB(T, 8, SBOD_CLS_FOCAL);                 \
       else if (C <= 16) SBOD_MB(T, 16, SBOD_CLS_FOCAL);               \
       else if (C <= 24) SBOD_MB(T, 24, SBOD_CLS_FOCAL);               \
       else if (C <= 32) SBOD_MB(T, 32, SBOD_CLS_FOCAL);               \
       else SBOD_MB(T, 0, SBOD_CLS_FOCAL);                             \
     } else {                                                          \
-      if (C <= 8) SBOD_MB(T, 8, SBOD_CLS_CE);                         \
+      if (C == 21) SBOD_MB21(T, SBOD_CLS_CE);                         \
+      else if (C <= 8) SBOD_MB(T, 8, SBOD_CLS_CE);                    \
       else if (C <= 16) SBOD_MB(T, 16, SBOD_CLS_CE);                  \
       else if (C <= 24) SBOD_MB(T, 24, SBOD_CLS_CE);                  \
       else if (C <= 32) SBOD_MB(T, 32, SBOD_CLS_CE);                  \
@@ -1703,6 +1720,7 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
     if (dtype == SBOD_DT_F32) SBOD_MB_C(float);
     else SBOD_MB_C(uint16_t);
 #undef SBOD_MB_C
+#undef SBOD_MB21
 #undef SBOD_MB
   }
   SBOD_LAUNCHED("k_multibox");
