@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SBOD_ABI_VERSION 3
+#define SBOD_ABI_VERSION 4
 
 typedef enum sbod_status {
   SBOD_OK = 0,
@@ -43,6 +43,11 @@ typedef enum sbod_status {
 const char *sbod_version(void);
 int sbod_abi_version(void);
 const char *sbod_last_error(void);
+/* Compile-time variants built into this library (bit mask): SBOD_VARIANT_ONE_LAUNCH_CRITERION =
+ * the one-launch focal criterion of sbod_criterion_focal (A/B builds only,
+ * scripts/build_variant_lib.sh; the product library has none and always runs two launches). */
+enum { SBOD_VARIANT_ONE_LAUNCH_CRITERION = 1 };
+int sbod_build_variants(void);
 
 /* Kernel timing for benchmarks: kernel_filter = a kernel name ("k_det_prepare"), "*" for every
  * instrumented kernel, or NULL / "" to stop.  Each call clears previous records.  Matching
@@ -222,12 +227,12 @@ size_t sbod_loss_workspace_bytes(int B, int P);
  * holding the whole batch; the hard-negative gradients and the loss cover this rank's rows
  * (the sum over ranks is the single-device loss).  Same workspace as the deferred call. */
 enum { SBOD_LOSS_DEFER_MINING = 64 };
-/* Focal criteria (no mining pass) finish the loss inside the fused pass: its workgroups fold
- * their partial sums into exact 128-bit fixed-point accumulators (2^-64 resolution; a partial
- * that is non-finite or >= 2^40 in magnitude switches the finish to a double sum of the fp32
- * partials, as the separate finaliser computes it) in the workspace's first
- * sbod_loss_zero_prefix_bytes() bytes, which must be zero on entry and are left zero by every
- * successful call (any B, P).  A caller that knows the workspace is clean (a previous successful
+/* Focal criteria (no mining pass) finish the loss inside the fused pass: the last workgroup to
+ * arrive sums every workgroup's fp32 partials exactly, as 128-bit fixed-point integers (2^-64
+ * resolution; a partial that is non-finite or >= 2^40 in magnitude switches the finish to a
+ * double sum of the fp32 partials, as the separate finaliser computes it).  Its arrival counters
+ * live in the workspace's first sbod_loss_zero_prefix_bytes() bytes, which must be zero on entry
+ * and are left zero by every successful call (any B, P).  A caller that knows the workspace is clean (a previous successful
  * call on it) passes SBOD_LOSS_WS_ZEROED and the call issues no memset (hipGraph capture);
  * without it the call zeroes them first (one hipMemsetAsync).  SBOD_LOSS_UNFUSED_FINISH
  * (diagnostics, tests) finishes a focal criterion with the separate finaliser launch instead
@@ -262,14 +267,18 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
  * grad_locs / grad_scores (may be NULL), loss_out {total, conf, loc, n_pos}.
  * The grid (B * ceil(P/256) workgroups) must be resident at once; when the occupancy query says
  * it is not (or with SBOD_CRIT_TWO_LAUNCH / SBOD_LOSS_UNFUSED_FINISH) the call runs the two
- * launches instead, on the same workspace, with the same results.  Data parallelism (a
+ * launches instead, on the same workspace, with the same results.  The one-launch form exists
+ * only in a variant library (sbod_build_variants() & SBOD_VARIANT_ONE_LAUNCH_CRITERION): its
+ * workgroups wait for each other, which stalls when other streams' kernels hold CUs (measured,
+ * DESIGN.md round 4); the product library always runs the two launches.  Data parallelism (a
  * normaliser all-reduced between the matcher and the loss) uses the two calls.
  * Workspace: sbod_criterion_workspace_bytes(B, Gmax, P); its first
  * sbod_criterion_zero_bytes(B, Gmax, P) bytes must be zero on entry and are left zero by every
  * successful call: pass SBOD_CRIT_WS_ZEROED when they are (else the call zeroes them, one
  * hipMemsetAsync).  flags: SBOD_LOSS_FOCAL_NORM, SBOD_CRIT_WS_ZEROED, SBOD_CRIT_TWO_LAUNCH,
  * SBOD_LOSS_UNFUSED_FINISH.  sbod_criterion_status() (diagnostics, synchronises the stream) reads
- * the word a bounded in-launch wait sets if it ever gives up (the loss is NaN then). */
+ * the sticky word the one-launch form sets if a bounded in-launch wait ever gave up (that call's
+ * loss and its waiting workgroups' gradients are NaN; the next call starts clean). */
 enum { SBOD_CRIT_WS_ZEROED = 128, SBOD_CRIT_TWO_LAUNCH = 1024 };
 size_t sbod_criterion_workspace_bytes(int B, int Gmax, int P);
 size_t sbod_criterion_zero_bytes(int B, int Gmax, int P);
@@ -293,10 +302,6 @@ int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *l
                                void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
                                void *stream);
 int sbod_criterion_status(const void *workspace, void *stream);
-/* A/B knob of the focal loss pass: tiles per workgroup (1 = k_multibox, the default; 2..16 =
- * k_multibox_tiles, software-pipelined, bit-identical results).  n < 1 only queries.  Returns the
- * previous value.  Initialised from the environment variable SBOD_MB_TILES when the library loads. */
-int sbod_set_multibox_tiles(int n);
 
 /* grad *= (*scale) in place unless *scale == 1 (decided on the device: no host sync).
  * Used by backward to apply the upstream gradient to gradients produced by the fused
@@ -351,13 +356,18 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
  *   SBOD_DETECT_INPUT_BF16 — locs and scores hold bf16 (C <= 32): each value is widened to fp32
  *   exactly on load, so the results equal those of the fp32 call on the widened tensors (no
  *   widened copies in HBM).  Without it both are fp32.
- *   Without a final NMS (window 0, C <= 64) the per-class NMS and the per-image merge run as ONE
- *   launch (the image's last class merges) and an image its first window of 64 candidates per
- *   class cannot decide reports det_count -1 (re-run it with a wider window); SBOD_DETECT_TWO_PASS
- *   keeps them two launches with the wider second window run inline (diagnostics, A/B).
+ *   The per-class NMS and the per-image merge run as two launches, the merge running a wider
+ *   second window inline for a class whose first window was truncated.  SBOD_DETECT_FUSED (ABI 4;
+ *   opt-in) runs them as ONE launch when there is no final NMS (window 0, C <= 64): the image's
+ *   last class merges, and an image its first window of 64 candidates per class cannot decide
+ *   reports det_count -1 (the caller re-runs it with a wider window).
+ *   Every kernel after k_det_prepare decodes prior indices from candidate keys; an index >= P
+ *   (a corrupted or stale candidate region) is never dereferenced: the image reports
+ *   det_count -2 (SBOD_DETECT_CORRUPT) and its outputs are unspecified.
  * Workspace: sbod_detect_workspace_bytes(B, P, C). */
 enum { SBOD_BOX_OFFSET = 0, SBOD_BOX_CENTER = 1, SBOD_BOX_CORNER = 2 };
-enum { SBOD_DETECT_COUNTERS_ZEROED = 1, SBOD_DETECT_INPUT_BF16 = 2, SBOD_DETECT_TWO_PASS = 4 };
+enum { SBOD_DETECT_COUNTERS_ZEROED = 1, SBOD_DETECT_INPUT_BF16 = 2, SBOD_DETECT_FUSED = 8 };
+enum { SBOD_DETECT_CORRUPT = -2 };
 size_t sbod_detect_counter_bytes(int B, int C);
 enum { SBOD_ACT_SOFTMAX = 0, SBOD_ACT_SIGMOID = 1 };
 size_t sbod_detect_workspace_bytes(int B, int P, int C);

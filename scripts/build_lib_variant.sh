@@ -13,5 +13,6 @@ for f in shape_based_object_detection_amd/csrc/*.hip; do
     -Iinclude -Ishape_based_object_detection_amd/csrc -c $f -o $OUT/$(basename $f).o &
 done
 wait
+for f in shape_based_object_detection_amd/csrc/*.hip; do test $OUT/$(basename $f).o -nt $f || { echo "compile failed: $f"; exit 1; }; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $LIBV/libsbod_hip_$NAME.so $OUT/*.o
 echo built $LIBV/libsbod_hip_$NAME.so

@@ -25,6 +25,7 @@ SIGNATURES = {
     'sbod_version': (ctypes.c_char_p, []),
     'sbod_abi_version': (I32, []),
     'sbod_last_error': (ctypes.c_char_p, []),
+    'sbod_build_variants': (I32, []),
     'sbod_null_kernel': (I32, [I32, P]),
     'sbod_iou_pairwise_f32': (I32, [P, P, I32, I32, P, I64, I32, I32, P, P]),
     'sbod_match_workspace_bytes': (SZ, [I32, I32]),
@@ -48,7 +49,6 @@ SIGNATURES = {
     'sbod_criterion_focal_lists': (I32, [P, P, P, I64, P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32,
                                          I32, F32, F32, F32, P, P, P, P, P, P, P, SZ, P]),
     'sbod_criterion_status': (I32, [P, P]),
-    'sbod_set_multibox_tiles': (I32, [I32]),
     'sbod_multibox_mine_global': (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, F32, P, I64, I64, P,
                                         P, P, SZ, P]),
     'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),
@@ -104,7 +104,9 @@ FOCAL = dict(softmax=0, sigmoid=1, bce=2)
 BOX = dict(offset=0, center=1, corner=2)
 ACT = dict(softmax=0, sigmoid=1)
 NMS = dict(tv=0, ref=1, diou=2)
-DETECT_COUNTERS_ZEROED, DETECT_INPUT_BF16, DETECT_TWO_PASS = 1, 2, 4
+DETECT_COUNTERS_ZEROED, DETECT_INPUT_BF16, DETECT_FUSED = 1, 2, 8
+DETECT_CORRUPT = -2
+VARIANT_ONE_LAUNCH_CRITERION = 1
 
 
 class SbodError(RuntimeError):

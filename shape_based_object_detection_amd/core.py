@@ -453,7 +453,13 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
     """A focal criterion on one device in ONE launch (sbod_criterion_focal): the matcher and the
     fused loss + gradient pass, the normaliser produced inside the launch.  Returns (scalar loss
     with autograd, device vector {total, conf, loc, n_pos_total}, (obj, ovl, n_pos)).
-    ``two_launch`` runs the same call as the matcher and loss launches (A/B, tests)."""
+    ``two_launch`` runs the same call as the matcher and loss launches — the only form the product
+    library has (the one-launch form is a variant build, sbod_build_variants(); asking for it from
+    the product library raises instead of silently running two launches)."""
+    if not two_launch and not (L.lib().sbod_build_variants() & L.VARIANT_ONE_LAUNCH_CRITERION):
+        raise L.SbodError('the one-launch criterion is built into the variant library only '
+                          '(EXTRA=-DSBOD_VARIANT_ONE_LAUNCH scripts/build_lib_variant.sh); this library runs the '
+                          'matcher and the loss pass as two launches (criterion.one_launch = False)')
     locs = locs.contiguous()
     scores = scores.contiguous()
     if locs.dtype not in (torch.float32, torch.bfloat16) or scores.dtype != locs.dtype:
@@ -609,6 +615,10 @@ class DetectHandle:
         counts = self._cnt_host.tolist()
         if not self._persistent:
             _COUNT_SLOTS.setdefault(self._slot_key, []).append((self._cnt_host, self._event))
+        if L.DETECT_CORRUPT in counts:
+            raise L.SbodError('detect: a candidate key of image(s) %s decodes to a prior index >= P (corrupted '
+                              'or stale detect workspace; its zero-on-entry contract was broken)'
+                              % [i for i, n in enumerate(counts) if n == L.DETECT_CORRUPT])
         if min(counts) < 0:   # rare: some image needs a wider candidate window (exactness)
             # The retry reuses the launch's workspace (cached per launch stream), so it runs on
             # THAT stream: a later detect already queued there (pipelined graph replays share
@@ -733,8 +743,8 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
         sc = scores.contiguous().float()
         lc = locs if (locs.is_contiguous() and locs.dtype == torch.float32) else locs.contiguous().float()
         in_flags = 0
-    if DETECT_TWO_PASS if two_pass is None else two_pass:
-        in_flags |= L.DETECT_TWO_PASS
+    if not (DETECT_TWO_PASS if two_pass is None else two_pass):
+        in_flags |= L.DETECT_FUSED
     pri = priors_cxcy.contiguous().float() if priors_cxcy is not None else None
     pm = pos_mask.contiguous().to(torch.uint8) if pos_mask is not None else None
     out_b = torch.empty(B, top_k, 4, dtype=torch.float32, device=dev)

@@ -241,6 +241,14 @@ int sbod_timing_query(const char *kernel, int *launches, double *total_ms) {
 const char *sbod_version(void) { return "sbod-hip 0.1.0 (gfx950)"; }
 int sbod_abi_version(void) { return SBOD_ABI_VERSION; }
 
+int sbod_build_variants(void) {
+#ifdef SBOD_VARIANT_ONE_LAUNCH
+  return SBOD_VARIANT_ONE_LAUNCH_CRITERION;
+#else
+  return 0;
+#endif
+}
+
 int sbod_null_kernel(int blocks, void *stream) {
   SBOD_REQUIRE(blocks > 0, "sbod_null_kernel: blocks %d", blocks);
   sbod::KernelTimer kt("k_null", sbod::as_stream(stream), true);

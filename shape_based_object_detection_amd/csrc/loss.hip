@@ -25,6 +25,24 @@ namespace sbod {
 
 SBOD_STAMP_DECL
 
+// Diagnostic build only (-DSBOD_BLOCK_STAMPS, scripts/build_stamps_lib.sh): k_multibox's
+// workgroups record eight wall-clock marks each while its stamps are armed — 0 wave 0's score
+// tile committed, 1 the positive list's barrier passed, 2 wave 0's box regression done, 3..6
+// each wave's rows done, 7 the gradient tile stored and the block sums taken — read by
+// sbod_debug_mb_marks (scripts/mb_imbalance.py).  Compiles to nothing otherwise.
+#ifdef SBOD_BLOCK_STAMPS
+static __device__ unsigned long long g_mb_marks[SBOD_STAMP_REGION * 8];
+#define MB_MARK(slot, cond)                                                                   \
+  do {                                                                                        \
+    if ((g_stamp_armed & (1 << 4)) && (cond)) {                                               \
+      const unsigned _b = blockIdx.x + gridDim.x * blockIdx.y;                                \
+      if (_b < SBOD_STAMP_REGION) g_mb_marks[_b * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                         \
+  } while (0)
+#else
+#define MB_MARK(slot, cond) do { } while (0)
+#endif
+
 constexpr int kLTile = 256;
 constexpr float kHalfBetaDefault = 0.5f / 9.f;
 
@@ -425,14 +443,166 @@ __device__ __forceinline__ void fx_add(unsigned long long *w, Fx128 v) {
 __device__ __forceinline__ unsigned long long xchg0(unsigned long long *w) {
   return __hip_atomic_exchange(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Called by wave 0 of every workgroup (all 64 lanes; conf_l / loc_l uniform).  The partials
-// array holds each workgroup's fp32 {conf, loc} for the double fallback.
-// fxc / fxl (k_multibox_tiles): the exact sums of the workgroup's per-tile partials, already in
-// fixed point (fx_ok: every partial foldable); conf_l / loc_l are then only the fallback's values.
 __device__ __forceinline__ Fx128 fx128_add(Fx128 x, Fx128 y) {
   const unsigned long long lo = x.lo + y.lo;
   return Fx128{lo, x.hi + y.hi + (lo < x.lo ? 1ull : 0ull)};
 }
+// exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'
+// budget is 1e-4 relative; the all-classes underflow test (p == 0 -> NaN) stays exact (below).
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+// Two block-wide sums with one pair of barriers (blockDim.x a multiple of 64, <= 1024); results
+// valid in every thread.
+__device__ __forceinline__ void block_sum2(float &x, float &y, float *scratch /* >= 32 */) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    x += __shfl_xor(x, m, kWave);
+    y += __shfl_xor(y, m, kWave);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    scratch[w] = x;
+    scratch[16 + w] = y;
+  }
+  __syncthreads();
+  float sx = 0.f, sy = 0.f;
+  for (int i = 0; i < nw; ++i) {
+    sx += scratch[i];
+    sy += scratch[16 + i];
+  }
+  x = sx;
+  y = sy;
+}
+
+// The fused finish of k_multibox (focal criteria, no mining pass), in two parts so that the
+// workgroup's arrival travels while its gradient tile is stored:
+//   loss_arrive (wave 0, before the tile store): the workgroup's fp32 partials {conf, loc} are
+//     written through (one 8-byte sc1 store), drained, and the workgroup counts itself in at its
+//     group (32 group counters, blk mod 32: same-address atomics serialise at the memory side,
+//     ~10 ns each);
+//   loss_complete (wave 0, after waves 1-3 issued the tile store): the group's last arriver
+//     counts the group in at the top counter, and the top's last arriver reads every workgroup's
+//     partials (sc1 loads) and sums them EXACTLY: each fp32 partial as a 128-bit fixed-point
+//     integer (value * 2^64, two's complement), added lane by lane and across the wave — integer
+//     adds, so the total is the same in any order and bitwise reproducible, with a resolution of
+//     2^-64 per partial (a loss total of 1e-12 keeps 1e-7 relative).  A partial of magnitude
+//     >= 2^40 or a non-finite one cannot be folded exactly: then the double sum of the partials
+//     (lane-strided, xor tree) is the result, as k_loss_final computes it — never silently wrong
+//     (a NaN row of the focal loss, the reference's 0 * log 0, makes a NaN loss that way).
+// Counters are left zero by their last arrivers (SBOD_LOSS_WS_ZEROED).  Every hand-off moves
+// through memory-side atomics or sc1 stores / loads, so no cache write-back or invalidation is
+// needed between the XCDs.  (Round 4's form folded each partial into group accumulators by
+// returning atomics before the arrival and moved each group's total up a level: four dependent
+// far-memory round trips after the tile store, 3-4.8 us of the last workgroups' 18 us span,
+// scripts/mb_imbalance.py.)
+__device__ __forceinline__ unsigned long long loss_arrive(const LossArgs &a, float conf_l, float loc_l, unsigned nblk,
+                                                          unsigned blk) {
+  const unsigned ng = nblk < kFinGroups ? nblk : kFinGroups;
+  unsigned long long old = 0ull;
+  if ((threadIdx.x & 63) == 0) {
+    st_wt_u64(reinterpret_cast<unsigned long long *>(a.partials) + blk,
+              (static_cast<unsigned long long>(__float_as_uint(loc_l)) << 32) | __float_as_uint(conf_l));
+    drain_vm();   // the partials written through before the count
+    old = __hip_atomic_fetch_add(a.fin + kFinStride * (blk % ng) + kFinArrive, 1ull, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return old;
+}
+// Wave 0: the group's last arriver counts the group in at the top counter (leaving its group
+// counter zero).  Returns 1 (uniform) in the workgroup that completes the top: every workgroup's
+// partials are then written through and it runs loss_sum_all.
+__device__ int loss_climb(const LossArgs &a, unsigned long long ticket, unsigned nblk, unsigned blk) {
+  const int lane = threadIdx.x & 63;
+  const unsigned ng = nblk < kFinGroups ? nblk : kFinGroups, g = blk % ng;
+  const unsigned in_group = (nblk - g + ng - 1) / ng;
+  unsigned long long *top = a.fin + kFinStride * kFinGroups + kFinArrive;
+  int last = 0;
+  if (lane == 0 && ticket == in_group - 1) {   // the group is complete: count it in at the top
+    __hip_atomic_store(a.fin + kFinStride * g + kFinArrive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = __hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+    if (last) __hip_atomic_store(top, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return __builtin_amdgcn_readfirstlane(last);
+}
+// The whole workgroup (the top's last arriver): every workgroup's partials by 16-byte sc1 buffer
+// loads (two workgroups' partials each, four loads in flight per thread: one memory round trip up
+// to 2,048 workgroups; reads past the last partial return zero through the buffer's range check),
+// folded exactly per thread, across the wave and across the four waves; thread 0 writes the loss.
+__device__ void loss_sum_all(const LossArgs &a, unsigned nblk, float n, float *out, unsigned long long *s_fx) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.partials, static_cast<short>(0), static_cast<int>(nblk * 8u),
+                                                    0x00020000);
+  Fx128 fc{0ull, 0ull}, fl{0ull, 0ull};
+  bool ok = true;
+  constexpr int kB = 3;
+  const unsigned npair = (nblk + 1u) / 2u;
+  for (unsigned q0 = 0; q0 < npair; q0 += kB * kLTile) {
+    u32x4_t w[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k)
+      w[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>((q0 + k * kLTile + tid) * 16u), 0, kCpolSc1);
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float c = __uint_as_float(w[k][2 * h]), l = __uint_as_float(w[k][2 * h + 1]);
+        const bool f = fx_foldable(c) && fx_foldable(l);
+        ok = ok && f;
+        fc = fx128_add(fc, to_fx128(f ? c : 0.f));
+        fl = fx128_add(fl, to_fx128(f ? l : 0.f));
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    fc = fx128_add(fc, Fx128{shfl_xor_u64(fc.lo, m), shfl_xor_u64(fc.hi, m)});
+    fl = fx128_add(fl, Fx128{shfl_xor_u64(fl.lo, m), shfl_xor_u64(fl.hi, m)});
+  }
+  const bool wave_ok = __ballot(!ok) == 0ull;
+  if (lane == 0) {
+    s_fx[5 * wv + 0] = fc.lo;
+    s_fx[5 * wv + 1] = fc.hi;
+    s_fx[5 * wv + 2] = fl.lo;
+    s_fx[5 * wv + 3] = fl.hi;
+    s_fx[5 * wv + 4] = wave_ok ? 1ull : 0ull;
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  bool all_ok = true;
+  fc = Fx128{0ull, 0ull};
+  fl = Fx128{0ull, 0ull};
+  for (int w2 = 0; w2 < kLTile / 64; ++w2) {
+    fc = fx128_add(fc, Fx128{s_fx[5 * w2 + 0], s_fx[5 * w2 + 1]});
+    fl = fx128_add(fl, Fx128{s_fx[5 * w2 + 2], s_fx[5 * w2 + 3]});
+    all_ok = all_ok && s_fx[5 * w2 + 4] != 0ull;
+  }
+  double c = fx128_value(fc.lo, fc.hi), l = fx128_value(fl.lo, fl.hi);
+  if (!all_ok) {
+    // a non-finite or huge partial: the double sum of every workgroup's fp32 partials, as
+    // k_loss_final computes it (lane-strided, then the xor tree)
+    c = 0.0;
+    l = 0.0;
+    const unsigned long long *pp = reinterpret_cast<const unsigned long long *>(a.partials);
+    for (unsigned i = lane; i < nblk; i += 64) {
+      const unsigned long long w = ld_wt_u64(pp + i);
+      c += static_cast<double>(__uint_as_float(static_cast<uint32_t>(w)));
+      l += static_cast<double>(__uint_as_float(static_cast<uint32_t>(w >> 32)));
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      c += __shfl_xor(c, m, 64);
+      l += __shfl_xor(l, m, 64);
+    }
+  }
+  if (lane == 0) loss_outputs(c, l, n, a.reg, a.cls, a.flags, a.reg_weight, out);
+}
+
+#ifdef SBOD_VARIANT_ONE_LAUNCH
+// Called by wave 0 of every workgroup (all 64 lanes; conf_l / loc_l uniform).  The partials
+// array holds each workgroup's fp32 {conf, loc} for the double fallback.
+// fxc / fxl (k_multibox_tiles): the exact sums of the workgroup's per-tile partials, already in
+// fixed point (fx_ok: every partial foldable); conf_l / loc_l are then only the fallback's values.
 __device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, unsigned nblk, float n, float *out,
                                 const Fx128 *fxc = nullptr, const Fx128 *fxl = nullptr, bool fx_ok = true) {
   // accumulators: kFinGroups group lines, then the top line.  Two levels because atomics on one
@@ -504,17 +674,17 @@ __device__ void multibox_finish(const LossArgs &a, float conf_l, float loc_l, un
     loss_outputs(c, l, n, a.reg, a.cls, a.flags, a.reg_weight, out);
     if (a.done != nullptr) {   // one-launch criterion: every workgroup has passed its wait
       a.npos_out[a.B] = static_cast<int32_t>(n);
-      if (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      // the wait-timeout word is cleared here with `done` (zero on entry for the next call); its
+      // value moves to the sticky diagnostics word after it (sbod_criterion_status)
+      const unsigned st = __hip_atomic_exchange(a.status, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (st != 0u) {
         out[0] = out[1] = out[2] = __builtin_nanf("");
+        __hip_atomic_fetch_or(a.status + 1, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __hip_atomic_store(a.done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
-
-// exp on the hardware exp2 unit (~1-2 ulp + 2^-24 relative argument rounding): the losses'
-// budget is 1e-4 relative; the all-classes underflow test (p == 0 -> NaN) stays exact (below).
-__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
 // One-launch criterion: every workgroup waits until all images' forced matches are counted in
 // (their positives are the gradients' normaliser).  The grid is co-resident (the host checks it
@@ -522,26 +692,62 @@ __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp
 // a bound on it keeps a broken launch from hanging the device: past kSpinLimit ticks of the
 // 100 MHz real-time clock the workgroup sets *status and goes on (the loss becomes NaN).
 constexpr unsigned long long kSpinLimit = 2000000ull;   // 20 ms
-__device__ __forceinline__ unsigned wait_all_images(unsigned long long *done, int B, unsigned *status) {
+__device__ __forceinline__ unsigned wait_all_images(unsigned long long *done, int B, unsigned *status,
+                                                    int *timed_out) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  *timed_out = 0;
   for (;;) {
     const unsigned long long v = ld_wt_u64(done);
     if ((v >> 32) >= static_cast<unsigned long long>(B)) return static_cast<unsigned>(v);
     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit) {
       __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *timed_out = 1;
       return static_cast<unsigned>(v);
     }
     __builtin_amdgcn_s_sleep(1);
   }
 }
+#endif  // SBOD_VARIANT_ONE_LAUNCH
 
-// The tile's rows after their matcher outputs are known: the class decision, the positive
-// list, the box regression of the positives and the classification (loss + gradient row into the
-// LDS tile).  Shared by k_multibox (one tile per workgroup) and k_multibox_tiles (several).
-// Every thread of the workgroup calls it (one barrier inside); conf_l / loc_l accumulate.
-// before_cls() runs after the last global load of the rows and before the classification (LDS
-// and ALU only): k_multibox_tiles issues the next tile's loads there, so that no wait for this
-// tile's loads (the wait counter is in order) also waits for them.
+// The box-regression inputs of a row that can be positive (IoU >= threshold: every positive is,
+// the forced matches included, since the matcher wrote 1.0 for them): its loc, prior, matched GT
+// box and (RefineDet ODM) ARM loc, loaded together with the row's label — in the same memory
+// round trip as the score tile, instead of a second one after the class decision.  Every load is
+// unconditional (a conditional one makes the wait-count insertion at the join wait for the whole
+// batch); a row that cannot be positive loads a dummy line shared by the workgroup (its prior's
+// first row: L2-resident, one request per wave).
+struct RegIn {
+  Box4 l, pc, t, arm;
+};
+template <typename T, int CLS>
+__device__ __forceinline__ RegIn reg_prefetch(const LossArgs &a, const T *__restrict__ locs, int p0, int row,
+                                              int64_t i, int objv, int offb, bool cand) {
+  const float *dummy = a.priors + 4 * static_cast<int64_t>(p0);
+  RegIn r;
+  if constexpr (sizeof(T) == 4) {
+    r.l = ld4(cand ? reinterpret_cast<const float *>(locs) + 4 * i : dummy);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2 *>(cand ? reinterpret_cast<const void *>(locs + 4 * i)
+                                                          : reinterpret_cast<const void *>(dummy));
+    const float4 w = widen4(u);
+    r.l = Box4{w.x, w.y, w.z, w.w};
+  }
+  r.pc = ld4(cand ? a.priors + 4 * static_cast<int64_t>(p0 + row) : dummy);
+  r.t = ld4(cand ? a.gt + 4 * static_cast<int64_t>(offb + objv) : dummy);
+  if constexpr (CLS == SBOD_CLS_CE)   // RefineDet's ODM (CE criteria only): the ARM box the target is encoded on
+    r.arm = ld4(cand && (a.flags & SBOD_MATCH_ODM) ? a.arm_locs + 4 * i : dummy);
+  else
+    r.arm = Box4{0.f, 0.f, 0.f, 0.f};
+  return r;
+}
+
+// The tile's rows after their matcher outputs are known: the class decision, the box regression
+// of the positives and the classification (loss + gradient row into the LDS tile).  Shared by
+// k_multibox (one tile per workgroup) and the A/B variants.  Every thread of the workgroup calls
+// it (one barrier inside); conf_l / loc_l accumulate.  before_cls() runs after the last global
+// load of the rows and before the classification (LDS and ALU only): k_multibox_tiles issues the
+// next tile's loads there, so that no wait for this tile's loads (the wait counter is in order)
+// also waits for them.
 struct NoPrefetch {
   __device__ void operator()() const {}
 };
@@ -549,16 +755,14 @@ struct NoPrefetch {
 // with no padding slots to compute or guard — the same values as the CM-slot form (a padding
 // slot only ever adds exp(-inf) = 0 or an ignored value).
 template <typename T, int CM, int CLS, int CE = 0, typename Pf = NoPrefetch>
-__device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__restrict__ locs, T *__restrict__ glocs,
-                                              T *__restrict__ gsc, int p0, int64_t rbase, bool valid, int64_t ic,
-                                              int objv, float v, int64_t labg, int offb, float n, float *s_sc,
-                                              int2 *s_plist, int *s_wcnt, float &conf_l, float &loc_l,
+__device__ __forceinline__ void multibox_rows(const LossArgs &a, T *__restrict__ glocs, T *__restrict__ gsc,
+                                              bool valid, int64_t ic, float v, int64_t labg, const RegIn &rg,
+                                              float n, float *s_sc, float &conf_l, float &loc_l,
                                               Pf before_cls = Pf()) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x;
   const int C = a.C;
   const bool odm = (a.flags & SBOD_MATCH_ODM) != 0;
   const bool grad = gsc != nullptr;
-  // The row's class decision before the barrier, so the tile's positive rows can be listed.
   int c = 0;
   bool negrow = false, easy = false, pos = false;
   if (valid) {
@@ -573,36 +777,15 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
     }
     pos = c > 0 && !easy;
   }
-  {   // each wave lists its positive rows (tile row, object) in its own 64 slots
-    const unsigned long long bal = __ballot(pos);
-    if (pos) s_plist[64 * wv + __popcll(bal & ((1ull << lane) - 1ull))] = make_int2(tid, objv);
-    if (lane == 0) s_wcnt[wv] = __popcll(bal);
-  }
-  __syncthreads();
-  // ---------------- box regression, compacted: positives are ~1-3 % of the rows, yet with one
-  // per wave the whole wave would run the DIoU / encode path (a dozen IEEE divisions, exps).
-  // The tile's positives are packed 64 per chunk and chunk k runs on wave k % 4 (usually one
-  // chunk): it re-reads its rows' loc / prior / GT box (L2 hits) and writes their gradient
-  // rows; every other row's gradient row is the zero written below by its own thread.
-  {
-    const int n0 = s_wcnt[0], n1 = s_wcnt[1], n2 = s_wcnt[2], n3 = s_wcnt[3];
-    const int total = n0 + n1 + n2 + n3;
-    for (int e0 = 64 * wv; e0 < total; e0 += kLTile) {
-      const int e = e0 + lane;
-      if (e >= total) break;
-      // entry e of the concatenation of the four waves' lists
-      const int ww = e < n0 ? 0 : (e < n0 + n1 ? 1 : (e < n0 + n1 + n2 ? 2 : 3));
-      const int r0 = e - (ww == 0 ? 0 : (ww == 1 ? n0 : (ww == 2 ? n0 + n1 : n0 + n1 + n2)));
-      const int2 pe = s_plist[64 * ww + r0];
-      const int64_t i = rbase + pe.x;
-      Box4 l;
-      if constexpr (sizeof(T) == 4)
-        l = ld4(reinterpret_cast<const float *>(locs) + 4 * i);
-      else
-        l = Box4{ldf(locs + 4 * i), ldf(locs + 4 * i + 1), ldf(locs + 4 * i + 2), ldf(locs + 4 * i + 3)};
-      const Box4 pc = ld4(a.priors + 4 * static_cast<int64_t>(p0 + pe.x));
-      const Box4 t = ld4(a.gt + 4 * static_cast<int64_t>(offb + pe.y));
-      float gl[4] = {0.f, 0.f, 0.f, 0.f};
+  // ---------------- box regression of the positive rows (~1-3 % of them) on the lanes that hold
+  // them, from the registers reg_prefetch filled with the tile's loads; a wave without a positive
+  // row skips the DIoU / encode path (a dozen IEEE divisions, exps) as a whole.  (Packing the
+  // tile's positives onto one wave re-read their rows after a barrier: a second memory round trip,
+  // +2 us on the ~20 % of workgroups with a positive, scripts/mb_imbalance.py.)
+  float gl[4] = {0.f, 0.f, 0.f, 0.f};
+  if (__ballot(pos)) {
+    if (pos) {
+      const Box4 l = rg.l, pc = rg.pc, t = rg.t;
       if (a.reg == SBOD_REG_DIOU) {  // SSD512.py:579-581: IouLoss(Diou) on decoded boxes
         const Box4 d = decode_tenfive_xy(l, pc);
         const OvOut r = aligned_overlap(SBOD_OV_DIOU, d, t, grad);
@@ -613,7 +796,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
           decode_backward(gb, l, pc, gl);
         }
       } else {  // smooth-L1 (Loss.py:213-217) or L1 on encoded targets
-        const Box4 pr = odm ? xy_to_cxcy(decode_tenfive_xy(ld4(a.arm_locs + 4 * i), pc)) : pc;
+        const Box4 pr = odm ? xy_to_cxcy(decode_tenfive_xy(rg.arm, pc)) : pc;
         const Box4 en = encode_tenfive(xy_to_cxcy(t), pr);
         const float lv[4] = {l.a, l.b, l.c, l.d}, ev[4] = {en.a, en.b, en.c, en.d};
         const bool l1 = a.reg == SBOD_REG_L1;
@@ -636,25 +819,20 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
           }
         }
       }
-      if (glocs) {
-        if constexpr (sizeof(T) == 4) {
-          st4_nt(reinterpret_cast<float *>(glocs) + 4 * i, Box4{gl[0], gl[1], gl[2], gl[3]});
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
-        }
-      }
     }
   }
+  MB_MARK(2, tid == 0);
+  __syncthreads();   // the score tile is in LDS (every thread committed its part)
+  MB_MARK(1, tid == 0);
   before_cls();
   if (valid) {
     const int64_t i = ic;
-    if (glocs && !pos) {
+    if (glocs) {   // the row's box gradient (zero unless positive)
       if constexpr (sizeof(T) == 4) {
-        st4_nt(reinterpret_cast<float *>(glocs) + 4 * i, Box4{0.f, 0.f, 0.f, 0.f});
+        st4_nt(reinterpret_cast<float *>(glocs) + 4 * i, Box4{gl[0], gl[1], gl[2], gl[3]});
       } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, 0.f);
+        for (int k = 0; k < 4; ++k) stf(glocs + 4 * i + k, gl[k]);
       }
     }
     // ---------------- classification
@@ -829,6 +1007,7 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, const T *__rest
       }
     }
   }
+  MB_MARK(3 + (tid >> 6), (tid & 63) == 0);
 }
 
 // CM > 0: class rows of C <= CM in registers (padding slots -inf: no per-slot guards in the
@@ -844,22 +1023,19 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
                                                      const T *__restrict__ scores,
                                                      T *__restrict__ glocs, T *__restrict__ gsc) {
   extern __shared__ __attribute__((aligned(16))) float s_sc[];
-  __shared__ float s_red[16];
-  __shared__ int2 s_plist[kLTile];        // positive rows: wave w's at [64 w, 64 w + count)
+  __shared__ float s_red[32];
+#ifdef SBOD_VARIANT_ONE_LAUNCH
   __shared__ int s_wcnt[kLTile / 64];
   __shared__ int s_misc[16];
+#endif
   STAMP_BEGIN();
   span_begin(a.span);
   PHASE_DECL;
   SEG_PHASE(0);
-  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x;
   const int P = a.P, C = a.C;
   const int np = min(kLTile, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
-  // memory schedule: the row's matcher outputs first, then the score tile, then the loads
-  // that depend on the matcher outputs (label, GT box, and the loc / prior of rows that can
-  // be positive) — all in flight together; the tile is committed to LDS last
-  // (a tile that does not qualify for the register path is staged first, with nothing live)
   const bool valid = tid < np;
   const int64_t ic = rbase + (valid ? tid : 0);
   constexpr int NB = CM / 4;
@@ -868,8 +1044,11 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   int objv, offb;
   float v, n;
   int64_t labg;
+  RegIn rg;
   typename TileVec<T>::V tr[NB > 0 ? NB : 1];
   if constexpr (kFused) {
+#ifdef SBOD_VARIANT_ONE_LAUNCH
+    const int lane = tid & 63, wv = tid >> 6;
     offb = a.off[b];
     // ---- phase 1: this tile's match (the dynamic LDS holds the waves' key rows until the
     // score tile is loaded)
@@ -916,7 +1095,7 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     if constexpr (NB > 0)
       if (fast) tile_commit(s_sc, tr, np * C);
     // ---- every image counted in: the batch's positives, then this tile's forced rewrites
-    if (tid == 0) s_misc[14] = static_cast<int>(wait_all_images(a.done, a.B, a.status));
+    if (tid == 0) s_misc[14] = static_cast<int>(wait_all_images(a.done, a.B, a.status, &s_misc[13]));
     __syncthreads();
     n = static_cast<float>(s_misc[14]);
     objv = m.bi;
@@ -930,148 +1109,101 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
       }
     }
     labg = a.labels[offb + objv];
+    rg = reg_prefetch<T, CLS>(a, locs, p0, tid, ic, objv, offb, valid && v >= a.thr);
+#else
+    return;   // the one-launch criterion is built into the variant library only
+#endif
   } else {
-    // memory schedule: the row's matcher outputs first, then the score tile, then the label
-    // that depends on the matcher outputs — all in flight together;
-    // the tile is committed to LDS last (a tile that does not qualify for the register path is
-    // staged first, with nothing live)
+    // memory schedule: the row's matcher outputs first, then the score tile, then the loads that
+    // depend on the matcher outputs (the label; the loc, prior and GT box of a row that can be
+    // positive) — all in flight together; the tile is committed to LDS last (a tile that does
+    // not qualify for the register path is staged first, with nothing live)
     if (!fast) tile_load(s_sc, tsrc, np * C);
     objv = a.obj[ic];
     v = a.ovl[ic];
     offb = a.off[b];
-    // every load below is unconditional (a tile that is not staged through registers loads an
-    // aligned dummy vector instead): a conditional load makes the wait-count insertion at
-    // the join assume the short path and wait for the whole batch
-    if constexpr (NB > 0)   // (the workspace's partials: 256-byte aligned, whatever `scores` is)
+    if constexpr (NB > 0 && sizeof(T) == 4) {
+      // fp32 tile by LDS-DMA: each wave-instruction copies 64 x 16 B straight into LDS (lane-
+      // linear: the same layout tile_commit writes), so the tile holds no VGPRs while the row's
+      // dependent loads below are in flight with it
+      if (fast) {
+        const float4 *src4 = reinterpret_cast<const float4 *>(tsrc);
+        const int n4 = (np * C) >> 2, q = 64 * (tid >> 6), lane = tid & 63;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int q0 = k * kLTile + q;   // the wave's first 16-byte chunk of this round (uniform)
+          if (q0 + lane < n4)
+            __builtin_amdgcn_global_load_lds(src4 + q0 + lane,
+                                             (__attribute__((address_space(3))) void *)(reinterpret_cast<float4 *>(s_sc) + q0),
+                                             16, 0, 0);
+        }
+      }
+    } else if constexpr (NB > 0) {   // bf16: widened in registers (the workspace's partials, 256-byte
+      // aligned, are the dummy source of a tile that does not qualify: every load unconditional —
+      // a conditional load makes the wait-count insertion at the join wait for the whole batch)
       tile_issue<T, NB>(tr, fast ? tsrc : reinterpret_cast<const T *>(a.partials), fast ? np * C : 4);
+    }
     __builtin_amdgcn_sched_barrier(0);   // keep the tile's loads ahead of the dependent chain
     labg = a.labels[offb + objv];
-    if constexpr (NB > 0)
+    rg = reg_prefetch<T, CLS>(a, locs, p0, tid, ic, objv, offb, valid && v >= a.thr);
+    if constexpr (NB > 0 && sizeof(T) != 4)
       if (fast) tile_commit(s_sc, tr, np * C);
     n = static_cast<float>(*a.npos_total);
+    MB_MARK(0, tid == 0);
   }
   SEG_PHASE(1);
   const bool grad = gsc != nullptr;
   float conf_l = 0.f, loc_l = 0.f;
-  multibox_rows<T, CM, CLS, CE>(a, locs, glocs, gsc, p0, rbase, valid, ic, objv, v, labg, offb, n, s_sc, s_plist,
-                                s_wcnt, conf_l, loc_l);
-  __syncthreads();
-  SEG_PHASE(2);
-  // the gradient tile: with SBOD_MB_W0_NOSTORE wave 0 (which runs the finish and its drain) stores
-  // none of it, so its drain waits for its own atomics only
-#ifdef SBOD_MB_W0_NOSTORE
-  if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 64, kLTile - 64);
-#else
-  if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
-#endif
-  conf_l = block_sum(conf_l, s_red);
-  loc_l = block_sum(loc_l, s_red + 8);
-  SEG_PHASE(3);
-  if (a.fin != nullptr) {
-    if (tid < 64) multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, n, a.out);
-  } else if (tid == 0) {
-    const int64_t blk = static_cast<int64_t>(b) * gridDim.x + blockIdx.x;
-    a.partials[2 * blk] = conf_l;
-    a.partials[2 * blk + 1] = loc_l;
+  multibox_rows<T, CM, CLS, CE>(a, glocs, gsc, valid, ic, v, labg, rg, n, s_sc, conf_l, loc_l);
+  __syncthreads();   // every gradient row is in the LDS tile
+#ifdef SBOD_VARIANT_ONE_LAUNCH
+  if constexpr (kFused) {
+    if (s_misc[13]) {   // this workgroup's wait gave up: its normaliser and forced rows are not
+      // final, so its gradients are poisoned (NaN) rather than plausible-looking and wrong
+      for (int e = tid; e < np * C; e += kLTile) s_sc[e] = __builtin_nanf("");
+      if (glocs && valid)
+        for (int k = 0; k < 4; ++k) stf(glocs + 4 * ic + k, __builtin_nanf(""));
+      __syncthreads();
+    }
   }
+#endif
+  SEG_PHASE(2);
+  const unsigned nblk = gridDim.x * gridDim.y, blk = blockIdx.x + gridDim.x * blockIdx.y;
+  if (a.fin != nullptr && !kFused) {
+    // the fused finish (focal): the block sums first, so wave 0's arrival is in flight while
+    // waves 1-3 store the gradient tile
+    block_sum2(conf_l, loc_l, s_red);
+    unsigned long long ticket = 0;
+    if (tid < 64) ticket = loss_arrive(a, conf_l, loc_l, nblk, blk);
+    if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 64, kLTile - 64);
+    MB_MARK(7, tid == 0);
+    __shared__ int s_last;
+    if (tid < 64) {
+      const int last = loss_climb(a, ticket, nblk, blk);
+      if (tid == 0) s_last = last;
+    }
+    __syncthreads();
+    if (s_last) loss_sum_all(a, nblk, n, a.out, reinterpret_cast<unsigned long long *>(s_sc));
+  } else {
+    if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
+    block_sum2(conf_l, loc_l, s_red);
+    MB_MARK(7, tid == 0);
+    if (a.fin != nullptr) {
+#ifdef SBOD_VARIANT_ONE_LAUNCH
+      if (tid < 64) multibox_finish(a, conf_l, loc_l, nblk, n, a.out);
+#endif
+    } else if (tid == 0) {
+      a.partials[2 * blk] = conf_l;
+      a.partials[2 * blk + 1] = loc_l;
+    }
+  }
+  SEG_PHASE(3);
 #ifdef SBOD_PHASE_CLOCKS
   if (tid == 0) ph[4] = __builtin_amdgcn_s_memrealtime();
   if (PHASE_PRINT_SEL)
     printf("PH multibox x%d b%d start %lld load %lld compute %lld store+sum %lld finish %lld\n", blockIdx.x, b,
            ph[0], ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3]);
 #endif
-  span_end(a.span);
-  STAMP_END(4, 1);
-}
-
-// The focal loss pass with several tiles per workgroup (tiles blockIdx.x * tpw .. + tpw of image
-// blockIdx.y), software-pipelined: as soon as tile t is committed to LDS, the registers that
-// carried it take tile t+1's scores (and its rows' matcher outputs), so t+1's loads are in flight
-// while t is computed and stored.  One tile per workgroup (k_multibox) puts every workgroup of
-// the launch in the same phase at once — all loading (HBM busy, ALUs idle), then all computing
-// (the reverse) — which is what bounds it at a large batch.  Register-path rows (CM > 0) and the
-// in-kernel finish only (focal, C <= 24: wider rows would spill); results are identical to k_multibox's (same per-row code, and
-// the finish's exact fixed-point sums do not depend on how rows are grouped into workgroups).
-template <typename T, int CM>
-__global__ __launch_bounds__(kLTile, 3) void k_multibox_tiles(LossArgs a, const T *__restrict__ locs,
-                                                              const T *__restrict__ scores, T *__restrict__ glocs,
-                                                              T *__restrict__ gsc, int tpw) {
-  static_assert(CM > 0, "k_multibox_tiles: register-path rows only");
-  extern __shared__ __attribute__((aligned(16))) float s_sc[];
-  __shared__ float s_red[16];
-  __shared__ int2 s_plist[kLTile];
-  __shared__ int s_wcnt[kLTile / 64];
-  STAMP_BEGIN();
-  span_begin(a.span);
-  constexpr int NB = CM / 4;
-  const int b = blockIdx.y, tid = threadIdx.x;
-  const int P = a.P, C = a.C;
-  const int ntx = (P + kLTile - 1) / kLTile;
-  const int x0 = blockIdx.x * tpw, x1 = min(x0 + tpw, ntx);
-  const int offb = a.off[b];
-  const float n = static_cast<float>(*a.npos_total);
-  const bool grad = gsc != nullptr;
-  const T *dummy = reinterpret_cast<const T *>(a.partials);   // 256-byte aligned workspace
-  float conf_l = 0.f, loc_l = 0.f;   // the workgroup's fp32 sums (the finish's fallback only)
-  Fx128 fxc{0ull, 0ull}, fxl{0ull, 0ull};   // exact sums of the per-tile partials
-  bool fx_ok = true;
-  typename TileVec<T>::V tr[NB];
-  // tile x0's loads (every load unconditional: a tile that does not qualify for the register path
-  // loads the aligned dummy, and is staged through LDS when its turn comes)
-  int p0 = x0 * kLTile;
-  int np = min(kLTile, P - p0);
-  int64_t rbase = static_cast<int64_t>(b) * P + p0;
-  bool fast = fast_tile<T, NB>(scores + rbase * C, np * C);
-  int64_t ic = rbase + (tid < np ? tid : 0);
-  int objv = a.obj[ic];
-  float v = a.ovl[ic];
-  tile_issue<T, NB>(tr, fast ? scores + rbase * C : dummy, fast ? np * C : 4);
-  for (int x = x0; x < x1; ++x) {
-    const bool valid = tid < np;
-    if (!fast) tile_load(s_sc, scores + rbase * C, np * C);
-    __builtin_amdgcn_sched_barrier(0);
-    const int64_t labg = a.labels[offb + objv];
-    if (fast) tile_commit(s_sc, tr, np * C);
-    // the next tile's loads into the registers just freed (the last tile loads the dummy), issued
-    // by multibox_rows after this tile's own loads
-    const bool more = x + 1 < x1;
-    const int p0n = more ? p0 + kLTile : p0;
-    const int npn = min(kLTile, P - p0n);
-    const int64_t rbn = static_cast<int64_t>(b) * P + p0n;
-    const bool fastn = more && fast_tile<T, NB>(scores + rbn * C, npn * C);
-    const int64_t icn = rbn + (tid < npn ? tid : 0);
-    int objn;
-    float vn;
-    float ct = 0.f, lt = 0.f;
-    multibox_rows<T, CM, SBOD_CLS_FOCAL>(a, locs, glocs, gsc, p0, rbase, valid, ic, objv, v, labg, offb, n, s_sc,
-                                         s_plist, s_wcnt, ct, lt, [&]() {
-                                           objn = a.obj[icn];
-                                           vn = a.ovl[icn];
-                                           tile_issue<T, NB>(tr, fastn ? scores + rbn * C : dummy, fastn ? npn * C : 4);
-                                         });
-    __syncthreads();
-    if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
-    // the tile's partials exactly as k_multibox's workgroup would report them, summed in fixed
-    // point (exact: the loss equals the one-tile kernel's bit for bit)
-    ct = block_sum(ct, s_red);
-    lt = block_sum(lt, s_red + 8);
-    fx_ok = fx_ok && fx_foldable(ct) && fx_foldable(lt);
-    if (fx_ok) {
-      fxc = fx128_add(fxc, to_fx128(ct));
-      fxl = fx128_add(fxl, to_fx128(lt));
-    }
-    conf_l += ct;
-    loc_l += lt;
-    __syncthreads();   // the tile's LDS rows are read out before the next tile is committed
-    p0 = p0n;
-    np = npn;
-    rbase = rbn;
-    fast = fastn;
-    ic = icn;
-    objv = objn;
-    v = vn;
-  }
-  if (tid < 64) multibox_finish(a, conf_l, loc_l, gridDim.x * gridDim.y, n, a.out, &fxc, &fxl, fx_ok);
   span_end(a.span);
   STAMP_END(4, 1);
 }
@@ -1427,6 +1559,7 @@ CritWs carve_crit(void *w, int B, int Gmax, int P) {
   return r;
 }
 
+#ifdef SBOD_VARIANT_ONE_LAUNCH
 // Workgroups of `kernel` (kLTile threads, `lds` dynamic bytes) resident at once on the current
 // device: the occupancy query times the CU count, cached per (device, kernel, lds).  The
 // one-launch criterion needs its whole grid resident (its workgroups wait for each other).  The
@@ -1454,20 +1587,7 @@ int resident_capacity(const void *kernel, size_t lds) {
   cache.push_back(Entry{dev, kernel, lds, per_cu * cus});
   return per_cu * cus;
 }
-// Tiles per workgroup of the focal loss pass: SBOD_MB_TILES (A/B), else 1 (k_multibox).  Measured
-// (scripts/gpu_tiles_ab.sh, SSD512 B=32 f32): 2 tiles per workgroup 24.7 us vs 20.3 us, the step
-// 0.0368 vs 0.0352 ms — the pass is VALU-issue-bound in its compute phase, and the prefetch
-// registers (152 VGPRs: 3 workgroups per CU instead of 6) cost more latency hiding than the
-// overlap of one tile's loads with the previous tile's compute gains.
-std::atomic<int> g_mb_tiles{[] {   // SBOD_MB_TILES read once; sbod_set_multibox_tiles() after
-  const char *e = std::getenv("SBOD_MB_TILES");
-  const int v = e ? std::atoi(e) : 1;
-  return v < 1 ? 1 : (v > 16 ? 16 : v);
-}()};
-int multibox_tiles_per_wg(int tiles) {
-  (void)tiles;
-  return g_mb_tiles.load(std::memory_order_relaxed);
-}
+#endif  // SBOD_VARIANT_ONE_LAUNCH
 }  // namespace
 
 extern "C" {
@@ -1509,6 +1629,7 @@ int sbod_criterion_focal(const void *locs, const void *scores, int dtype, int B,
   const int lflags = flags & (SBOD_LOSS_FOCAL_NORM | SBOD_LOSS_UNFUSED_FINISH);
   const dim3 grid((P + kLTile - 1) / kLTile, B);
   const size_t nblk = static_cast<size_t>(grid.x) * B;
+#ifdef SBOD_VARIANT_ONE_LAUNCH
   // the tile's rows (+ 8 floats, as k_multibox), the match phase's key rows, and the forced
   // match's LDS form beyond 64 objects: one dynamic region, used in turn
   size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
@@ -1531,6 +1652,13 @@ int sbod_criterion_focal(const void *locs, const void *scores, int dtype, int B,
 #undef SBOD_CRIT_K
   const bool one = (flags & (SBOD_CRIT_TWO_LAUNCH | SBOD_LOSS_UNFUSED_FINISH)) == 0 &&
                    nblk <= static_cast<size_t>(resident_capacity(kfused, lds));
+#else
+  // the one-launch form (k_multibox<..., true>: workgroups that wait for each other) is built into
+  // the variant library only (scripts/build_variant_lib.sh); the product library always runs the
+  // matcher and the loss pass as separate launches
+  (void)nblk;
+  const bool one = false;
+#endif
   if (!one) {   // the two-launch form on the same workspace (both parts are zero on entry)
     const int st = sbod_match_f32(gt_boxes, gt_labels, gt_offsets, B, Gmax, priors_xy, nullptr, nullptr, P, threshold,
                                   0.01f, SBOD_MATCH_WS_ZEROED, obj, ovl, n_pos, ws.match_ws, ws.match_bytes, stream);
@@ -1540,6 +1668,7 @@ int sbod_criterion_focal(const void *locs, const void *scores, int dtype, int B,
                               SBOD_CLS_FOCAL, lflags | SBOD_LOSS_WS_ZEROED, 3, reg_weight, focal_alpha, focal_gamma,
                               grad_locs, grad_scores, loss_out, ws.loss_ws, ws.loss_bytes, stream);
   }
+#ifdef SBOD_VARIANT_ONE_LAUNCH
   const LossWs lw = carve(ws.loss_ws, B, P);
   LossArgs a{B, P, C, priors_cxcy, nullptr, nullptr, gt_boxes, gt_labels, gt_offsets, nullptr, nullptr, nullptr,
              threshold, neg_threshold, 0.01f, reg, SBOD_CLS_FOCAL, lflags, reg_weight, focal_alpha,
@@ -1577,6 +1706,9 @@ int sbod_criterion_focal(const void *locs, const void *scores, int dtype, int B,
   }
   SBOD_LAUNCHED("k_criterion");
   return SBOD_OK;
+#else
+  return SBOD_OK;
+#endif
 }
 
 int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *label_ptrs, const int32_t *counts,
@@ -1615,12 +1747,13 @@ int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *l
 }
 
 int sbod_criterion_status(const void *workspace, void *stream) {
-  // diagnostics: the one-launch criterion's wait-timeout word (nonzero: a wait gave up), read
-  // with a stream synchronisation
+  // diagnostics: the one-launch criterion's sticky wait-timeout word (nonzero: a wait gave up in
+  // some call on this workspace; the per-call word is cleared by each call's finish), read with a
+  // stream synchronisation
   SBOD_REQUIRE(workspace != nullptr, "sbod_criterion_status: null workspace");
   unsigned v = 0;
   hipStream_t s = as_stream(stream);
-  if (hipMemcpyAsync(&v, static_cast<const char *>(workspace) + 8, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+  if (hipMemcpyAsync(&v, static_cast<const char *>(workspace) + 12, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return launch_status("sbod_criterion_status");
   return static_cast<int>(v);
@@ -1666,27 +1799,6 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
   dim3 grid((P + kLTile - 1) / kLTile, B);
   // + 8 floats: the register path's constant-offset row reads may run up to 7 past the last row
   const size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
-  const int tpw = fused && C <= 24 ? multibox_tiles_per_wg(static_cast<int>(grid.x) * B) : 1;
-  if (tpw > 1) {   // several tiles per workgroup, pipelined (k_multibox_tiles)
-    const dim3 g2((grid.x + tpw - 1) / tpw, B);
-    KernelTimer kt("k_multibox", s, true);
-    a.span = kt.span();
-#define SBOD_MBT(T, CM)                                                                                      \
-  tlaunch(kt, (k_multibox_tiles<T, CM>), g2, dim3(kLTile), lds, s, a, static_cast<const T *>(locs),            \
-          static_cast<const T *>(scores), static_cast<T *>(grad_locs), static_cast<T *>(grad_scores), tpw)
-#define SBOD_MBT_C(T)                  \
-  do {                                 \
-    if (C <= 8) SBOD_MBT(T, 8);        \
-    else if (C <= 16) SBOD_MBT(T, 16); \
-    else SBOD_MBT(T, 24);              \
-  } while (0)
-    if (dtype == SBOD_DT_F32) SBOD_MBT_C(float);
-    else SBOD_MBT_C(uint16_t);
-#undef SBOD_MBT_C
-#undef SBOD_MBT
-    SBOD_LAUNCHED("k_multibox_tiles");
-    return SBOD_OK;
-  }
   {
     KernelTimer kt("k_multibox", s, true);
     a.span = kt.span();
@@ -1731,12 +1843,6 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
 }
 
 size_t sbod_loss_zero_prefix_bytes(void) { return kFinBytes; }
-
-int sbod_set_multibox_tiles(int n) {
-  const int prev = g_mb_tiles.load();
-  if (n >= 1) g_mb_tiles.store(n > 16 ? 16 : n);
-  return prev;
-}
 
 size_t sbod_loss_pool_offset(int B, int P) {
   return carve(nullptr, B, P).pool_off;
@@ -1803,3 +1909,17 @@ int sbod_focal_f32(int kind, const float *logits, const int64_t *target, int64_t
 }  // extern "C"
 
 SBOD_STAMP_EXPORT(loss)
+
+#ifdef SBOD_BLOCK_STAMPS
+// k_multibox's per-workgroup marks (diagnostic build): copies the first n workgroups' 8 marks out,
+// then clears them.
+extern "C" int sbod_debug_mb_marks(unsigned long long *host, int n) {
+  const int cap = static_cast<int>(SBOD_STAMP_REGION);
+  if (host && n > 0)
+    hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mb_marks), sizeof(unsigned long long) * 8 * (n < cap ? n : cap));
+  void *sym = nullptr;
+  if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_mb_marks)) == hipSuccess)
+    hipMemset(sym, 0, sizeof(unsigned long long) * 8 * cap);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+#endif

@@ -721,6 +721,17 @@ struct SegOut {
 };
 
 constexpr int kSegSortCap = 2048;  // segments up to this size are selected in LDS
+// A candidate key's prior index is dereferenced (its decoded box) only when < P: a corrupted or
+// stale candidate region (a caller's workspace contract broken) must never read out of bounds.
+// The segment then reports kKcCorrupt as its kept count, and the image's merge reports
+// det_count SBOD_DETECT_CORRUPT (-2) instead of detections.
+constexpr uint32_t kKcCorrupt = 0xffffffffu;
+constexpr int32_t kDetCorrupt = SBOD_DETECT_CORRUPT;
+__device__ __forceinline__ uint32_t key_prior(unsigned long long k, int P, bool &bad) {
+  const uint32_t p = key_low(k);
+  bad = p >= static_cast<uint32_t>(P);
+  return bad ? 0u : p;
+}
 
 
 // Block-level segment work for (image b, class c): top-`window` candidates by key, greedy NMS,
@@ -785,13 +796,23 @@ __device__ void segment_body(const unsigned long long *cand, const uint32_t *can
     __syncthreads();
     bitonic_desc(sk, N);
   }
+  int bad_any = 0;
   for (int i = threadIdx.x; i < q; i += blockDim.x) {
-    const uint32_t p = key_low(sk[i]);
+    bool bad;
+    const uint32_t p = key_prior(sk[i], P, bad);
+    bad_any |= bad;
     const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
     sb[i] = bx;
     sa[i] = (bx.c - bx.a) * (bx.d - bx.b);
   }
-  __syncthreads();
+  if (__syncthreads_or(bad_any)) {
+    if (threadIdx.x == 0) {
+      o.kc[seg] = kKcCorrupt;
+      o.lastkey[seg] = 0;
+    }
+    __syncthreads();
+    return;
+  }
   const int nk = q <= kMatrixMax
                      ? block_greedy_matrix<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, mat, &s_nk)
                      : block_greedy<SBOD_NMS_TV>(sb, sa, q, thr, 1.f, kf, kl, s_flag, s_m, &s_nk);
@@ -907,15 +928,23 @@ __global__ __launch_bounds__(kAllThreads) void k_det_segment_all(
     __syncthreads();
     bitonic_desc(s_key, kAllChunk);
     // load the chunk's boxes; test each against every box kept so far
-    bool alive = false;
+    bool alive = false, bad = false;
     if (tid < q) {
-      const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(s_key[tid])));
+      const uint32_t p = key_prior(s_key[tid], P, bad);
+      const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
       const float ar = (bx.c - bx.a) * (bx.d - bx.b);
       alive = true;
       for (int i = 0; i < kept && alive; ++i)
         if (suppresses<SBOD_NMS_TV>(kbox[i], karea[i], bx, ar, thr, 1.f)) alive = false;
       s_box[tid] = bx;
       s_area[tid] = ar;
+    }
+    if (__syncthreads_or(bad)) {
+      if (tid == 0) {
+        o.kc[seg] = kKcCorrupt;
+        o.lastkey[seg] = 0ull;
+      }
+      return;
     }
     // order-preserving compaction of the survivors
     const unsigned long long bal = __ballot(alive);
@@ -1103,7 +1132,12 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
   // latency overlaps it) and each key carries its original lane to find its box afterwards
   unsigned long long v = lane < q ? s_sel[lane] : 0ull;
   Box4 bu{0.f, 0.f, 0.f, 0.f};
-  if (lane < q) bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(v)));
+  bool bad = false;
+  if (lane < q) {
+    const uint32_t p = key_prior(v, P, bad);
+    bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
+  }
+  const bool corrupt = __ballot(bad) != 0ull;
   int pos = lane;
 #pragma unroll
   for (int k = 2; k <= 64; k <<= 1) {
@@ -1165,8 +1199,8 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
   const uint32_t llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), q - 1);
   const uint32_t lhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), q - 1);
   if (lane == 0) {
-    o.kc[seg] = __popcll(kept);
-    o.lastkey[seg] = n > q ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
+    o.kc[seg] = corrupt ? kKcCorrupt : static_cast<uint32_t>(__popcll(kept));
+    o.lastkey[seg] = n > q && !corrupt ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
   }
   SEG_PHASE(4);
 #ifdef SBOD_PHASE_CLOCKS
@@ -1364,10 +1398,16 @@ __device__ __forceinline__ void segment_w(
   // ---- wave 0: sort descending over lanes; boxes fetched before the sort (latency overlap),
   // each key carries its original lane to find its box afterwards
   unsigned long long v = 0ull;
+  bool corrupt = false;
   if (wv == 0) {
     v = lane < q ? s_sel[lane] : 0ull;
     Box4 bu{0.f, 0.f, 0.f, 0.f};
-    if (lane < q) bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(v)));
+    bool bad = false;
+    if (lane < q) {
+      const uint32_t p = key_prior(v, P, bad);
+      bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
+    }
+    corrupt = __ballot(bad) != 0ull;
     int pos = lane;
 #pragma unroll
     for (int k = 2; k <= 64; k <<= 1) {
@@ -1450,17 +1490,18 @@ __device__ __forceinline__ void segment_w(
   unsigned long long *ko = o.kept + seg * stride;
   const uint32_t llo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), q - 1);
   const uint32_t lhi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), q - 1);
-  const unsigned long long lk = n > q ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
+  const unsigned long long lk = n > q && !corrupt ? ((static_cast<unsigned long long>(lhi) << 32) | llo) : 0ull;
+  const uint32_t kcv = corrupt ? kKcCorrupt : static_cast<uint32_t>(__popcll(kept));
   if constexpr (kWT) {
     if ((kept >> lane) & 1ull) st_wt_u64(ko + __popcll(kept & ((1ull << lane) - 1ull)), v);
     if (lane == 0) {
-      st_wt_u32(reinterpret_cast<int32_t *>(o.kc) + seg, static_cast<uint32_t>(__popcll(kept)));
+      st_wt_u32(reinterpret_cast<int32_t *>(o.kc) + seg, kcv);
       st_wt_u64(o.lastkey + seg, lk);
     }
   } else {
     if ((kept >> lane) & 1ull) ko[__popcll(kept & ((1ull << lane) - 1ull))] = v;
     if (lane == 0) {
-      o.kc[seg] = __popcll(kept);
+      o.kc[seg] = kcv;
       o.lastkey[seg] = lk;
     }
   }
@@ -1524,7 +1565,7 @@ __device__ __forceinline__ int merge_rank(
   __shared__ uint32_t r_off[kRankC + 1], r_kc[kRankC];
   __shared__ unsigned long long r_L;
   __shared__ uint32_t r_trunc, r_kth;
-  __shared__ int r_m, r_total, r_any;
+  __shared__ int r_m, r_total, r_any, r_corrupt;
   const int nslot = (C - 1) * wmax;   // kc <= wmax entries per class (stored at `stride`)
   if (C > kRankC || static_cast<size_t>(nslot) * 20 > static_cast<size_t>(kRankLds) || (nslot & 1)) return -1;
   const int tid = threadIdx.x, NT = blockDim.x;
@@ -1579,7 +1620,9 @@ __device__ __forceinline__ int merge_rank(
     for (int m = 32; m >= 1; m >>= 1) tr = max(tr, static_cast<uint32_t>(__shfl_xor(tr, m, 64)));
     const int total = static_cast<int>(__shfl(incl, 63, 64));
     const bool any = __ballot(lk != 0ull) != 0ull;   // whole wave (not inside the lane-0 branch)
+    const bool corrupt = __ballot(kcv == kKcCorrupt) != 0ull;
     if (c == 0) {
+      r_corrupt = corrupt;
       r_trunc = tr;
       r_any = any;
       r_total = total;
@@ -1589,6 +1632,13 @@ __device__ __forceinline__ int merge_rank(
   }
   __syncthreads();
   SEG_PHASE(1);
+  if (r_corrupt) {   // a segment met a prior index >= P: no detections, the caller is told
+    if (tid == 0) {
+      if (pass == 1) need[b] = 0;
+      out_count[b] = kDetCorrupt;
+    }
+    return 0;
+  }
   const int total = r_total;
   const bool any_trunc = r_any != 0;
   float *ob = out_boxes + static_cast<int64_t>(b) * top_k * 4;
@@ -1746,7 +1796,7 @@ __device__ __forceinline__ int merge_body(
   __shared__ int s_misc[4];
   __shared__ unsigned long long s_st[2];
   __shared__ float s_trunc;
-  __shared__ int s_any_trunc, s_cnt;
+  __shared__ int s_any_trunc, s_cnt, s_corrupt;
   __shared__ unsigned long long s_flag[16];
   __shared__ unsigned long long s_m[kMergeThreads];
   __shared__ int s_nk;
@@ -1774,9 +1824,10 @@ __device__ __forceinline__ int merge_body(
   if (tid == 0) {
     uint32_t acc = 0;
     float tr = -__builtin_inff();
-    int any = 0;
+    int any = 0, corrupt = 0;
     s_off[0] = 0;
     for (int c = 0; c < C; ++c) {
+      corrupt |= s_kc[c] == kKcCorrupt;
       acc += s_kc[c];
       s_off[c + 1] = acc;
       if (s_lk[c] == s_lk[c]) {
@@ -1786,8 +1837,16 @@ __device__ __forceinline__ int merge_body(
     }
     s_trunc = tr;
     s_any_trunc = any;
+    s_corrupt = corrupt;
   }
   __syncthreads();
+  if (s_corrupt) {   // a segment met a prior index >= P: no detections, the caller is told
+    if (tid == 0) {
+      if (pass == 1) need[b] = 0;
+      out_count[b] = kDetCorrupt;
+    }
+    return 0;
+  }
   // an undecidable image: ask for the second pass (pass 1) or report -1
   auto undecided = [&]() {
     if (tid == 0) {
@@ -2198,7 +2257,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
                     int flags, float *det_boxes, int64_t *det_labels, float *det_scores,
                     int32_t *det_count, int32_t *det_count_host, float *debug_probs,
                     float *debug_boxes, void *workspace, size_t workspace_bytes, void *stream) {
-  SBOD_REQUIRE((flags & ~(SBOD_DETECT_COUNTERS_ZEROED | SBOD_DETECT_INPUT_BF16 | SBOD_DETECT_TWO_PASS)) == 0,
+  SBOD_REQUIRE((flags & ~(SBOD_DETECT_COUNTERS_ZEROED | SBOD_DETECT_INPUT_BF16 | SBOD_DETECT_FUSED)) == 0,
                "sbod_detect_f32: unknown flags 0x%x", flags);
   const bool bf16 = (flags & SBOD_DETECT_INPUT_BF16) != 0;
   SBOD_REQUIRE(!bf16 || C <= 32, "sbod_detect_f32: bf16 input supports C <= 32 (C=%d)", C);
@@ -2276,7 +2335,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
   const int rank_slots = (C - 1) * w1;
   const bool fuse = !exhaustive && final_nms < 0.f && two && w1 <= 64 && C <= kRankC &&
                     static_cast<size_t>(rank_slots) * 20 <= static_cast<size_t>(kRankLds) && (rank_slots & 1) == 0 &&
-                    (flags & SBOD_DETECT_TWO_PASS) == 0;
+                    (flags & SBOD_DETECT_FUSED) != 0;
   if (fuse) {
     KernelTimer kt("k_det_nms", s, true);
     tlaunch(kt, k_det_nms<kNmsW>, dim3(C - 1, B), dim3(64 * kNmsW), static_cast<size_t>(rank_slots) * 20, s,

@@ -57,9 +57,10 @@ class _AnchorCriterion(nn.Module):
         self.grad_reduction = 'mean'
         self.force_collectives = False   # run the collectives even in a one-rank group (tests)
         # focal on one device: the matcher and the loss pass as separate launches (default), or as
-        # ONE launch (opt-in: its workgroups wait for each other, so it needs the whole device —
-        # with kernels of other streams sharing the CUs the grid is not co-resident and the
-        # bounded wait ends in a NaN loss; measured slower alone too)
+        # ONE launch (opt-in, variant library only: its workgroups wait for each other, so it needs
+        # the whole device — with kernels of other streams sharing the CUs the grid is not
+        # co-resident and the bounded wait ends in a NaN loss; measured slower alone too,
+        # DESIGN.md round 4)
         self.one_launch = False
         self.last_components = None
 

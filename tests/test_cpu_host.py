@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert missing == [], missing
     assert set(syms) <= set(L.SIGNATURES), set(syms) - set(L.SIGNATURES)
     assert L.MISSING == []
-    assert lib.sbod_abi_version() == 3
+    assert lib.sbod_abi_version() == 4
     assert b'gfx950' in lib.sbod_version()
 
 
@@ -127,23 +127,24 @@ def test_no_kernel_spills_to_scratch():
     assert bad == {}, bad
 
 
-def test_one_launch_criterion_residency_cap():
-    """The one-launch criterion's grid must be resident at once; the library caps its occupancy
-    query at 6 blocks per CU (loss.hip kCritBlocksPerCU), which holds while the kernels need at
-    most 112 SGPRs: 256-thread blocks per CU <= floor(800 / (ceil(sgpr / 16) * 16 + 16))
-    (MI355X_MICROARCH.md, residency).  A code change that raises the SGPR count past that fails
-    here instead of as an in-launch wait timeout on the GPU."""
+def test_product_library_has_no_ab_variants():
+    """the losing A/B forms are out of the product library — no one-launch
+    criterion kernel (k_multibox<..., true>: workgroups waiting on each other), no multi-tile loss
+    pass (k_multibox_tiles), and sbod_build_variants() says so; asking for the one-launch form
+    raises instead of silently running two launches."""
     import json
     path = os.path.join(REPO, 'shape_based_object_detection_amd', 'lib', 'kernel_resources.json')
     if not os.path.exists(path):
         pytest.skip('library not built with resource remarks')
     usage = json.load(open(path))
-    fused = {k: v for k, v in usage.items() if 'k_multibox' in k and 'Lb1E' in k}
-    assert len(fused) == 10, sorted(fused)
-    for k, v in fused.items():
-        sg = v['TotalSGPRs']
-        assert 800 // ((sg + 15) // 16 * 16 + 16) >= 6, (k, sg)
-        assert v['ScratchSize'] == 0
+    assert not [k for k in usage if 'k_multibox' in k and 'Lb1E' in k]
+    assert not [k for k in usage if 'k_multibox_tiles' in k]
+    assert L.lib().sbod_build_variants() == 0
+    assert not hasattr(L.lib(), 'sbod_set_multibox_tiles')
+    spec = core.CriterionSpec(L.REG['diou'], L.CLS['focal'])
+    with pytest.raises(L.SbodError, match='variant library'):
+        core.criterion_focal(torch.zeros(1, 8, 4), torch.zeros(1, 8, 21), None, None, None, spec, 0.5, 0.4,
+                             two_launch=False)
 
 
 def test_stress_anchor_generator_size():

@@ -2,19 +2,35 @@
 fused loss pass in one launch, k_multibox<..., true>) against the same call as two launches
 (k_match_tile + k_match_final, then k_multibox) and against the oracle.
 
-The two forms run the same per-prior arithmetic and the same exact fixed-point finish, so the
-matcher outputs, the positive counts, the loss vector and every gradient must be bit-identical;
-the oracle comparison is the north_star's 1e-4 relative."""
+The one-launch form lost its A/B and its workgroups wait for each other, so it
+is built into a VARIANT library only (EXTRA=-DSBOD_VARIANT_ONE_LAUNCH bash
+scripts/build_lib_variant.sh onelaunch; run this file with SBOD_LIB pointing at it).  With the
+product library these tests skip; tests/test_cpu_host.py checks the product library has none of it.
+
+The two forms run the same per-prior arithmetic and exact fixed-point finishes of the same
+per-workgroup partials, so the matcher outputs, the positive counts, the loss vector and every
+gradient must be bit-identical; the oracle comparison is the north_star's 1e-4 relative."""
 import numpy as np
 import pytest
 import torch
 
 from oracle import loss_ref as LR
+from shape_based_object_detection_amd import _lib as L
 from shape_based_object_detection_amd import core, synth
 from shape_based_object_detection_amd.models import criteria as CR
 from shape_based_object_detection_amd.models.priors import prior_table
 
-pytestmark = pytest.mark.gpu
+
+def _variant_built():
+    try:
+        return bool(L.lib().sbod_build_variants() & L.VARIANT_ONE_LAUNCH_CRITERION)
+    except L.SbodError:
+        return False
+
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not _variant_built(), reason='one-launch criterion: variant library only '
+                                                              '(SBOD_LIB=.../libsbod_hip_onelaunch.so)')]
 DEV = 'cuda'
 
 
@@ -137,3 +153,46 @@ def test_criterion_class_uses_one_launch_and_captures():
         assert core.criterion_status(DEV) == 0   # (the capture stream's workspace)
     assert loss.item() == e_loss
     assert torch.equal(lo.grad, e_gl) and torch.equal(sc.grad, e_gs)
+
+
+def test_timed_out_wait_poisons_gradients_and_next_call_is_clean():
+    """a one-launch call whose in-launch wait gives up (the grid not co-resident: a
+    long kernel of another stream holds the CUs) returns a NaN loss AND NaN gradients in the
+    workgroups that gave up, and the timeout word is cleared by that call's finish — the next
+    call on the same workspace (alone on the device) is finite and equals the two-launch form.
+    Whether the first call times out depends on the other stream's timing; the sticky diagnostics
+    word (sbod_criterion_status) says whether it did."""
+    P = torch.from_numpy(prior_table('SSD512')).to(DEV)
+    B = 32
+    boxes, labels = synth.make_gt(B, seed=5)
+    locs, scores = synth.make_preds(B, P.shape[0], 21, seed=5)
+    crit = CR.MultiBoxLoss512(priors_cxcy=P, config=Cfg(reg_weights=1.0, device=DEV, n_classes=21, reg_loss='diou',
+                                                        cls_loss='focal'))
+    spec = crit._spec()
+    gt = core.pack_gt([b.to(DEV) for b in boxes], [l.to(DEV) for l in labels])
+    hog_a = torch.randn(8192, 8192, device=DEV)
+    other = torch.cuda.Stream()
+    outs = []
+    for k in range(2):
+        lo = locs.to(DEV).requires_grad_(True)
+        sc = scores.to(DEV).requires_grad_(True)
+        if k == 0:   # a long GEMM on another stream first: the launch may not get every CU
+            with torch.cuda.stream(other):
+                for _ in range(4):
+                    hog_a = hog_a @ hog_a
+                    hog_a = hog_a / hog_a.abs().max()
+        loss, comps, _ = core.criterion_focal(lo, sc, gt, crit.priors_cxcy, crit.priors_xy, spec, crit.threshold,
+                                              crit.threshold - 0.1, two_launch=False)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs.append((loss.item(), sc.grad.clone(), core.criterion_status(DEV)))
+    first_loss, first_gs, first_status = outs[0]
+    if first_status != 0:
+        assert first_loss != first_loss and bool(torch.isnan(first_gs).any())
+    lo = locs.to(DEV).requires_grad_(True)
+    sc = scores.to(DEV).requires_grad_(True)
+    ref, _, _ = core.criterion_focal(lo, sc, gt, crit.priors_cxcy, crit.priors_xy, spec, crit.threshold,
+                                     crit.threshold - 0.1, two_launch=True)
+    ref.backward()
+    assert outs[1][0] == ref.item()
+    assert torch.equal(outs[1][1], sc.grad)

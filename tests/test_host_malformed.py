@@ -58,7 +58,7 @@ def _call_all(value):
     lib = L.lib()
     out = {}
     skip = {'sbod_timing_enable', 'sbod_timing_query', 'sbod_timing_every', 'sbod_timing_reset_graphs',
-            'sbod_memcpy_d2h_async', 'sbod_stream_wait', 'sbod_set_multibox_tiles'}   # (a knob, not a call)
+            'sbod_memcpy_d2h_async', 'sbod_stream_wait'}
     for name, (res, args) in L.SIGNATURES.items():
         if name in skip or not args:
             continue
