@@ -1,8 +1,15 @@
-"""Data-parallel sharding on CPU (gloo, world_size 2): each rank owns half the images, the batch
-positive count is SUM-all-reduced through ``core.allreduce_npos`` (the same call the criteria use
-over RCCL), and every rank normalises by it.  Then the sum of the shard losses equals the
-single-process loss and every rank's gradients equal its slice of the full-batch gradients
-(SURVEY §8(e)).  The loss arithmetic is the oracle's (the HIP kernels are covered by -m gpu)."""
+"""Data-parallel sharding on CPU (gloo, world sizes 2, 4 and 8 — this container's 8 cores): each
+rank owns a slice of the images, the batch positive count is SUM-all-reduced through
+``core.allreduce_npos`` (the same call the criteria use over RCCL), and every rank normalises by
+it.  Then the sum of the shard losses equals the single-process loss and every rank's gradients
+equal its slice of the full-batch gradients.  The loss arithmetic is the oracle's
+(the HIP kernels are covered by -m gpu).
+
+Cases: even and UNEVEN shards (B=30 over 4: 7, 8, 7, 8 images), B=32 over 8,
+a rank whose images have no positive at all, MultiBoxLoss300's global hard-negative exchange
+(SSD300.py:580-588) at 2, 4 and 8 ranks (and its loud refusal of unequal shards), config C5's
+batch 64 over 8 with FCOSLoss's (positives + images) normaliser (FCOSDet.py:527-529), and the
+criterion classes with DDP's gradient averaging."""
 import os
 import socket
 
@@ -16,7 +23,8 @@ from oracle import loss_ref as LR
 from shape_based_object_detection_amd import core, synth
 from shape_based_object_detection_amd.models.priors import prior_table
 
-B, C = 4, 21
+C = 21
+FAR = torch.tensor([[1.5, 1.5, 1.6, 1.6]])   # outside every prior: an image without positives
 
 
 def _free_port():
@@ -27,15 +35,53 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kind, reg, cls, out_q):
+def _priors():
+    return torch.from_numpy(prior_table('SSD300')[::3].copy())
+
+
+def _shard(rank, world, B):
+    return slice(rank * B // world, (rank + 1) * B // world)
+
+
+def _data(B, seed, P, zero_rank=None, world=1):
+    """Ground truth and predictions of the whole batch; with ``zero_rank`` that rank's images get
+    one object outside every prior (no positive, no forced match)."""
+    boxes, labels = synth.make_gt(B, seed=seed)
+    locs, scores = synth.make_preds(B, P.shape[0], C, seed=seed)
+    if zero_rank is not None:
+        for i in range(B)[_shard(zero_rank, world, B)]:
+            boxes[i], labels[i] = FAR.clone(), torch.tensor([3])
+    return boxes, labels, locs, scores
+
+
+def _run(target, world, *args):
+    """Start `world` gloo ranks running target(rank, world, port, *args, queue); results by rank."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _init(rank, world, port):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    torch.set_num_threads(1)
     dist.init_process_group('gloo', rank=rank, world_size=world)
+
+
+def _worker(rank, world, port, kind, reg, cls, B, seed, zero_rank, out_q):
+    _init(rank, world, port)
     try:
-        P = torch.from_numpy(prior_table('SSD300')[::3].copy())
-        boxes, labels = synth.make_gt(B, seed=77)
-        locs, scores = synth.make_preds(B, P.shape[0], C, seed=77)
-        sl = slice(rank * B // world, (rank + 1) * B // world)
+        P = _priors()
+        boxes, labels, locs, scores = _data(B, seed, P, zero_rank, world)
+        sl = _shard(rank, world, B)
         my_boxes, my_labels = boxes[sl], labels[sl]
         n_local = LR.local_npos(P, my_boxes, my_labels)
         npos = torch.tensor([0, n_local], dtype=torch.int32)   # [per-image..., total] layout
@@ -46,51 +92,62 @@ def _worker(rank, world, port, kind, reg, cls, out_q):
         loss.backward()
         total = loss.detach().clone()
         dist.all_reduce(total)
-        out_q.put((rank, float(total), int(tot.item()), lo.grad.numpy(), sc.grad.numpy()))
+        out_q.put((rank, float(total), int(tot.item()), n_local, lo.grad.numpy(), sc.grad.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('kind,reg,cls', [('ssd512', 'diou', 'focal'), ('retina', 'smoothl1', 'ce'),
-                                          ('ssd512', 'smoothl1', 'ce')])
-def test_dp_shards_match_single_process(kind, reg, cls):
-    world = 2
-    ctx = mp.get_context('spawn')
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, reg, cls, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    P = torch.from_numpy(prior_table('SSD300')[::3].copy())
-    boxes, labels = synth.make_gt(B, seed=77)
-    locs, scores = synth.make_preds(B, P.shape[0], C, seed=77)
+def _single(kind, reg, cls, B, seed, zero_rank=None, world=1):
+    P = _priors()
+    boxes, labels, locs, scores = _data(B, seed, P, zero_rank, world)
     lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
     ref = LR.criterion(kind, P, lo, sc, boxes, labels, reg, cls)
     ref.backward()
-    assert res[0][2] == res[1][2] == LR.local_npos(P, boxes, labels)
-    np.testing.assert_allclose(res[0][1], ref.item(), rtol=1e-5)
-    np.testing.assert_allclose(np.concatenate([r[3] for r in res]), lo.grad.numpy(), rtol=1e-5, atol=1e-9)
-    np.testing.assert_allclose(np.concatenate([r[4] for r in res]), sc.grad.numpy(), rtol=1e-5, atol=1e-9)
+    return ref.item(), LR.local_npos(P, boxes, labels), lo.grad.numpy(), sc.grad.numpy()
 
 
-def _worker_global_pool(rank, world, port, out_q):
+def _check(res, ref_loss, ref_npos, ref_gl, ref_gs, world):
+    assert len(res) == world
+    assert all(r[2] == ref_npos for r in res)               # every rank holds the global count
+    assert sum(r[3] for r in res) == ref_npos
+    np.testing.assert_allclose(res[0][1], ref_loss, rtol=1e-5)
+    np.testing.assert_allclose(np.concatenate([r[4] for r in res]), ref_gl, rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(np.concatenate([r[5] for r in res]), ref_gs, rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize('kind,reg,cls,world,B', [
+    ('ssd512', 'diou', 'focal', 2, 4), ('retina', 'smoothl1', 'ce', 2, 4), ('ssd512', 'smoothl1', 'ce', 2, 4),
+    ('ssd512', 'diou', 'focal', 4, 30), ('retina', 'smoothl1', 'ce', 4, 30),     # uneven: 7, 8, 7, 8 images
+    ('ssd512', 'diou', 'focal', 8, 32), ('ssd512', 'smoothl1', 'ce', 8, 32), ('retina', 'diou', 'focal', 8, 32)])
+def test_dp_shards_match_single_process(kind, reg, cls, world, B):
+    res = _run(_worker, world, kind, reg, cls, B, 77, None)
+    _check(res, *_single(kind, reg, cls, B, 77), world)
+
+
+@pytest.mark.parametrize('kind,reg,cls', [('ssd512', 'diou', 'focal'), ('ssd512', 'smoothl1', 'ce'),
+                                          ('retina', 'diou', 'focal')])
+def test_dp_rank_without_positives(kind, reg, cls):
+    """Rank 2 of 4 holds only images without a positive: it contributes zero to the count, its
+    regression terms vanish, its negatives are still normalised by the global count."""
+    world, B = 4, 8
+    res = _run(_worker, world, kind, reg, cls, B, 91, 2)
+    assert res[2][3] == 0 and res[0][2] > 0
+    assert not np.any(res[2][4])                               # no box gradient on that rank
+    _check(res, *_single(kind, reg, cls, B, 91, zero_rank=2, world=world), world)
+
+
+def _worker_global_pool(rank, world, port, B, seed, zero_rank, out_q):
     """MultiBoxLoss300 CE: hard negatives are mined over the WHOLE batch (SSD300.py:580-588), so
     the ranks exchange their pools through ``core.allgather_pool`` (the criteria's exchange
     step) and each mines its rows of the global top-k."""
-    os.environ['MASTER_ADDR'] = '127.0.0.1'
-    os.environ['MASTER_PORT'] = str(port)
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    _init(rank, world, port)
     try:
-        P = torch.from_numpy(prior_table('SSD300')[::3].copy())
-        boxes, labels = synth.make_gt(B, seed=78)
-        locs, scores = synth.make_preds(B, P.shape[0], C, seed=78)
-        sl = slice(rank * B // world, (rank + 1) * B // world)
+        P = _priors()
+        boxes, labels, locs, scores = _data(B, seed, P, zero_rank, world)
+        sl = _shard(rank, world, B)
         my_boxes, my_labels = boxes[sl], labels[sl]
-        npos = torch.tensor([0, LR.local_npos(P, my_boxes, my_labels)], dtype=torch.int32)
+        n_local = LR.local_npos(P, my_boxes, my_labels)
+        npos = torch.tensor([0, n_local], dtype=torch.int32)
         tot = int(core.allreduce_npos(npos).item())
         pool = LR.ssd300_pool(P, scores[sl], my_boxes, my_labels)
         pool_all, off = core.allgather_pool()(pool)
@@ -101,47 +158,95 @@ def _worker_global_pool(rank, world, port, out_q):
         loss.backward()
         total = loss.detach().clone()
         dist.all_reduce(total)
-        out_q.put((rank, float(total), off, lo.grad.numpy(), sc.grad.numpy()))
+        out_q.put((rank, float(total), tot, n_local, lo.grad.numpy(), sc.grad.numpy(), off))
     finally:
         dist.destroy_process_group()
 
 
-def test_dp_ssd300_global_mining_exchange():
-    world = 2
-    ctx = mp.get_context('spawn')
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_global_pool, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    P = torch.from_numpy(prior_table('SSD300')[::3].copy())
-    boxes, labels = synth.make_gt(B, seed=78)
-    locs, scores = synth.make_preds(B, P.shape[0], C, seed=78)
-    lo, sc = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
-    ref = LR.criterion('ssd300', P, lo, sc, boxes, labels, 'l1', 'ce')
+@pytest.mark.parametrize('world,B,zero_rank', [(2, 4, None), (4, 8, None), (8, 32, None), (8, 32, 5)])
+def test_dp_ssd300_global_mining_exchange(world, B, zero_rank):
+    res = _run(_worker_global_pool, world, B, 78, zero_rank)
+    P = _priors()
+    assert [r[6] for r in res] == [r * (B // world) * P.shape[0] for r in range(world)]   # rank-major offsets
+    _check(res, *_single('ssd300', 'l1', 'ce', B, 78, zero_rank, world), world)
+
+
+def _worker_uneven_pool(rank, world, port, B, out_q):
+    _init(rank, world, port)
+    try:
+        P = _priors()
+        boxes, labels, locs, scores = _data(B, 80, P)
+        sl = _shard(rank, world, B)
+        pool = LR.ssd300_pool(P, scores[sl], boxes[sl], labels[sl])
+        try:
+            core.allgather_pool()(pool)
+            out_q.put((rank, 'gathered'))
+        except RuntimeError as e:
+            out_q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_ssd300_uneven_shards_refused_on_every_rank():
+    """The global pool needs equal per-rank batches (a DistributedSampler with drop_last gives
+    them): B=30 over 4 ranks fails loudly on EVERY rank instead of desynchronising the gather."""
+    res = _run(_worker_uneven_pool, 4, 30)
+    assert all('unequal batches' in r[1] for r in res), res
+
+
+def _worker_c5(rank, world, port, b_rank, locs_per_img, out_q):
+    """Config C5's split (FCOS, batch 64 over 8 ranks): each rank's sigmoid-focal sum over its
+    8 images, normalised by the GLOBAL (positives + images) that FCOSLoss divides by
+    (FCOSDet.py:527-529), exchanged by ``core.allreduce_npos``."""
+    _init(rank, world, port)
+    try:
+        logits, labels = _c5_rows(rank, b_rank, locs_per_img)
+        n_local = int((labels > 0).sum()) + b_rank
+        tot = int(core.allreduce_npos(torch.tensor([0, n_local], dtype=torch.int32)).item())
+        z = logits.clone().requires_grad_(True)
+        loss = LR.focal_sigmoid(z, labels) / tot
+        loss.backward()
+        total = loss.detach().clone()
+        dist.all_reduce(total)
+        out_q.put((rank, float(total), tot, n_local, z.grad.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _c5_rows(rank, b_rank, locs_per_img, n_classes=81):
+    g = torch.Generator().manual_seed(500 + rank)
+    rows = b_rank * locs_per_img
+    logits = torch.randn(rows, n_classes, generator=g)
+    labels = torch.zeros(rows, dtype=torch.int64)
+    pos = torch.rand(rows, generator=g) < 0.015
+    labels[pos] = torch.randint(1, n_classes, (int(pos.sum()),), generator=g)
+    return logits, labels
+
+
+def test_dp_c5_batch64_over_8_normaliser():
+    world, b_rank, lpi = 8, 8, 300
+    res = _run(_worker_c5, world, b_rank, lpi)
+    parts = [_c5_rows(r, b_rank, lpi) for r in range(world)]
+    z = torch.cat([p[0] for p in parts]).requires_grad_(True)
+    y = torch.cat([p[1] for p in parts])
+    norm = int((y > 0).sum()) + world * b_rank
+    ref = LR.focal_sigmoid(z, y) / norm
     ref.backward()
-    assert [r[2] for r in res] == [0, (B // world) * P.shape[0]]
+    assert all(r[2] == norm for r in res) and sum(r[3] for r in res) == norm
     np.testing.assert_allclose(res[0][1], ref.item(), rtol=1e-5)
-    np.testing.assert_allclose(np.concatenate([r[3] for r in res]), lo.grad.numpy(), rtol=1e-5, atol=1e-9)
-    np.testing.assert_allclose(np.concatenate([r[4] for r in res]), sc.grad.numpy(), rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(np.concatenate([r[4] for r in res]), z.grad.numpy(), rtol=1e-5, atol=1e-10)
 
 
-def _worker_criterion_class(rank, world, port, kind, reg, cls, out_q):
+def _worker_criterion_class(rank, world, port, kind, reg, cls, B, out_q):
     """The drop-in criterion CLASS with ``distributed = True`` over gloo, through a CPU seam: its
     orchestration runs unchanged, only the device entry points it calls (pack_gt, match,
     fused_criterion) are oracle-backed CPU stand-ins.  Shared 'network' parameters theta feed
     every rank's predictions, and their gradients are AVERAGED over ranks as DDP does."""
-    os.environ['MASTER_ADDR'] = '127.0.0.1'
-    os.environ['MASTER_PORT'] = str(port)
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    _init(rank, world, port)
     try:
         from shape_based_object_detection_amd import _lib as L
         from shape_based_object_detection_amd.models import criteria as CR
-        P = torch.from_numpy(prior_table('SSD300')[::3].copy())
+        P = _priors()
         calls = []
         reg_name = {v: k for k, v in L.REG.items()}
         cls_name = {v: k for k, v in L.CLS.items()}
@@ -182,7 +287,7 @@ def _worker_criterion_class(rank, world, port, kind, reg, cls, out_q):
         crit.distributed = True
         boxes, labels = synth.make_gt(B, seed=79)
         locs, scores = synth.make_preds(B, P.shape[0], C, seed=79)
-        sl = slice(rank * B // world, (rank + 1) * B // world)
+        sl = _shard(rank, world, B)
         th_l = torch.zeros(4, requires_grad=True)
         th_s = torch.zeros(C, requires_grad=True)
         loss = crit(locs[sl] + th_l, scores[sl] + th_s, boxes[sl], labels[sl])
@@ -199,27 +304,18 @@ def _worker_criterion_class(rank, world, port, kind, reg, cls, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('kind,reg,cls', [('ssd512', 'diou', 'focal'), ('ssd300', 'smoothl1', 'ce'),
-                                          ('retina', 'smoothl1', 'ce')])
-def test_dp_criterion_class_ddp_mean(kind, reg, cls):
+@pytest.mark.parametrize('kind,reg,cls,world', [('ssd512', 'diou', 'focal', 2), ('ssd300', 'smoothl1', 'ce', 2),
+                                                ('retina', 'smoothl1', 'ce', 2), ('ssd512', 'diou', 'focal', 4),
+                                                ('ssd300', 'smoothl1', 'ce', 4)])
+def test_dp_criterion_class_ddp_mean(kind, reg, cls, world):
     """criterion.distributed = True: the class makes the exchange calls (positive-count all-reduce;
     SSD300 CE also the pool all-gather), and with DDP's gradient AVERAGING the shared parameters'
     gradient and the mean loss equal the single-process batch's."""
-    world = 2
-    ctx = mp.get_context('spawn')
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_criterion_class, args=(r, world, port, kind, reg, cls, q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    B = 8
+    res = _run(_worker_criterion_class, world, kind, reg, cls, B)
     want = ['match', 'allreduce_npos'] + (['allgather_pool'] if kind == 'ssd300' else [])
     assert all(r[1] == want for r in res), [r[1] for r in res]
-    P = torch.from_numpy(prior_table('SSD300')[::3].copy())
+    P = _priors()
     boxes, labels = synth.make_gt(B, seed=79)
     locs, scores = synth.make_preds(B, P.shape[0], C, seed=79)
     th_l = torch.zeros(4, requires_grad=True)
