@@ -714,6 +714,61 @@ def c2_figure(dev, steps, warmup, B=16, n_batches=12, det_form='two'):
                          'timing': 'HIP events attached to each dispatch, 12 eager criterion halves alone'}}
 
 
+def api_figure(st, steps, dist, dev, depth=4):
+    """The drop-in API path as a caller issues it (train_anchor.py:271-284 and :342-363): the
+    reference-named criterion class on the per-image GT lists, ``loss.backward()`` (autograd's own
+    upstream gradient), and ``models.utils.detect(...)`` — with ``async_=True`` so the step is
+    pipelined ``depth`` deep like the headline (step k issued before step k-depth+1's lists are
+    collected; no other host sync).  Every call does its full per-call host work (argument checks,
+    GT packing, allocations, autograd).  Returns ms per step and the host time per call."""
+    from shape_based_object_detection_amd.models import utils as MU
+    crit = CR.MultiBoxLoss512(priors_cxcy=st.priors, config=st.cfg)
+    host = [0.0, 0.0, 0.0, 0.0]
+
+    def one(k):
+        bt = st.batches[k % len(st.batches)]
+        bt.locs.grad = None
+        bt.scores.grad = None
+        t0 = time.perf_counter()
+        loss = crit(bt.locs, bt.scores, bt.boxes, bt.labels)
+        t1 = time.perf_counter()
+        loss.backward()
+        t2 = time.perf_counter()
+        h = MU.detect(bt.locs.detach(), bt.det_scores, 0.01, 0.45, 200, st.priors, st.cfg, async_=True)
+        t3 = time.perf_counter()
+        host[0] += t1 - t0
+        host[1] += t2 - t1
+        host[2] += t3 - t2
+        return h
+
+    def loop(n):
+        pend = collections.deque()
+        for k in range(n):
+            pend.append(one(k))
+            if len(pend) >= depth:
+                t = time.perf_counter()
+                pend.popleft().wait()
+                host[3] += time.perf_counter() - t
+        while pend:
+            pend.popleft().wait()
+
+    loop(2 * depth)
+    torch.cuda.synchronize()
+    host[:] = [0.0, 0.0, 0.0, 0.0]
+    n = max(steps, 50)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loop(n)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {'ms_per_step': round(el / n * 1e3, 4), 'steps': n, 'pipeline_depth': depth,
+            'host_us_per_call': {'criterion': round(host[0] / n * 1e6, 1), 'backward': round(host[1] / n * 1e6, 1),
+                                 'detect': round(host[2] / n * 1e6, 1),
+                                 'collect_incl_wait': round(host[3] / n * 1e6, 1)},
+            'calls': 'MultiBoxLoss512(...)(locs, scores, boxes, labels); loss.backward(); '
+                     'models.utils.detect(..., async_=True) collected %d steps later' % (depth - 1)}
+
+
 def timed(fn, steps, dist, dev, per_step=None, finish=None):
     torch.cuda.synchronize()
     if dist:
@@ -851,9 +906,12 @@ def main():
     dom_avg_s = ms_dom / n_dom * 1e-3 if n_dom else float('nan')
 
     eager_ms = None
+    api = None
     if st.use_graph:        # the same step without the graph, for the host-overhead comparison
         n_e = min(a.steps, 20)
         eager_ms = timed(st.eager, n_e, dist, dev) / n_e * 1e3
+        if world == 1:      # the drop-in API path a caller drives
+            api = api_figure(st, min(a.steps, 200), dist, dev)
 
     spans = []
     if st.use_graph:
@@ -933,6 +991,8 @@ def main():
         'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
+        'api_ms_per_step': api['ms_per_step'] if api else None,
+        'api': api,
     }
     algo = ALGO_BYTES[dominant](wl)
     achieved = algo / dom_avg_s / 1e9

@@ -89,19 +89,70 @@ def _pack_fast(boxes, labels, capacity, per_image, dev_index, out_b, out_l, out_
     return r
 
 
-def pack_gt(boxes, labels, device=None, allow_empty=False):
+# pack_gt's output buffers for regular device batches, cached per (device, stream, batch size)
+# and grown on demand: every consumer of a pack runs in stream order on the stream that packed
+# it, so the next pack on that stream may overwrite the buffers (as the per-stream workspaces).
+_PACK_CACHE = {}
+_PACK_CAP = {}    # rows to allocate next time for a key whose batch overflowed its buffers
+
+
+def _pack_cached(boxes, labels, allow_empty):
+    """The C++ list check + sbod_gt_pack launch into the stream's cached buffers (no Python loop
+    over the images, no allocation).  None when the batch needs the Python path."""
+    ext = L.host_ext
+    if ext is None or type(boxes) is not list or type(labels) is not list or not boxes:
+        return None
+    b0 = boxes[0]
+    if not b0.is_cuda:
+        return None
+    dev = b0.device
+    B = len(boxes)
+    stream = L._raw_stream(dev.index)
+    key = (dev.index, stream, B)
+    buf = _PACK_CACHE.get(key)
+    if buf is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None   # nothing is allocated under capture: the Python path's own tensors
+        cap = max(_PACK_CAP.get(key, 0), 256 * B)
+        buf = _PACK_CACHE[key] = (torch.empty(cap, 4, dtype=torch.float32, device=dev),
+                                  torch.empty(cap, dtype=torch.int64, device=dev),
+                                  torch.empty(B + 1, dtype=torch.int32, device=dev), cap)
+    gb, gl, off, cap = buf
+    r = ext.pack_device_lists(boxes, labels, cap, -1, dev.index, gb.data_ptr(), gl.data_ptr(), off.data_ptr(),
+                              stream, allow_empty)
+    if r is None:
+        return None
+    if type(r) is int:
+        raise L.SbodError('sbod_gt_pack failed (%d): %s' % (r, L.lib().sbod_last_error().decode(errors='replace')))
+    n = sum(r)
+    return GtPack(gb[:n], gl[:n], off, r)
+
+
+def pack_gt(boxes, labels, device=None, allow_empty=False, reuse=False):
     """Pack per-image lists into a GtPack with ONE device launch (sbod_gt_pack: the pointers
     and offsets travel in the kernel arguments).  An image with no objects raises like the
     reference does (``overlap.max(dim=0)`` of an empty matrix, models/SSD512.py:538).  A GtPack
-    (e.g. from ``GtStaging.stage``) is returned as is."""
+    (e.g. from ``GtStaging.stage``) is returned as is.  ``reuse=True`` (a caller that consumes
+    the pack at once on the current stream, e.g. the criterion classes): a regular device batch
+    (lists of [G,4] float32 / [G] int64 contiguous device tensors) is checked and packed in C++
+    into buffers cached per stream, which the NEXT reuse-pack on that stream overwrites; anything
+    else (conversions, errors) takes the Python path with buffers of its own."""
     if isinstance(boxes, GtPack):
         return boxes
     if len(boxes) != len(labels):
         raise ValueError('boxes and labels must have the same length')
+    if reuse:
+        fast = _pack_cached(boxes, labels, allow_empty)
+        if fast is not None:
+            return fast
     counts = [b.shape[0] for b in boxes]
     _check_counts(counts, allow_empty)
     bx, lb, dev = _as_rows(boxes, labels)
     n = sum(counts)
+    key = (dev.index, L._raw_stream(dev.index), len(counts))
+    if key in _PACK_CACHE and n > _PACK_CACHE[key][3] and not torch.cuda.is_current_stream_capturing():
+        _PACK_CAP[key] = 2 * n    # the stream's buffers grow on its next regular call
+        del _PACK_CACHE[key]
     gb = torch.empty(max(n, 1), 4, dtype=torch.float32, device=dev)
     gl = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     off = torch.empty(len(counts) + 1, dtype=torch.int32, device=dev)
@@ -448,23 +499,39 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
     return loss, holder[0]
 
 
+_VARIANTS = []        # sbod_build_variants(), queried once
+_CRIT_SIZES = {}      # (B, Gmax, P) -> (workspace bytes, zero-on-entry bytes)
+_MATCH_OUT = {}       # (device, stream, B, P) -> (obj, ovl, npos) reused by criterion classes
+
+
+def _variants():
+    if not _VARIANTS:
+        _VARIANTS.append(L.lib().sbod_build_variants())
+    return _VARIANTS[0]
+
+
 def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, neg_threshold,
-                    two_launch=False):
+                    two_launch=False, fresh_match=True):
     """A focal criterion on one device in ONE launch (sbod_criterion_focal): the matcher and the
     fused loss + gradient pass, the normaliser produced inside the launch.  Returns (scalar loss
     with autograd, device vector {total, conf, loc, n_pos_total}, (obj, ovl, n_pos)).
     ``two_launch`` runs the same call as the matcher and loss launches — the only form the product
     library has (the one-launch form is a variant build, sbod_build_variants(); asking for it from
-    the product library raises instead of silently running two launches)."""
-    if not two_launch and not (L.lib().sbod_build_variants() & L.VARIANT_ONE_LAUNCH_CRITERION):
+    the product library raises instead of silently running two launches).
+    ``fresh_match=False`` (the criterion classes, which do not keep the matcher outputs): obj /
+    ovl / n_pos live in buffers reused by the next call on the same stream."""
+    if not two_launch and not (_variants() & L.VARIANT_ONE_LAUNCH_CRITERION):
         raise L.SbodError('the one-launch criterion is built into the variant library only '
                           '(EXTRA=-DSBOD_VARIANT_ONE_LAUNCH scripts/build_lib_variant.sh); this library runs the '
                           'matcher and the loss pass as two launches (criterion.one_launch = False)')
-    locs = locs.contiguous()
-    scores = scores.contiguous()
-    if locs.dtype not in (torch.float32, torch.bfloat16) or scores.dtype != locs.dtype:
+    if not locs.is_contiguous():
+        locs = locs.contiguous()
+    if not scores.is_contiguous():
+        scores = scores.contiguous()
+    ldt = locs.dtype
+    if (ldt is not torch.float32 and ldt is not torch.bfloat16) or scores.dtype is not ldt:
         raise TypeError('sbod criterion: locs/scores must both be float32 or bfloat16')
-    dt = L.DT_F32 if locs.dtype == torch.float32 else L.DT_BF16
+    dt = L.DT_F32 if ldt is torch.float32 else L.DT_BF16
     B, P, C = scores.shape
     if locs.shape != (B, P, 4) or priors_cxcy.shape[0] != P:
         raise AssertionError('n_priors mismatch: priors %d, locs %s, scores %s'
@@ -472,12 +539,23 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
     if gt.batch != B:
         raise ValueError('criterion: %d images of ground truth for a batch of %d' % (gt.batch, B))
     dev = locs.device
-    stream = L.stream_of(locs)
-    obj = torch.empty(B, P, dtype=torch.int32, device=dev)
-    ovl = torch.empty(B, P, dtype=torch.float32, device=dev)
-    npos = torch.empty(B + 1, dtype=torch.int32, device=dev)
+    stream = L._raw_stream(dev.index)
+    mkey = (dev.index, stream, B, P)
+    mo = None if fresh_match else _MATCH_OUT.get(mkey)
+    if mo is None:
+        mo = (torch.empty(B, P, dtype=torch.int32, device=dev), torch.empty(B, P, dtype=torch.float32, device=dev),
+              torch.empty(B + 1, dtype=torch.int32, device=dev))
+        if not fresh_match and not torch.cuda.is_current_stream_capturing():
+            _MATCH_OUT[mkey] = mo
+    obj, ovl, npos = mo
     gmax = max(int(gt.gmax), 1)
-    pxy = priors_xy.contiguous()
+    pxy = priors_xy if priors_xy.is_contiguous() else priors_xy.contiguous()
+    sizes = _CRIT_SIZES.get((B, gmax, P))
+    if sizes is None:
+        lib = L.lib()
+        sizes = _CRIT_SIZES[(B, gmax, P)] = (lib.sbod_criterion_workspace_bytes(B, gmax, P),
+                                             lib.sbod_criterion_zero_bytes(B, gmax, P))
+    nb, zb = sizes
     holder = []
 
     def run(want_grad):
@@ -485,19 +563,18 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
         holder.append(out)
         gl = torch.empty_like(locs) if want_grad else None
         gs = torch.empty_like(scores) if want_grad else None
-        lib = L.lib()
-        nb = lib.sbod_criterion_workspace_bytes(B, gmax, P)
-        zb = lib.sbod_criterion_zero_bytes(B, gmax, P)
         ws = workspace(nb, dev, 'criterion')
+        wp = ws.data_ptr()
         zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion')
-        _CLEAN.pop(ws.data_ptr(), None)
+        _CLEAN.pop(wp, None)
         flags = ((spec.flags & (L.LOSS_FOCAL_NORM | L.LOSS_UNFUSED_FINISH)) | zflag |
                  (L.CRIT_TWO_LAUNCH if two_launch else 0))
-        L.call('sbod_criterion_focal', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy), L.ptr(pxy),
-               L.ptr(gt.boxes), L.ptr(gt.labels), L.ptr(gt.offsets), gmax, float(threshold), float(neg_threshold),
-               spec.reg, flags, float(spec.reg_weight), float(spec.alpha), float(spec.gamma), L.ptr(obj), L.ptr(ovl),
-               L.ptr(npos), L.ptr(gl), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
-        _CLEAN[ws.data_ptr()] = zb   # (only the zero-on-entry prefix is known clean)
+        L.call('sbod_criterion_focal', locs.data_ptr(), scores.data_ptr(), dt, B, P, C, priors_cxcy.data_ptr(),
+               pxy.data_ptr(), gt.boxes.data_ptr(), gt.labels.data_ptr(), gt.offsets.data_ptr(), gmax,
+               float(threshold), float(neg_threshold), spec.reg, flags, float(spec.reg_weight), float(spec.alpha),
+               float(spec.gamma), obj.data_ptr(), ovl.data_ptr(), npos.data_ptr(), L.ptr(gl), L.ptr(gs),
+               out.data_ptr(), wp, nb, stream)
+        _CLEAN[wp] = zb   # (only the zero-on-entry prefix is known clean)
         return out, gl, gs
 
     want = torch.is_grad_enabled() and (locs.requires_grad or scores.requires_grad)
@@ -624,7 +701,7 @@ class DetectHandle:
             # THAT stream: a later detect already queued there (pipelined graph replays share
             # the workspace) finishes first and leaves the counters zero, and the retry cannot
             # overlap it.  cnt.cpu() then waits for the retry in that stream's order.
-            with torch.cuda.stream(self._stream):
+            with torch.cuda.stream(torch.cuda.ExternalStream(self._stream)):
                 _detect_launch(*self._launch_args(4096))
                 counts = cnt.cpu().tolist()
                 if min(counts) < 0:
@@ -637,6 +714,8 @@ class DetectHandle:
         if in_place and lc is not locs:
             locs.copy_(lc)          # models/utils.py:224 clamps the caller's tensor in place
         if min(counts) == top_k:     # every image full (the usual eval case)
+            if self._full is None:
+                self._full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
             res = self._full
         else:
             sizes = []
@@ -695,10 +774,21 @@ def reserve_count_slots(dev, B, n):
         free.append((torch.empty(B, dtype=torch.int32, pin_memory=True), torch.cuda.Event()))
 
 
+_DET_SIZES = {}   # (B, P, C) -> (workspace bytes, counter bytes)
+
+
+def _det_sizes(B, P, C):
+    v = _DET_SIZES.get((B, P, C))
+    if v is None:
+        lib = L.lib()
+        v = _DET_SIZES[(B, P, C)] = (lib.sbod_detect_workspace_bytes(B, P, C), lib.sbod_detect_counter_bytes(B, C))
+    return v
+
+
 def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn, out,
                    dbg, ws, nb, cnt_host, in_flags, window):
     out_b, out_l, out_s, cnt = out
-    need = L.lib().sbod_detect_counter_bytes(B, C)
+    need = _det_sizes(B, P, C)[1]
     flags = _zeroed_flag(ws, need, L.DETECT_COUNTERS_ZEROED, 'detect') | in_flags
     # a call that fails part-way can leave its counters non-zero (k_det_prepare has added to
     # them, k_det_merge never ran): the workspace counts as clean again only after a success
@@ -753,7 +843,7 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     cnt = torch.empty(B, dtype=torch.int32, device=dev)
     dbg_p = torch.empty(B, P, C, dtype=torch.float32, device=dev) if debug else None
     dbg_b = torch.empty(B, P, 4, dtype=torch.float32, device=dev) if debug else None
-    nb = L.lib().sbod_detect_workspace_bytes(B, P, C)
+    nb = _det_sizes(B, P, C)[0]
     ws = workspace(nb, dev, 'detect')
     fn = -1.0 if final_nms is None else float(final_nms)
     # counts -> pinned host memory (written by the last detect kernel itself) behind an event,
@@ -773,15 +863,21 @@ def detect(locs, scores, min_score, max_overlap, top_k, priors_cxcy, box_type='o
     launch = (lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overlap, top_k, fn,
               (out_b, out_l, out_s, cnt), (dbg_p, dbg_b), ws, nb, cnt_host, in_flags)
     _detect_launch(*launch, window)
+    raw = L._raw_stream(dev.index)   # the stream whose workspace the launch used
     if not capture:
-        ev.record(torch.cuda.current_stream(dev))
-    # the per-image views for the usual all-full case are built while the kernels run
-    full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0)))
+        ce = ev.cuda_event   # 0 until torch creates the event at its first record
+        if ce:
+            L.call('sbod_event_record', ce, raw)
+        else:
+            ev.record(torch.cuda.current_stream(dev))
+    # the per-image views for the usual all-full case: built while the kernels run when the call
+    # waits for them itself, else by wait() (a pipelined caller collects them later anyway)
+    full = (list(out_b.unbind(0)), list(out_l.unbind(0)), list(out_s.unbind(0))) if not async_ else None
     h = DetectHandle((lc, locs, sc, B, top_k, in_place, debug), (out_b, out_l, out_s, cnt, dbg_p, dbg_b),
                      cnt_host, ev, full, window, persistent=capture)
     h._launch = launch
     h._slot_key = (dev, B)
-    h._stream = torch.cuda.current_stream(dev)   # the stream whose workspace the launch used
+    h._stream = raw
     return h if (async_ or capture) else h.wait()
 
 

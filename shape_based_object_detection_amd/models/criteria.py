@@ -105,14 +105,14 @@ class _AnchorCriterion(nn.Module):
                                              _cfg(self.config, 'reg_loss', 'smoothl1'),
                                              _cfg(self.config, 'cls_loss', 'ce'), self.threshold,
                                              self.neg_pos_ratio, self.alpha)
-        gt = core.pack_gt(boxes, labels)
+        gt = core.pack_gt(boxes, labels, reuse=True)   # consumed by this call's launches only
         spec = self._spec()
         if spec.cls == L.CLS['focal'] and not self.distributed:
             # one device, no mining: the matcher and the loss pass in one C call (the matcher's
             # launches then the loss launch; ONE launch with ``one_launch``)
             loss, comps, _ = core.criterion_focal(predicted_locs, predicted_scores, gt, self.priors_cxcy,
                                                   self.priors_xy, spec, self.threshold, self.threshold - 0.1,
-                                                  two_launch=not self.one_launch)
+                                                  two_launch=not self.one_launch, fresh_match=False)
             self.last_components = comps
             return loss
         obj, ovl, npos = core.match(gt, self.priors_xy, P, self.threshold)

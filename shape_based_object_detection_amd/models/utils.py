@@ -25,7 +25,10 @@ def _cfg(config, key, default=None):
 
 
 def detect(predicted_locs, predicted_scores, min_score, max_overlap, top_k, priors_cxcy, config,
-           prior_positives_idx=None):
+           prior_positives_idx=None, async_=False):
+    """``async_=True`` (an addition; the reference has no such argument) returns a handle whose
+    ``wait()`` gives the lists: the caller can queue the next step's work before the one host sync
+    detect needs (its per-image counts)."""
     model = _cfg(config, 'model', {}) or {}
     box_type = model.get('box_type', 'offset') if isinstance(model, dict) else getattr(model, 'box_type')
     focal_type = str(_cfg(config, 'focal_type', 'softmax'))
@@ -36,7 +39,7 @@ def detect(predicted_locs, predicted_scores, min_score, max_overlap, top_k, prio
                                priors_cxcy.cpu() if priors_cxcy is not None else None, bt, act,
                                prior_positives_idx)
     return core.detect(predicted_locs, predicted_scores, min_score, max_overlap, top_k, priors_cxcy,
-                       box_type=bt, act=act, pos_mask=prior_positives_idx)
+                       box_type=bt, act=act, pos_mask=prior_positives_idx, async_=async_)
 
 
 def detect_objects(predicted_locs, predicted_scores, min_score, max_overlap, top_k, priors_cxcy,
