@@ -83,6 +83,9 @@ def parse(argv=None):
                     help='graph mode: which graph of a step is submitted first')
     ap.add_argument('--crit-form', choices=('two', 'one'), default='two',
                     help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
+    ap.add_argument('--finish', choices=('fused', 'separate'), default='fused',
+                    help='focal loss finish: in the loss pass\'s last-arriving workgroup (fused) or a separate '
+                         'one-block launch after it (same exact sum)')
     ap.add_argument('--det-form', choices=('two', 'one'), default='two',
                     help='detect: per-class NMS and per-image merge as two launches or one (k_det_nms)')
     ap.add_argument('--hw-queues', type=int, default=None,
@@ -312,7 +315,7 @@ class Step:
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
-                 crit_streams=2, depth=4, submit='direct', gt_fold=True):
+                 crit_streams=2, depth=4, submit='direct', gt_fold=True, finish='fused'):
         self.dev, self.B = dev, B
         self.gt_fold = bool(gt_fold)
         Pn = prior_table(ARCH)
@@ -323,6 +326,7 @@ class Step:
         self.crit = CR.MultiBoxLoss512(priors_cxcy=self.priors, config=self.cfg)
         self.crit.distributed = world > 1
         self.crit.one_launch = crit_form == 'one'
+        self.crit.separate_finish = finish == 'separate'
         self.det_two_pass = det_form == 'two'
         self.batches = [Batch(B, 1000 * rank + 100 * i, dev, dtype) for i in range(max(1, n_batches))]
         cap = max(int(b.shape[0]) for bt in self.batches for b in bt.boxes)
@@ -664,14 +668,14 @@ class Step:
         return self.replay() if self.graph is not None else self.eager()
 
 
-def c2_figure(dev, steps, warmup, B=16, n_batches=12, det_form='two'):
+def c2_figure(dev, steps, warmup, B=16, n_batches=12, det_form='two', finish='fused'):
     """Config C2 (SSD512 batch=16 bf16 on 1 GPU): the same captured step with bf16 locs / scores
     (and bf16 gradients) for the criterion, and the detect reading the bf16 activations directly
     (SBOD_DETECT_INPUT_BF16: widened exactly on load, no fp32 copies).  ``n_batches`` resident batches
     (~23 MB touched per step) keep the rotation above the Infinity Cache.  Algorithmic bytes of
     the criterion at 2 B/element: SURVEY §8(d) (16.56 MB at B=16)."""
     st = Step(dev, B, 0, 1, graph=True, n_batches=n_batches, dtype=torch.bfloat16, priority='detect',
-              det_form=det_form)
+              det_form=det_form, finish=finish)
     for _ in range(max(warmup - 1, 1)):
         st.eager_split()
     torch.cuda.synchronize()
@@ -858,7 +862,7 @@ def main():
     st = Step(dev, B, rank, world, graph=not a.eager, two_streams=not a.one_stream, priority=a.priority,
               n_batches=a.batches, order=a.order, det_streams=a.det_streams, crit_form=a.crit_form,
               det_form=a.det_form, crit_streams=a.crit_streams, depth=a.depth, submit=a.submit,
-              gt_fold=a.gt_fold)
+              gt_fold=a.gt_fold, finish=a.finish)
     P = st.P
     # workload constants for the algorithmic byte counts (computed before any timing; the
     # candidate count is averaged over the resident batches)
@@ -988,7 +992,7 @@ def main():
         'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams),
         'pipeline_depth': st.depth, 'submit': st.submit,
         'gt_fold': st.gt_fold if st.submit == 'direct' else None,
-        'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'criterion_form': a.crit_form, 'detect_form': a.det_form,
+        'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'criterion_form': a.crit_form, 'loss_finish': a.finish, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
         'api_ms_per_step': api['ms_per_step'] if api else None,
@@ -1024,7 +1028,7 @@ def main():
     if dp is not None:
         line['dp_train_step_with_grad_allreduce'] = dp
     if not a.no_c2 and world == 1:
-        line['c2_bf16'] = c2_figure(dev, a.steps, a.warmup, det_form=a.c2_det_form)
+        line['c2_bf16'] = c2_figure(dev, a.steps, a.warmup, det_form=a.c2_det_form, finish=a.finish)
     if not a.no_dcn:
         maps = [dcn_figure(dev, H=h, iters=5 if h >= 32 else 20) for h in (64, 32, 16, 8)]
         tot_ms = sum(m['ms'] for m in maps)

@@ -227,18 +227,20 @@ size_t sbod_loss_workspace_bytes(int B, int P);
  * holding the whole batch; the hard-negative gradients and the loss cover this rank's rows
  * (the sum over ranks is the single-device loss).  Same workspace as the deferred call. */
 enum { SBOD_LOSS_DEFER_MINING = 64 };
-/* Focal criteria (no mining pass) finish the loss inside the fused pass: the last workgroup to
- * arrive sums every workgroup's fp32 partials exactly, as 128-bit fixed-point integers (2^-64
- * resolution; a partial that is non-finite or >= 2^40 in magnitude switches the finish to a
- * double sum of the fp32 partials, as the separate finaliser computes it).  Its arrival counters
- * live in the workspace's first sbod_loss_zero_prefix_bytes() bytes, which must be zero on entry
- * and are left zero by every successful call (any B, P).  A caller that knows the workspace is clean (a previous successful
- * call on it) passes SBOD_LOSS_WS_ZEROED and the call issues no memset (hipGraph capture);
- * without it the call zeroes them first (one hipMemsetAsync).  SBOD_LOSS_UNFUSED_FINISH
- * (diagnostics, tests) finishes a focal criterion with the separate finaliser launch instead
- * (per-workgroup partials summed in double). */
+/* Focal criteria (no mining pass) finish the loss inside the fused pass: every workgroup
+ * publishes its fp32 partials as one tagged 16-byte record and the grid's last workgroup sums
+ * all of them exactly, as 128-bit fixed-point integers (2^-64 resolution; a partial that is
+ * non-finite or >= 2^40 in magnitude switches the finish to a double sum of the fp32 partials in
+ * record order, as the separate finaliser computes it).  The finish's state — an epoch word and
+ * the records — is the workspace's first sbod_loss_zero_bytes(B, P) bytes: zero on entry, or as a
+ * previous successful call with the same B and P (fused or not) left them.  A caller that knows
+ * that passes SBOD_LOSS_WS_ZEROED and the call issues no memset (hipGraph capture); without it the
+ * call zeroes them first (one hipMemsetAsync).  A finish whose wait for the records timed out
+ * (2 s: a hardware fault) makes this and every later loss on the workspace NaN until it is zeroed.
+ * SBOD_LOSS_UNFUSED_FINISH finishes a focal criterion with the separate one-block finaliser
+ * launch instead (the same exact sum: the same loss bit for bit). */
 enum { SBOD_LOSS_WS_ZEROED = 128, SBOD_LOSS_UNFUSED_FINISH = 512 };
-size_t sbod_loss_zero_prefix_bytes(void);
+size_t sbod_loss_zero_bytes(int B, int P);
 size_t sbod_loss_pool_offset(int B, int P);
 int sbod_multibox_mine_global(const void *scores, int dtype, int B, int P, int C,
                               const int32_t *npos_total, int reg, int cls, int flags,
@@ -273,8 +275,9 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
  * DESIGN.md round 4); the product library always runs the two launches.  Data parallelism (a
  * normaliser all-reduced between the matcher and the loss) uses the two calls.
  * Workspace: sbod_criterion_workspace_bytes(B, Gmax, P); its first
- * sbod_criterion_zero_bytes(B, Gmax, P) bytes must be zero on entry and are left zero by every
- * successful call: pass SBOD_CRIT_WS_ZEROED when they are (else the call zeroes them, one
+ * sbod_criterion_zero_bytes(B, Gmax, P) bytes must be zero on entry, or as a previous successful
+ * call with the same B, Gmax and P left them (the loss finish's epoch word and records, as for
+ * sbod_multibox_loss): pass SBOD_CRIT_WS_ZEROED when they are (else the call zeroes them, one
  * hipMemsetAsync).  flags: SBOD_LOSS_FOCAL_NORM, SBOD_CRIT_WS_ZEROED, SBOD_CRIT_TWO_LAUNCH,
  * SBOD_LOSS_UNFUSED_FINISH.  sbod_criterion_status() (diagnostics, synchronises the stream) reads
  * the sticky word the one-launch form sets if a bounded in-launch wait ever gave up (that call's

@@ -96,7 +96,8 @@ def run(label, B, dtype, reps=6):
     dev = torch.device('cuda', 0)
     lib = L.lib()
     for n, a in (('sbod_debug_stamps_loss', [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
-                 ('sbod_debug_mb_marks', [ctypes.c_void_p, ctypes.c_int])):
+                 ('sbod_debug_mb_marks', [ctypes.c_void_p, ctypes.c_int]),
+                 ('sbod_debug_fin_marks', [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p])):
         getattr(lib, n).argtypes = a
     st = BM.Step(dev, B, 0, 1, graph=False, n_batches=6, dtype=dtype, priority='detect')
     P = st.P
@@ -105,18 +106,37 @@ def run(label, B, dtype, reps=6):
     for _ in range(6):
         st.eager_half('criterion')
     torch.cuda.synchronize()
-    rows, spans = [], []
+    rows, spans, fins = [], [], []
     for r in range(reps):
         lib.sbod_debug_stamps_loss(1 << KID, None, 0)
         lib.sbod_debug_mb_marks(None, 0)
+        lib.sbod_debug_fin_marks(None, 0, None)
         st.eager_half('criterion')
         torch.cuda.synchronize()
         bt = st.batches[(st.k - 1) % len(st.batches)]
         start, end, hw, marks = read(lib, nblk)
+        seen = (ctypes.c_ulonglong * REG)()
+        fm = (ctypes.c_ulonglong * 8)()
+        lib.sbod_debug_fin_marks(seen, REG, fm)
+        seen = np.frombuffer(seen, dtype=np.uint64)[:nblk].astype(np.int64)
+        fm = np.frombuffer(fm, dtype=np.uint64).astype(np.int64)
         lib.sbod_debug_stamps_loss(0, None, 0)
         pos, neg, nrow = tile_stats(st, bt, P)
         t0 = start.min()
         spans.append(round((end.max() - t0) / 100.0, 2))
+        if fm[0]:
+            # the fused finish: when each record was published (its block's mark 7, after the
+            # record store) and when the gatherer first saw it
+            pub = marks[:, 7]
+            lag = (seen - pub) / 100.0
+            last = int(np.argmax(pub))
+            fins.append({'rep': r, 'enter_us': (fm[0] - t0) / 100.0, 'first_sweep_us': (fm[1] - t0) / 100.0,
+                         'all_folded_us': (fm[2] - t0) / 100.0, 'written_us': (fm[3] - t0) / 100.0,
+                         'sweeps_t0': int(fm[4]), 'last_pub_us': (pub.max() - t0) / 100.0,
+                         'last_seen_us': (seen.max() - t0) / 100.0,
+                         'lag_p50_p90_max_us': [round(float(np.percentile(lag, q)), 2) for q in (50, 90, 100)],
+                         'lag_of_last_published_us': round(float(lag[last]), 2),
+                         'kernel_end_us': (end.max() - t0) / 100.0})
         cu_count = {}
         for h in hw:
             cu_count[int(h)] = cu_count.get(int(h), 0) + 1
@@ -131,7 +151,7 @@ def run(label, B, dtype, reps=6):
                          'se': int((hw[i] >> 4) & 0x3), 'xcd': int(hw[i] >> 6), 'per_cu': cu_count[int(hw[i])],
                          'commit_us': rel(m[0]), 'plist_us': rel(m[1]), 'regress_us': rel(m[2]),
                          'rows_w0_us': w[0], 'rows_w123_us': float(np.nanmax(w[1:])), 'store_us': rel(m[7])})
-    res = {'label': label, 'B': B, 'spans_us': spans, 'analysis': analyse(rows)}
+    res = {'label': label, 'B': B, 'spans_us': spans, 'finish': fins, 'analysis': analyse(rows)}
     print(json.dumps(res), flush=True)
     del st
     torch.cuda.synchronize()

@@ -41,7 +41,7 @@ SIGNATURES = {
     'sbod_multibox_loss': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, P, F32, F32,
                                  F32, I32, I32, I32, I32, F32, F32, F32, P, P, P, P, SZ, P]),
     'sbod_loss_pool_offset': (SZ, [I32, I32]),
-    'sbod_loss_zero_prefix_bytes': (SZ, []),
+    'sbod_loss_zero_bytes': (SZ, [I32, I32]),
     'sbod_criterion_workspace_bytes': (SZ, [I32, I32, I32]),
     'sbod_criterion_zero_bytes': (SZ, [I32, I32, I32]),
     'sbod_criterion_focal': (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32, I32, F32, F32, F32,

@@ -343,7 +343,7 @@ def match(gt, anchors, P, threshold=0.5, flags=0, priors_cxcy=None, arm_scores=N
            L.ptr(anchors.contiguous()), L.ptr(priors_cxcy), L.ptr(arm_scores), P, float(threshold),
            float(theta), int(flags) | zflag, L.ptr(obj), L.ptr(ovl), L.ptr(npos), L.ptr(ws), nb,
            L.stream_of(anchors))
-    _CLEAN[ws.data_ptr()] = nb
+    _CLEAN[ws.data_ptr()] = (nb, None)
     return obj, ovl, npos
 
 
@@ -474,7 +474,7 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
         ws = workspace(nb, dev, 'loss')
         flags = spec.flags | (L.LOSS_DEFER_MINING if exchange is not None else 0)
         # the fused finish's accumulators are left zero by every successful call
-        zprefix = _loss_zero_prefix()
+        zprefix = _loss_zero_bytes(B, P)
         zflag = _zeroed_flag(ws, zprefix, L.LOSS_WS_ZEROED, 'criterion')
         _CLEAN.pop(ws.data_ptr(), None)
         L.call('sbod_multibox_loss', L.ptr(locs), L.ptr(scores), dt, B, P, C, L.ptr(priors_cxcy),
@@ -483,7 +483,7 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
                float(threshold), float(neg_threshold), float(theta), spec.reg, spec.cls, flags | zflag,
                int(spec.neg_pos_ratio), float(spec.reg_weight), float(spec.alpha), float(spec.gamma),
                L.ptr(gl), L.ptr(gs), L.ptr(out), L.ptr(ws), nb, stream)
-        _CLEAN[ws.data_ptr()] = zprefix   # (only the accumulator prefix is zero)
+        _CLEAN[ws.data_ptr()] = (zprefix, None)   # (only the finish's state is known clean)
         if exchange is not None:
             off = L.lib().sbod_loss_pool_offset(B, P)
             pool = ws.narrow(0, off, 4 * B * P).view(torch.float32)
@@ -565,7 +565,7 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
         gs = torch.empty_like(scores) if want_grad else None
         ws = workspace(nb, dev, 'criterion')
         wp = ws.data_ptr()
-        zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion')
+        zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion', (B, gmax, P))
         _CLEAN.pop(wp, None)
         flags = ((spec.flags & (L.LOSS_FOCAL_NORM | L.LOSS_UNFUSED_FINISH)) | zflag |
                  (L.CRIT_TWO_LAUNCH if two_launch else 0))
@@ -574,7 +574,7 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
                float(threshold), float(neg_threshold), spec.reg, flags, float(spec.reg_weight), float(spec.alpha),
                float(spec.gamma), obj.data_ptr(), ovl.data_ptr(), npos.data_ptr(), L.ptr(gl), L.ptr(gs),
                out.data_ptr(), wp, nb, stream)
-        _CLEAN[wp] = zb   # (only the zero-on-entry prefix is known clean)
+        _CLEAN[wp] = (zb, (B, gmax, P))   # (only the zero-on-entry prefix, for this layout)
         return out, gl, gs
 
     want = torch.is_grad_enabled() and (locs.requires_grad or scores.requires_grad)
@@ -746,19 +746,23 @@ def _count_slot(dev, B):
 # leaves its candidate counters zero, so after the first call on a workspace no memset is
 # needed — none in a captured graph (SBOD_DETECT_COUNTERS_ZEROED).
 _CLEAN = {}
-_LOSS_ZERO_PREFIX = []     # sbod_loss_zero_prefix_bytes(): the fused finish's accumulators (queried once)
+_LOSS_ZERO = {}     # (B, P) -> sbod_loss_zero_bytes: the fused finish's epoch word and records
 
 
-def _loss_zero_prefix():
-    if not _LOSS_ZERO_PREFIX:
-        _LOSS_ZERO_PREFIX.append(int(L.lib().sbod_loss_zero_prefix_bytes()))
-    return _LOSS_ZERO_PREFIX[0]
+def _loss_zero_bytes(B, P):
+    z = _LOSS_ZERO.get((B, P))
+    if z is None:
+        z = _LOSS_ZERO[(B, P)] = int(L.lib().sbod_loss_zero_bytes(B, P))
+    return z
 
 
-def _zeroed_flag(ws, need, flag, what):
-    """``flag`` when the first ``need`` bytes of ``ws`` are known zero, else 0 (the call zeroes
-    them itself: a memset, which must not be captured)."""
-    if _CLEAN.get(ws.data_ptr(), 0) >= need:
+def _zeroed_flag(ws, need, flag, what, layout=None):
+    """``flag`` when the first ``need`` bytes of ``ws`` are known clean, else 0 (the call zeroes
+    them itself: a memset, which must not be captured).  ``layout``: the clean state is only valid
+    for a call whose workspace layout key matches the last successful call's (the criterion's
+    loss-finish state sits at a shape-dependent offset and is not all-zero between calls)."""
+    ent = _CLEAN.get(ws.data_ptr())
+    if ent is not None and ent[0] >= need and (layout is None or ent[1] == layout):
         return flag
     if torch.cuda.is_current_stream_capturing():
         raise L.SbodError('%s under hipGraph capture: run it once on the capture stream with this '
@@ -799,7 +803,7 @@ def _detect_launch(lc, sc, B, P, C, pri, pm, box_type, act, min_score, max_overl
            L.ptr(dbg[1]), L.ptr(ws), nb, L.stream_of(sc))
     # only this call's prefix is known clean: a call with a smaller B * C writes other regions
     # over the rest of a larger one's counters
-    _CLEAN[ws.data_ptr()] = need
+    _CLEAN[ws.data_ptr()] = (need, None)
 
 
 # The per-class NMS and the per-image merge as two launches (k_det_segment_w4, k_det_merge with

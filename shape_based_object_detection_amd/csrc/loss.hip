@@ -39,8 +39,22 @@ static __device__ unsigned long long g_mb_marks[SBOD_STAMP_REGION * 8];
       if (_b < SBOD_STAMP_REGION) g_mb_marks[_b * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     }                                                                                         \
   } while (0)
+// the fused finish's gatherer: when it first saw each record, and its own marks (0 entered,
+// 1 thread 0's first sweep done, 2 every record folded, 3 loss written; 4 thread 0's sweeps)
+static __device__ unsigned long long g_fin_seen[SBOD_STAMP_REGION];
+static __device__ unsigned long long g_fin_marks[8];
+#define FIN_SEEN(i)                                                                                 \
+  do {                                                                                              \
+    if ((g_stamp_armed & (1 << 4)) && (i) < SBOD_STAMP_REGION) g_fin_seen[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define FIN_MARK(slot, v)                                      \
+  do {                                                         \
+    if ((g_stamp_armed & (1 << 4))) g_fin_marks[slot] = (v);   \
+  } while (0)
 #else
 #define MB_MARK(slot, cond) do { } while (0)
+#define FIN_SEEN(i) do { } while (0)
+#define FIN_MARK(slot, v) do { } while (0)
 #endif
 
 constexpr int kLTile = 256;
@@ -371,6 +385,7 @@ struct LossArgs {
   unsigned *status;           // nonzero: a wait gave up (see kSpinLimit)
   unsigned long long *forced; // [B][Gmax] (prior << 32 | object) rewritten by the forced match
   int32_t *nforced;           // [B]
+  void *recs;                 // fused finish: [nblk] 16-byte records {conf, tag, loc, tag}
 };
 
 // The fused finish of k_multibox (focal / no mining).  Each workgroup folds its partial sums
@@ -475,82 +490,85 @@ __device__ __forceinline__ void block_sum2(float &x, float &y, float *scratch /*
   y = sy;
 }
 
-// The fused finish of k_multibox (focal criteria, no mining pass), in two parts so that the
-// workgroup's arrival travels while its gradient tile is stored:
-//   loss_arrive (wave 0, before the tile store): the workgroup's fp32 partials {conf, loc} are
-//     written through (one 8-byte sc1 store), drained, and the workgroup counts itself in at its
-//     group (32 group counters, blk mod 32: same-address atomics serialise at the memory side,
-//     ~10 ns each);
-//   loss_complete (wave 0, after waves 1-3 issued the tile store): the group's last arriver
-//     counts the group in at the top counter, and the top's last arriver reads every workgroup's
-//     partials (sc1 loads) and sums them EXACTLY: each fp32 partial as a 128-bit fixed-point
-//     integer (value * 2^64, two's complement), added lane by lane and across the wave — integer
-//     adds, so the total is the same in any order and bitwise reproducible, with a resolution of
-//     2^-64 per partial (a loss total of 1e-12 keeps 1e-7 relative).  A partial of magnitude
-//     >= 2^40 or a non-finite one cannot be folded exactly: then the double sum of the partials
-//     (lane-strided, xor tree) is the result, as k_loss_final computes it — never silently wrong
-//     (a NaN row of the focal loss, the reference's 0 * log 0, makes a NaN loss that way).
-// Counters are left zero by their last arrivers (SBOD_LOSS_WS_ZEROED).  Every hand-off moves
-// through memory-side atomics or sc1 stores / loads, so no cache write-back or invalidation is
-// needed between the XCDs.  (Round 4's form folded each partial into group accumulators by
-// returning atomics before the arrival and moved each group's total up a level: four dependent
-// far-memory round trips after the tile store, 3-4.8 us of the last workgroups' 18 us span,
+// The fused finish of k_multibox (focal criteria, no mining pass): no counters.  Every
+// workgroup publishes its fp32 partials as ONE 16-byte write-through record {conf, tag, loc, tag}
+// — two 8-byte granules {value, tag}, each validating itself (MI355X_MICROARCH.md inter-workgroup
+// visibility, the data-is-the-flag form) — and retires; the grid's last workgroup (linear id
+// nblk - 1: dispatched last, so every other workgroup is already resident or done, and it is the
+// only one that waits: no co-residency assumption, nothing can starve it) stores its own tile,
+// then sweeps every record with 16-byte sc1 loads until each carries this call's tag, folding each
+// the first time it is seen, EXACTLY: each fp32 partial as a 128-bit fixed-point integer (value *
+// 2^64, two's complement), integer adds — the total is the same in any order, bitwise
+// reproducible, with a resolution of 2^-64 per partial (a loss total of 1e-12 keeps 1e-7
+// relative).  A partial of magnitude >= 2^40 or a non-finite one cannot be folded exactly: then
+// the double sum of all partials in record order (a second, ordered pass) is the result, as
+// k_loss_final computes it — never silently wrong (a NaN row of the focal loss, the reference's
+// 0 * log 0, makes a NaN loss that way).
+// Tags: the call's epoch word E (read by every workgroup at its start; written only by the
+// finisher, after it has seen every record of the call) gives tag E + 1 (never 0); records left
+// by earlier calls carry tags <= E, and a zeroed workspace holds E = 0 and tags 0
+// (sbod_loss_zero_bytes: the epoch word and the records are the zero-on-entry prefix).  The
+// finisher's wait is bounded (kGatherTicks of the 100 MHz clock): a timeout — a hardware fault,
+// never a schedule — makes this and every later call's loss NaN (a sticky word, cleared only by
+// the zeroing memset), since a record landing after it could carry a later call's tag.
+// Critical path after the last record is issued: its write landing + one sweep + the fold.
+// (Rounds 4-5a counted arrivals on 32 group counters and a top counter: a drain, two dependent
+// far-memory atomics and the partials read after the last tile, 3.6-4.5 us of an 18 us launch,
 // scripts/mb_imbalance.py.)
-__device__ __forceinline__ unsigned long long loss_arrive(const LossArgs &a, float conf_l, float loc_l, unsigned nblk,
-                                                          unsigned blk) {
-  const unsigned ng = nblk < kFinGroups ? nblk : kFinGroups;
-  unsigned long long old = 0ull;
-  if ((threadIdx.x & 63) == 0) {
-    st_wt_u64(reinterpret_cast<unsigned long long *>(a.partials) + blk,
-              (static_cast<unsigned long long>(__float_as_uint(loc_l)) << 32) | __float_as_uint(conf_l));
-    drain_vm();   // the partials written through before the count
-    old = __hip_atomic_fetch_add(a.fin + kFinStride * (blk % ng) + kFinArrive, 1ull, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return old;
+constexpr int kFinEpoch = kFinStride * kFinGroups + 8;    // u64 word index in the fin region
+constexpr int kFinSticky = kFinStride * kFinGroups + 9;
+constexpr unsigned long long kGatherTicks = 200000000ull;   // 2 s
+__device__ __forceinline__ unsigned loss_tag(unsigned epoch) { return epoch + 1u ? epoch + 1u : 1u; }
+// One lane: the workgroup's record, written through.
+__device__ __forceinline__ void loss_publish(const LossArgs &a, float conf_l, float loc_l, unsigned tag, unsigned nblk,
+                                             unsigned blk) {
+  const u32x4_t v = {__float_as_uint(conf_l), tag, __float_as_uint(loc_l), tag};
+  st_wt_b128(a.recs, nblk * 16u, blk * 16u, v);
 }
-// Wave 0: the group's last arriver counts the group in at the top counter (leaving its group
-// counter zero).  Returns 1 (uniform) in the workgroup that completes the top: every workgroup's
-// partials are then written through and it runs loss_sum_all.
-__device__ int loss_climb(const LossArgs &a, unsigned long long ticket, unsigned nblk, unsigned blk) {
-  const int lane = threadIdx.x & 63;
-  const unsigned ng = nblk < kFinGroups ? nblk : kFinGroups, g = blk % ng;
-  const unsigned in_group = (nblk - g + ng - 1) / ng;
-  unsigned long long *top = a.fin + kFinStride * kFinGroups + kFinArrive;
-  int last = 0;
-  if (lane == 0 && ticket == in_group - 1) {   // the group is complete: count it in at the top
-    __hip_atomic_store(a.fin + kFinStride * g + kFinArrive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = __hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-    if (last) __hip_atomic_store(top, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return __builtin_amdgcn_readfirstlane(last);
-}
-// The whole workgroup (the top's last arriver): every workgroup's partials by 16-byte sc1 buffer
-// loads (two workgroups' partials each, four loads in flight per thread: one memory round trip up
-// to 2,048 workgroups; reads past the last partial return zero through the buffer's range check),
-// folded exactly per thread, across the wave and across the four waves; thread 0 writes the loss.
-__device__ void loss_sum_all(const LossArgs &a, unsigned nblk, float n, float *out, unsigned long long *s_fx) {
+// The whole workgroup (the finisher): every record of this call, folded exactly; thread 0 writes
+// the loss and the next epoch.
+__device__ void loss_gather(const LossArgs &a, unsigned nblk, unsigned tag, float n, float *out,
+                            unsigned long long *s_fx, double *s_red) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.partials, static_cast<short>(0), static_cast<int>(nblk * 8u),
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.recs, static_cast<short>(0), static_cast<int>(nblk * 16u),
                                                     0x00020000);
+  constexpr int kB = 8;   // records per thread per sweep: 2,048 workgroups in one batch
+  const unsigned nk = (nblk + kLTile - 1u) / kLTile;
   Fx128 fc{0ull, 0ull}, fl{0ull, 0ull};
-  bool ok = true;
-  constexpr int kB = 3;
-  const unsigned npair = (nblk + 1u) / 2u;
-  for (unsigned q0 = 0; q0 < npair; q0 += kB * kLTile) {
-    u32x4_t w[kB];
+  bool ok = true, late = false;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) FIN_MARK(0, t0);
+  unsigned sweeps = 0;
+  for (unsigned k0 = 0; k0 < nk && !late; k0 += kB) {
+    unsigned pend = 0;
 #pragma unroll
     for (int k = 0; k < kB; ++k)
-      w[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>((q0 + k * kLTile + tid) * 16u), 0, kCpolSc1);
+      if ((k0 + k) * kLTile + tid < nblk) pend |= 1u << k;
+    while (pend != 0u) {
+      u32x4_t w[kB];
 #pragma unroll
-    for (int k = 0; k < kB; ++k) {
+      for (int k = 0; k < kB; ++k)   // past the last record: zero through the range check
+        w[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(((k0 + k) * kLTile + tid) * 16u), 0, kCpolSc1);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float c = __uint_as_float(w[k][2 * h]), l = __uint_as_float(w[k][2 * h + 1]);
-        const bool f = fx_foldable(c) && fx_foldable(l);
-        ok = ok && f;
-        fc = fx128_add(fc, to_fx128(f ? c : 0.f));
-        fl = fx128_add(fl, to_fx128(f ? l : 0.f));
+      for (int k = 0; k < kB; ++k) {
+        if (((pend >> k) & 1u) && w[k][1] == tag && w[k][3] == tag) {
+          const float c = __uint_as_float(w[k][0]), l = __uint_as_float(w[k][2]);
+          const bool f = fx_foldable(c) && fx_foldable(l);
+          ok = ok && f;
+          fc = fx128_add(fc, to_fx128(f ? c : 0.f));
+          fl = fx128_add(fl, to_fx128(f ? l : 0.f));
+          pend &= ~(1u << k);
+          FIN_SEEN((k0 + k) * kLTile + tid);
+        }
+      }
+      ++sweeps;
+      if (tid == 0 && sweeps == 1) FIN_MARK(1, __builtin_amdgcn_s_memrealtime());
+      if (pend != 0u) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kGatherTicks) {
+          late = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
     }
   }
@@ -559,43 +577,52 @@ __device__ void loss_sum_all(const LossArgs &a, unsigned nblk, float n, float *o
     fc = fx128_add(fc, Fx128{shfl_xor_u64(fc.lo, m), shfl_xor_u64(fc.hi, m)});
     fl = fx128_add(fl, Fx128{shfl_xor_u64(fl.lo, m), shfl_xor_u64(fl.hi, m)});
   }
-  const bool wave_ok = __ballot(!ok) == 0ull;
+  const bool wave_ok = __ballot(!ok) == 0ull, wave_late = __ballot(late) != 0ull;
   if (lane == 0) {
     s_fx[5 * wv + 0] = fc.lo;
     s_fx[5 * wv + 1] = fc.hi;
     s_fx[5 * wv + 2] = fl.lo;
     s_fx[5 * wv + 3] = fl.hi;
-    s_fx[5 * wv + 4] = wave_ok ? 1ull : 0ull;
+    s_fx[5 * wv + 4] = (wave_ok ? 1ull : 0ull) | (wave_late ? 2ull : 0ull);
   }
   __syncthreads();
-  if (wv != 0) return;
-  bool all_ok = true;
+  if (tid == 0) {
+    FIN_MARK(2, __builtin_amdgcn_s_memrealtime());
+    FIN_MARK(4, sweeps);
+  }
+  bool all_ok = true, any_late = false;
   fc = Fx128{0ull, 0ull};
   fl = Fx128{0ull, 0ull};
   for (int w2 = 0; w2 < kLTile / 64; ++w2) {
     fc = fx128_add(fc, Fx128{s_fx[5 * w2 + 0], s_fx[5 * w2 + 1]});
     fl = fx128_add(fl, Fx128{s_fx[5 * w2 + 2], s_fx[5 * w2 + 3]});
-    all_ok = all_ok && s_fx[5 * w2 + 4] != 0ull;
+    all_ok = all_ok && (s_fx[5 * w2 + 4] & 1ull) != 0ull;
+    any_late = any_late || (s_fx[5 * w2 + 4] & 2ull) != 0ull;
   }
   double c = fx128_value(fc.lo, fc.hi), l = fx128_value(fl.lo, fl.hi);
-  if (!all_ok) {
-    // a non-finite or huge partial: the double sum of every workgroup's fp32 partials, as
-    // k_loss_final computes it (lane-strided, then the xor tree)
+  if (!all_ok && !any_late) {
+    // a non-finite or huge partial: the double sum of every workgroup's fp32 partials in record
+    // order (thread-strided, then the block tree: the same order every call)
     c = 0.0;
     l = 0.0;
-    const unsigned long long *pp = reinterpret_cast<const unsigned long long *>(a.partials);
-    for (unsigned i = lane; i < nblk; i += 64) {
-      const unsigned long long w = ld_wt_u64(pp + i);
-      c += static_cast<double>(__uint_as_float(static_cast<uint32_t>(w)));
-      l += static_cast<double>(__uint_as_float(static_cast<uint32_t>(w >> 32)));
+    for (unsigned i = tid; i < nblk; i += kLTile) {
+      const u32x4_t w = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(i * 16u), 0, kCpolSc1);
+      c += static_cast<double>(__uint_as_float(w[0]));
+      l += static_cast<double>(__uint_as_float(w[2]));
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      c += __shfl_xor(c, m, 64);
-      l += __shfl_xor(l, m, 64);
-    }
+    __syncthreads();
+    c = block_sum(c, s_red);
+    __syncthreads();
+    l = block_sum(l, s_red);
   }
-  if (lane == 0) loss_outputs(c, l, n, a.reg, a.cls, a.flags, a.reg_weight, out);
+  if (tid == 0) {
+    unsigned long long *fin = a.fin;
+    if (any_late) st_wt_u64(fin + kFinSticky, 1ull);
+    if (any_late || ld_wt_u64(fin + kFinSticky) != 0ull) c = l = __builtin_nan("");
+    loss_outputs(c, l, n, a.reg, a.cls, a.flags, a.reg_weight, out);
+    st_wt_u64(fin + kFinEpoch, tag);   // the next call's epoch: every record of this one is in
+    FIN_MARK(3, __builtin_amdgcn_s_memrealtime());
+  }
 }
 
 #ifdef SBOD_VARIANT_ONE_LAUNCH
@@ -1043,6 +1070,7 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   const bool fast = fast_tile<T, NB>(tsrc, np * C);
   int objv, offb;
   float v, n;
+  unsigned epoch = 0;   // the fused finish's epoch (loss_gather)
   int64_t labg;
   RegIn rg;
   typename TileVec<T>::V tr[NB > 0 ? NB : 1];
@@ -1149,6 +1177,7 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     if constexpr (NB > 0 && sizeof(T) != 4)
       if (fast) tile_commit(s_sc, tr, np * C);
     n = static_cast<float>(*a.npos_total);
+    if (a.fin != nullptr) epoch = static_cast<unsigned>(ld_wt_u64(a.fin + kFinEpoch));
     MB_MARK(0, tid == 0);
   }
   SEG_PHASE(1);
@@ -1170,20 +1199,18 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   SEG_PHASE(2);
   const unsigned nblk = gridDim.x * gridDim.y, blk = blockIdx.x + gridDim.x * blockIdx.y;
   if (a.fin != nullptr && !kFused) {
-    // the fused finish (focal): the block sums first, so wave 0's arrival is in flight while
-    // waves 1-3 store the gradient tile
+    // the fused finish (focal): this workgroup's record, its tile, and in the grid's last
+    // workgroup the gather of every record
     block_sum2(conf_l, loc_l, s_red);
-    unsigned long long ticket = 0;
-    if (tid < 64) ticket = loss_arrive(a, conf_l, loc_l, nblk, blk);
-    if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 64, kLTile - 64);
+    const unsigned tag = loss_tag(epoch);
+    if (tid == 0) loss_publish(a, conf_l, loc_l, tag, nblk, blk);
+    if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
     MB_MARK(7, tid == 0);
-    __shared__ int s_last;
-    if (tid < 64) {
-      const int last = loss_climb(a, ticket, nblk, blk);
-      if (tid == 0) s_last = last;
+    if (blk == nblk - 1u) {
+      __syncthreads();   // the tile's LDS reads done: the gather's scratch reuses it
+      loss_gather(a, nblk, tag, n, a.out, reinterpret_cast<unsigned long long *>(s_sc),
+                  reinterpret_cast<double *>(s_sc) + 32);
     }
-    __syncthreads();
-    if (s_last) loss_sum_all(a, nblk, n, a.out, reinterpret_cast<unsigned long long *>(s_sc));
   } else {
     if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
     block_sum2(conf_l, loc_l, s_red);
@@ -1348,6 +1375,10 @@ __global__ __launch_bounds__(kHBlock) void k_hnm(const float *__restrict__ pool,
   if (tid == 0) hnm_sum[seg] = sum;
 }
 
+// The separate finaliser (CE criteria after the mining pass, or a focal criterion with
+// SBOD_LOSS_UNFUSED_FINISH): one block sums every workgroup's fp32 partials and the mining
+// segments' sums EXACTLY (128-bit fixed point, as the fused finish: the same loss bit for bit
+// whichever finish ran), falling back to a double sum when a value cannot be folded.
 __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ partials, int nparts,
                                                     const float *__restrict__ hnm, int nseg,
                                                     const int32_t *__restrict__ npos_total, int reg,
@@ -1355,16 +1386,59 @@ __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ pa
                                                     float *__restrict__ out) {
   STAMP_BEGIN();
   __shared__ double s_red[16];
-  double c = 0.0, l = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
-    c += partials[2 * i];
-    l += partials[2 * i + 1];
+  __shared__ unsigned long long s_fx[5 * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  Fx128 fc{0ull, 0ull}, fl{0ull, 0ull};
+  bool ok = true;
+  for (int i = tid; i < nparts; i += blockDim.x) {
+    const float2 v = reinterpret_cast<const float2 *>(partials)[i];
+    const bool f = fx_foldable(v.x) && fx_foldable(v.y);
+    ok = ok && f;
+    fc = fx128_add(fc, to_fx128(f ? v.x : 0.f));
+    fl = fx128_add(fl, to_fx128(f ? v.y : 0.f));
   }
-  for (int i = threadIdx.x; i < nseg; i += blockDim.x) c += hnm[i];
-  c = block_sum(c, s_red);
+  for (int i = tid; i < nseg; i += blockDim.x) {
+    const float v = hnm[i];
+    const bool f = fx_foldable(v);
+    ok = ok && f;
+    fc = fx128_add(fc, to_fx128(f ? v : 0.f));
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    fc = fx128_add(fc, Fx128{shfl_xor_u64(fc.lo, m), shfl_xor_u64(fc.hi, m)});
+    fl = fx128_add(fl, Fx128{shfl_xor_u64(fl.lo, m), shfl_xor_u64(fl.hi, m)});
+  }
+  const bool wave_ok = __ballot(!ok) == 0ull;
+  if (lane == 0) {
+    s_fx[5 * wv + 0] = fc.lo;
+    s_fx[5 * wv + 1] = fc.hi;
+    s_fx[5 * wv + 2] = fl.lo;
+    s_fx[5 * wv + 3] = fl.hi;
+    s_fx[5 * wv + 4] = wave_ok ? 1ull : 0ull;
+  }
   __syncthreads();
-  l = block_sum(l, s_red);
-  if (threadIdx.x == 0) loss_outputs(c, l, static_cast<float>(*npos_total), reg, cls, flags, reg_weight, out);
+  bool all_ok = true;
+  fc = Fx128{0ull, 0ull};
+  fl = Fx128{0ull, 0ull};
+  for (int w2 = 0; w2 < static_cast<int>(blockDim.x >> 6); ++w2) {
+    fc = fx128_add(fc, Fx128{s_fx[5 * w2 + 0], s_fx[5 * w2 + 1]});
+    fl = fx128_add(fl, Fx128{s_fx[5 * w2 + 2], s_fx[5 * w2 + 3]});
+    all_ok = all_ok && s_fx[5 * w2 + 4] != 0ull;
+  }
+  double c = fx128_value(fc.lo, fc.hi), l = fx128_value(fl.lo, fl.hi);
+  if (!all_ok) {   // a non-finite or huge value: the double sum
+    c = 0.0;
+    l = 0.0;
+    for (int i = tid; i < nparts; i += blockDim.x) {
+      c += partials[2 * i];
+      l += partials[2 * i + 1];
+    }
+    for (int i = tid; i < nseg; i += blockDim.x) c += hnm[i];
+    c = block_sum(c, s_red);
+    __syncthreads();
+    l = block_sum(l, s_red);
+  }
+  if (tid == 0) loss_outputs(c, l, static_cast<float>(*npos_total), reg, cls, flags, reg_weight, out);
   STAMP_END(6, 1);
 }
 
@@ -1471,16 +1545,21 @@ namespace {
 struct LossWs {
   float *partials, *pool, *hnm;
   unsigned long long *fin;
-  size_t pool_off;   // byte offset of `pool` (sbod_loss_pool_offset)
+  void *recs;
+  size_t pool_off;     // byte offset of `pool` (sbod_loss_pool_offset)
+  size_t zero_bytes;   // the fused finish's state: epoch word (in `fin`) and records
   size_t bytes;
 };
 LossWs carve(void *w, int B, int P) {
   const size_t nblk = static_cast<size_t>(B) * ((P + kLTile - 1) / kLTile);
   LossWs r;
-  // the fused finish's accumulators first: a fixed prefix whatever B and P are, so "the first
-  // 32 bytes are zero" (SBOD_LOSS_WS_ZEROED) carries over between calls of different shapes
+  // the fused finish's state first (zero on entry, SBOD_LOSS_WS_ZEROED): its words, then one
+  // record per workgroup; no other pass writes them
   r.fin = ws_at<unsigned long long>(w, 0);
   size_t o = align_up(kFinBytes);
+  r.recs = ws_at<char>(w, o);
+  o += align_up(nblk * 16);
+  r.zero_bytes = o;
   r.partials = ws_at<float>(w, o);
   o += align_up(nblk * 2 * sizeof(float));
   r.pool = ws_at<float>(w, o);
@@ -1548,8 +1627,9 @@ CritWs carve_crit(void *w, int B, int Gmax, int P) {
   r.match_bytes = sbod_match_workspace_bytes_p(B, Gmax, P);
   o += align_up(r.match_bytes);
   r.loss_ws = ws_at<char>(w, o);
-  r.loss_bytes = carve(nullptr, B, P).bytes;
-  r.zero_bytes = o + kFinBytes;
+  const LossWs lw = carve(nullptr, B, P);
+  r.loss_bytes = lw.bytes;
+  r.zero_bytes = o + lw.zero_bytes;
   o += align_up(r.loss_bytes);
   r.forced = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * Gmax * 8);
@@ -1784,18 +1864,19 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
     return SBOD_E_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
-  // no mining pass (focal): the fused pass finishes the loss itself (multibox_finish), so the
-  // step has no k_loss_final launch; its accumulators are zero on entry (SBOD_LOSS_WS_ZEROED)
-  // (every call without the flag zeroes them, fused or not: a caller marks the workspace clean
-  // after ANY successful call, and a mining-path call never touches them)
+  // no mining pass (focal): the fused pass finishes the loss itself (loss_gather), so the step
+  // has no k_loss_final launch; its state (epoch word, records) is zero on entry or as a previous
+  // call of the same shape left it (SBOD_LOSS_WS_ZEROED); every call without the flag zeroes
+  // it, fused or not, and a mining-path call of the same shape never touches it
   const bool fused = cls == SBOD_CLS_FOCAL && !(flags & (SBOD_LOSS_DEFER_MINING | SBOD_LOSS_UNFUSED_FINISH));
   if ((flags & SBOD_LOSS_WS_ZEROED) == 0 &&
-      hipMemsetAsync(ws.fin, 0, kFinBytes, s) != hipSuccess)
+      hipMemsetAsync(ws.fin, 0, ws.zero_bytes, s) != hipSuccess)
     return launch_status("hipMemsetAsync(loss)");
   LossArgs a{B, P, C, priors_cxcy, odm_arm_locs, arm_scores, gt_boxes, gt_labels, gt_offsets, obj,
              npos_total, ovl, threshold, neg_threshold, theta, reg, cls, flags, reg_weight,
              focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool, nullptr,
              fused ? ws.fin : nullptr, loss_out};
+  a.recs = ws.recs;
   dim3 grid((P + kLTile - 1) / kLTile, B);
   // + 8 floats: the register path's constant-offset row reads may run up to 7 past the last row
   const size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
@@ -1842,7 +1923,7 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
                          reg_weight, ws.pool, static_cast<int64_t>(B) * P, 0, grad_scores, loss_out, ws, s);
 }
 
-size_t sbod_loss_zero_prefix_bytes(void) { return kFinBytes; }
+size_t sbod_loss_zero_bytes(int B, int P) { return carve(nullptr, B > 0 ? B : 1, P > 0 ? P : 1).zero_bytes; }
 
 size_t sbod_loss_pool_offset(int B, int P) {
   return carve(nullptr, B, P).pool_off;
@@ -1913,6 +1994,15 @@ SBOD_STAMP_EXPORT(loss)
 #ifdef SBOD_BLOCK_STAMPS
 // k_multibox's per-workgroup marks (diagnostic build): copies the first n workgroups' 8 marks out,
 // then clears them.
+extern "C" int sbod_debug_fin_marks(unsigned long long *seen, int n, unsigned long long *marks) {
+  const int cap = static_cast<int>(SBOD_STAMP_REGION);
+  if (seen && n > 0) hipMemcpyFromSymbol(seen, HIP_SYMBOL(g_fin_seen), sizeof(unsigned long long) * (n < cap ? n : cap));
+  if (marks) hipMemcpyFromSymbol(marks, HIP_SYMBOL(g_fin_marks), sizeof(unsigned long long) * 8);
+  void *sym = nullptr;
+  if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_fin_seen)) == hipSuccess) hipMemset(sym, 0, sizeof(unsigned long long) * cap);
+  if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_fin_marks)) == hipSuccess) hipMemset(sym, 0, sizeof(unsigned long long) * 8);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
 extern "C" int sbod_debug_mb_marks(unsigned long long *host, int n) {
   const int cap = static_cast<int>(SBOD_STAMP_REGION);
   if (host && n > 0)

@@ -62,6 +62,10 @@ class _AnchorCriterion(nn.Module):
         # co-resident and the bounded wait ends in a NaN loss; measured slower alone too,
         # DESIGN.md round 4)
         self.one_launch = False
+        # focal: sum the workgroups' loss partials in a separate one-block launch after the loss
+        # pass instead of in its last-arriving workgroup (the same exact fixed-point sum, so the
+        # same loss bit for bit; DESIGN.md round 5 has the A/B)
+        self.separate_finish = False
         self.last_components = None
 
     def increase_threshold(self, increment=0.1):
@@ -71,7 +75,7 @@ class _AnchorCriterion(nn.Module):
 
     def _spec(self):
         key = (str(_cfg(self.config, 'reg_loss', 'smoothl1')), str(_cfg(self.config, 'cls_loss', 'ce')),
-               self.neg_pos_ratio, self.alpha, self.distributed)
+               self.neg_pos_ratio, self.alpha, self.distributed, self.separate_finish)
         if getattr(self, '_spec_key', None) != key:
             self._spec_cache = self._build_spec()
             self._spec_key = key
@@ -87,6 +91,8 @@ class _AnchorCriterion(nn.Module):
         if cls_loss == 'FOCAL':
             cls = L.CLS['focal']
             flags = L.LOSS_FOCAL_NORM if self.KIND == 'retina' else 0
+            if self.separate_finish:
+                flags |= L.LOSS_UNFUSED_FINISH
         else:
             cls = L.CLS['ce']
             flags = {'ssd512': L.POOL['nonpos'], 'ssd300': L.POOL['global_neg'],

@@ -1,6 +1,6 @@
 """The focal criteria's in-launch loss finish (loss.hip multibox_finish) at the edges of its
 range, against the oracle (Loss.py:9-38 focal_loss through models/*.py) and against the
-separate double-accumulating finaliser (SBOD_LOSS_UNFUSED_FINISH):
+separate one-block finaliser (``separate_finish``, SBOD_LOSS_UNFUSED_FINISH):
 
   * RetinaNet-sized grids (B=32, P=32,736: 4,096 workgroups, 128 per accumulator line);
   * large but finite logits (per-row losses ~100) and huge ones (softmax underflow: the
@@ -8,7 +8,8 @@ separate double-accumulating finaliser (SBOD_LOSS_UNFUSED_FINISH):
   * a near-zero loss (every row exactly 0 but a dozen at 1e-7): the fixed-point resolution.
 
 Tolerance: fp32 losses within 1e-4 relative of the oracle (north_star); the fused and the
-unfused finish sum the same fp32 workgroup partials, so they agree within 1e-6."""
+separate finish sum the same fp32 workgroup partials exactly (128-bit fixed point), so their
+components are bit-identical."""
 import numpy as np
 import pytest
 import torch
@@ -33,10 +34,9 @@ CLASSES = {'ssd512': CR.MultiBoxLoss512, 'retina': CR.RetinaFocalLoss}
 def _crit(kind, P, reg, reg_weights=1.0, unfused=False):
     crit = CLASSES[kind](priors_cxcy=P.to(DEV), config=Cfg(reg_weights=reg_weights, device=DEV, n_classes=21,
                                                            reg_loss=reg, cls_loss='focal'))
+    crit.separate_finish = unfused
     if unfused:
-        s = crit._spec()
-        crit._spec_cache = core.CriterionSpec(s.reg, s.cls, s.flags | L.LOSS_UNFUSED_FINISH, s.neg_pos_ratio,
-                                              s.reg_weight, s.alpha, s.gamma)
+        assert crit._spec().flags & L.LOSS_UNFUSED_FINISH
     return crit
 
 
@@ -65,7 +65,7 @@ def test_fused_finish_retina_full_batch():
     locs, scores = synth.make_preds(B, P.shape[0], 21, seed=23)
     fused, cf, gf = _loss(_crit('retina', P, 'diou'), locs, scores, boxes, labels)
     unf, cu, gu = _loss(_crit('retina', P, 'diou', unfused=True), locs, scores, boxes, labels)
-    np.testing.assert_allclose(cf, cu, rtol=1e-6)
+    assert np.array_equal(cf, cu)
     assert np.array_equal(gf, gu)
     ref, _ = _oracle('retina', P, locs, scores, boxes, labels, 'diou')
     np.testing.assert_allclose(fused, ref, rtol=1e-4)
@@ -88,7 +88,7 @@ def test_fused_finish_large_logits(scale):
     else:
         assert np.isfinite(fused) and fused > 100.0   # normalised by n_pos: ~1e3 at x10
         np.testing.assert_allclose(fused, ref, rtol=1e-4)
-        np.testing.assert_allclose(cf, cu, rtol=1e-6)
+        assert np.array_equal(cf, cu)
 
 
 def test_fused_finish_near_zero_loss():
@@ -119,4 +119,40 @@ def test_fused_finish_near_zero_loss():
     ref, _ = _oracle('ssd512', P, locs, scores, boxes, labels, 'smoothl1', reg_weights=0.0)
     assert 1e-7 < ref < 1e-5
     np.testing.assert_allclose(fused, ref, rtol=1e-4)
-    np.testing.assert_allclose(cf[1], cu[1], rtol=1e-6)
+    assert np.array_equal(cf, cu)
+
+
+def test_finish_epochs_repeat_and_interleave():
+    """The fused finish's records carry a per-call tag (the workspace's epoch + 1, loss.hip
+    loss_gather): calls in a row on one workspace give the same loss bits; calls of another
+    shape and CE mining calls (the same workspace: their partials and pools lie past the records)
+    in between change nothing; the separate finaliser gives the same bits."""
+    Pt = torch.from_numpy(prior_table('SSD512'))
+    Pn = Pt.shape[0]
+    crit = _crit('ssd512', Pt, 'diou')
+    ce = CR.MultiBoxLoss512(priors_cxcy=Pt.to(DEV), config=Cfg(reg_weights=1.0, device=DEV, n_classes=21,
+                                                               reg_loss='diou', cls_loss='ce'))
+    spec_f, spec_ce = crit._spec(), ce._spec()
+    spec_u = core.CriterionSpec(spec_f.reg, spec_f.cls, spec_f.flags | L.LOSS_UNFUSED_FINISH, spec_f.neg_pos_ratio,
+                                spec_f.reg_weight, spec_f.alpha, spec_f.gamma)
+
+    def run(spec, B, seed):
+        boxes, labels = synth.make_gt(B, seed=seed)
+        locs, scores = synth.make_preds(B, Pn, 21, seed=seed)
+        gt = core.pack_gt([b.to(DEV) for b in boxes], [l.to(DEV) for l in labels])
+        obj, ovl, npos = core.match(gt, crit.priors_xy, Pn, crit.threshold)
+        _, comps = core.fused_criterion(locs.to(DEV), scores.to(DEV), gt, obj, ovl, npos, npos[B:],
+                                        crit.priors_cxcy, spec, crit.threshold, crit.threshold - 0.1)
+        return comps.cpu().numpy()
+
+    a = run(spec_f, 8, 61)
+    assert np.isfinite(a).all()
+    for _ in range(4):
+        assert np.array_equal(run(spec_f, 8, 61), a)
+    b = run(spec_f, 3, 62)
+    run(spec_ce, 8, 63)
+    run(spec_ce, 2, 64)
+    assert np.array_equal(run(spec_f, 8, 61), a)
+    assert np.array_equal(run(spec_f, 3, 62), b)
+    assert np.array_equal(run(spec_u, 8, 61), a)
+    assert np.array_equal(run(spec_f, 8, 61), a)
