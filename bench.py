@@ -83,7 +83,7 @@ def parse(argv=None):
                     help='graph mode: which graph of a step is submitted first')
     ap.add_argument('--crit-form', choices=('two', 'one'), default='two',
                     help='focal criterion: matcher + loss launches (two) or the one-launch form (one)')
-    ap.add_argument('--finish', choices=('fused', 'separate'), default='fused',
+    ap.add_argument('--finish', choices=('fused', 'separate'), default='separate',
                     help='focal loss finish: in the loss pass\'s last-arriving workgroup (fused) or a separate '
                          'one-block launch after it (same exact sum)')
     ap.add_argument('--det-form', choices=('two', 'one'), default='two',
@@ -163,7 +163,7 @@ ALGO_BYTES = {
     'k_criterion': lambda w: w['B'] * w['P'] * (2 * (16 + 4 * w['C']) + 8) + 32 * w['P'],
 }
 HBM_KERNELS = tuple(ALGO_BYTES)
-ALL_KERNELS = HBM_KERNELS + ('k_det_nms', 'k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm')
+ALL_KERNELS = HBM_KERNELS + ('k_det_nms', 'k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm', 'k_loss_final')
 PMC_FILE = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
 
 
@@ -315,7 +315,7 @@ class Step:
 
     def __init__(self, dev, B, rank, world, graph, two_streams=True, priority='none', n_batches=6,
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
-                 crit_streams=2, depth=4, submit='direct', gt_fold=True, finish='fused'):
+                 crit_streams=2, depth=4, submit='direct', gt_fold=True, finish='separate'):
         self.dev, self.B = dev, B
         self.gt_fold = bool(gt_fold)
         Pn = prior_table(ARCH)
@@ -668,7 +668,7 @@ class Step:
         return self.replay() if self.graph is not None else self.eager()
 
 
-def c2_figure(dev, steps, warmup, B=16, n_batches=12, det_form='two', finish='fused'):
+def c2_figure(dev, steps, warmup, B=16, n_batches=12, det_form='two', finish='separate'):
     """Config C2 (SSD512 batch=16 bf16 on 1 GPU): the same captured step with bf16 locs / scores
     (and bf16 gradients) for the criterion, and the detect reading the bf16 activations directly
     (SBOD_DETECT_INPUT_BF16: widened exactly on load, no fp32 copies).  ``n_batches`` resident batches
@@ -896,18 +896,29 @@ def main():
     # the roofline's duration: the dominant kernel's half of the step (criterion or detect)
     # alone, so no kernel of the other half shares the CUs and HBM with it (the in-step figure
     # is kernel_us_per_step above; the concurrent step is step_hbm_frac)
-    half = 'detect' if dominant.startswith('k_det') else 'criterion'
-    st.eager_half(half)
-    torch.cuda.synchronize()
-    L.timing_enable(dominant)
-    t_win0 = time.monotonic_ns()    # the pass's host window: a kernel trace of this run selects
-    for _ in range(max(a.timing_steps, 10)):   # the same dispatches (scripts/roofline_check.py)
-        st.eager_half(half)
-    torch.cuda.synchronize()
-    t_win1 = time.monotonic_ns()
-    n_dom, ms_dom = L.timing_query(dominant)
-    L.timing_enable(None)
-    dom_avg_s = ms_dom / n_dom * 1e-3 if n_dom else float('nan')
+    def alone(kern):
+        """``kern`` timed in its half of the step (criterion or detect) alone: (launches, mean s,
+        host window)"""
+        hf = 'detect' if kern.startswith('k_det') else 'criterion'
+        st.eager_half(hf)
+        torch.cuda.synchronize()
+        L.timing_enable(kern)
+        w0 = time.monotonic_ns()    # the pass's host window: a kernel trace of this run selects
+        for _ in range(max(a.timing_steps, 10)):   # the same dispatches (scripts/roofline_check.py)
+            st.eager_half(hf)
+        torch.cuda.synchronize()
+        w1 = time.monotonic_ns()
+        nk, msk = L.timing_query(kern)
+        L.timing_enable(None)
+        return hf, nk, (msk / nk * 1e-3 if nk else float('nan')), w0, w1
+
+    half, n_dom, dom_avg_s, t_win0, t_win1 = alone(dominant)
+    # the other half's main HBM kernel, timed the same way (both halves' rooflines in the line)
+    others = {}
+    for k in ('k_multibox', 'k_det_prepare'):
+        if k != dominant and k in kernel_us:
+            _, nk, sk, _, _ = alone(k)
+            others[k] = (nk, sk)
 
     eager_ms = None
     api = None
@@ -1019,6 +1030,11 @@ def main():
             'timing': 'in the replayed graph: first workgroup start to last workgroup end '
                       '(s_memrealtime), excludes the dispatch ramp and the end-of-kernel release',
             'clock_hz': L.lib().sbod_timing_clock_hz()}
+    line['roofline_other'] = {
+        k: {'avg_us': round(sk * 1e6, 2), 'launches_timed': nk, 'in_step_avg_us': kernel_us.get(k),
+            'algorithmic_bytes_per_launch': ALGO_BYTES[k](wl),
+            'frac': round(ALGO_BYTES[k](wl) / sk / 1e9 / HBM_PEAK_GBS, 4)}
+        for k, (nk, sk) in others.items()}
     line['kernel_us_per_step'] = kernel_us
     line['kernel_launches_timed'] = kernel_n
     line['resident_batches'] = len(st.batches)

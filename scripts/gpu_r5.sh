@@ -41,6 +41,9 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d['roofline']
 print('bench', d['ms_per_step'], 'ms', d['value'], 'img/s', 'roofline', r['kernel'], r['avg_us'], 'us frac', r['frac'],
       'kernels', d.get('kernel_us_per_step'), 'host', d.get('host_us_per_step'))
+for k, v in (d.get('roofline_other') or {}).items():
+    print('other', k, v['avg_us'], 'us frac', v['frac'], 'in-step', v['in_step_avg_us'])
+print('api', d.get('api_ms_per_step'))
 if 'c2_bf16' in d:
     c = d['c2_bf16']
     print('c2', c['ms_per_step'], 'ms', c['roofline']['avg_us'], 'us frac', c['roofline']['frac'])

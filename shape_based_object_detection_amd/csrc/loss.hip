@@ -1599,8 +1599,11 @@ int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const in
 #undef SBOD_HNM
     SBOD_LAUNCHED("k_hnm");
   }
-  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(256), 0, s, ws.partials, nblk, ws.hnm, nseg, npos_total, reg,
-                     cls, flags, reg_weight, loss_out);
+  {
+    KernelTimer kt("k_loss_final", s, true);
+    tlaunch(kt, k_loss_final, dim3(1), dim3(256), 0, s, static_cast<const float *>(ws.partials), nblk,
+            static_cast<const float *>(ws.hnm), nseg, npos_total, reg, cls, flags, reg_weight, loss_out);
+  }
   SBOD_LAUNCHED("k_loss_final");
   return SBOD_OK;
 }

@@ -62,10 +62,12 @@ class _AnchorCriterion(nn.Module):
         # co-resident and the bounded wait ends in a NaN loss; measured slower alone too,
         # DESIGN.md round 4)
         self.one_launch = False
-        # focal: sum the workgroups' loss partials in a separate one-block launch after the loss
-        # pass instead of in its last-arriving workgroup (the same exact fixed-point sum, so the
-        # same loss bit for bit; DESIGN.md round 5 has the A/B)
-        self.separate_finish = False
+        # focal: the workgroups' loss partials are summed by a separate one-block launch after the
+        # loss pass (default), or by the loss pass's last workgroup gathering every workgroup's
+        # record (False: one launch fewer; its gather waits out the pass's store drain, ~4 us).
+        # The same exact fixed-point sum either way: the same loss bit for bit; the same step time
+        # (same-box A/B)
+        self.separate_finish = True
         self.last_components = None
 
     def increase_threshold(self, increment=0.1):

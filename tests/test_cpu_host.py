@@ -69,11 +69,11 @@ class Cfg(dict):
 
 
 @pytest.mark.parametrize('cls,reg,clsl,exp_reg,exp_cls,exp_flags', [
-    (CR.MultiBoxLoss512, 'diou', 'focal', 'diou', 'focal', 0),
+    (CR.MultiBoxLoss512, 'diou', 'focal', 'diou', 'focal', L.LOSS_UNFUSED_FINISH),
     (CR.MultiBoxLoss512, 'smoothl1', 'ce', 'smoothl1', 'ce', L.POOL['nonpos']),
     (CR.MultiBoxLoss300, 'l1', 'ce', 'l1', 'ce', L.POOL['global_neg']),
-    (CR.MultiBoxLoss300, 'DIoU', 'Focal', 'diou', 'focal', 0),
-    (CR.RetinaFocalLoss, 'diou', 'focal', 'diou', 'focal', L.LOSS_FOCAL_NORM),
+    (CR.MultiBoxLoss300, 'DIoU', 'Focal', 'diou', 'focal', L.LOSS_UNFUSED_FINISH),
+    (CR.RetinaFocalLoss, 'diou', 'focal', 'diou', 'focal', L.LOSS_FOCAL_NORM | L.LOSS_UNFUSED_FINISH),
     (CR.RetinaFocalLoss, 'smoothl1', 'ce', 'smoothl1', 'ce', L.POOL['neg']),
 ])
 def test_criterion_specs_follow_reference(cls, reg, clsl, exp_reg, exp_cls, exp_flags, monkeypatch):
@@ -82,7 +82,12 @@ def test_criterion_specs_follow_reference(cls, reg, clsl, exp_reg, exp_cls, exp_
     c = cls(priors_cxcy=torch.zeros(4, 4), config=Cfg(reg_weights=2.0, device='cpu', n_classes=21,
                                                       reg_loss=reg, cls_loss=clsl))
     s = c._spec()
+    # focal: the separate loss finish is the default (criteria.py separate_finish)
     assert (s.reg, s.cls, s.flags) == (L.REG[exp_reg], L.CLS[exp_cls], exp_flags)
+    if exp_cls == 'focal':
+        c.separate_finish = False
+        assert c._spec().flags == exp_flags & ~L.LOSS_UNFUSED_FINISH
+        c.separate_finish = True
     assert s.reg_weight == 2.0 and s.neg_pos_ratio == 3
     c.increase_threshold()
     assert abs(c.threshold - 0.6) < 1e-12
