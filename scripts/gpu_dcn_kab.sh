@@ -1,0 +1,36 @@
+#!/bin/bash
+# DCN per-kernel A/B: rocprofv3 kernel trace of the 64x64 (and 8x8) maps for the product library
+# and each named variant library; prints the median duration of every DCN kernel per library.
+#   bash scripts/gpu_dcn_kab.sh TAG variant1 [variant2 ...]
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=$1; shift
+O=gpurun_out; mkdir -p $O
+LIBV=$PWD/shape_based_object_detection_amd/lib/variants
+run() {   # name lib
+  local name=$1 lib=$2
+  if [ -n "$lib" ]; then export SBOD_LIB=$lib; else unset SBOD_LIB; fi
+  timeout -k 10 200 rocprofv3 --kernel-trace -d $O/kab_${TAG}_$name -o run --output-format csv -- \
+      python scripts/dcn_maps.py --maps ${MAPS:-64,8} --iters 5 > $O/kab_${TAG}_$name.log 2>&1 || { echo "$name failed"; tail -20 $O/kab_${TAG}_$name.log; exit 1; }
+  python - $O/kab_${TAG}_$name/run_kernel_trace.csv $name <<'PY'
+import csv, sys, statistics
+d = {}
+for r in csv.DictReader(open(sys.argv[1])):
+    n = r['Kernel_Name'].split('(')[0].replace('void ', '').replace('sbod::', '')[:34]
+    key = '%s %sx%sx%s' % (n, r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'])
+    d.setdefault(key, []).append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
+tot = {}
+for k, v in d.items():
+    if 'rocprim' in k:
+        continue
+    print('%-10s %-62s n %3d median %8.2f' % (sys.argv[2], k, len(v), statistics.median(v)))
+PY
+  grep '"ms"' $O/kab_${TAG}_$name.log | python -c "
+import json,sys
+for ln in sys.stdin:
+    r=json.loads(ln); print('$name', r['config'][-22:], 'ms', r['ms'], 'eager', r.get('eager_ms'))"
+}
+run product ''
+for v in "$@"; do run $v $LIBV/libsbod_hip_$v.so; done
+echo EXIT 0

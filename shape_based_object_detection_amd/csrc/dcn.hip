@@ -24,6 +24,53 @@
 namespace sbod {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+#ifdef SBOD_DCN_SPLIT_BF16
+// ---- split-bf16 contraction (the fp32 products on the bf16 matrix cores).  An fp32 value is the
+// exact sum of three bf16 parts, x = h + m + l (h = bf16(x) round-to-nearest-even, m =
+// bf16(x - h), l = x - h - m: 24 significant bits = 3 x 8, every subtraction exact).  A product
+// a*b is then sum_{i,j} a_i b_j; the six terms of order <= 2^-16 relative (hh, hm, mh, hl, lh,
+// mm) are kept, the three below 2^-26 (ml, lm, ll) dropped, every bf16 x bf16 product is exact
+// in the MFMA's fp32 accumulation — so each K = 16 step adds its products with fp32-level error
+// (<= 2^-25 relative per product from the dropped terms), as the fp32 MFMA does, at 6
+// v_mfma_f32_32x32x16_bf16 (32 cycles each) per 16 K instead of 8 v_mfma_f32_32x32x2_f32 (64
+// cycles each): 2.7x the fp32 matrix rate (MI355X_MICROARCH.md: fp32 MFMA runs at the fp32 vector
+// rate, 1/16 of bf16).  Non-finite inputs give NaN (inf - inf in the split), not +-inf.
+__device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l) {
+  h = static_cast<__bf16>(x);
+  const float r = x - static_cast<float>(h);
+  m = static_cast<__bf16>(r);
+  l = static_cast<__bf16>(r - static_cast<float>(m));
+}
+struct Split8 {
+  bf16x8 p[3];   // high, middle, low parts of 8 consecutive K values
+};
+__device__ __forceinline__ Split8 split8(const float (&v)[8]) {
+  Split8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    __bf16 h, m, l;
+    split3(v[i], h, m, l);
+    r.p[0][i] = h;
+    r.p[1][i] = m;
+    r.p[2][i] = l;
+  }
+  return r;
+}
+// acc += A[32 x 16] B[16 x 32] from the split parts: the small terms first
+__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+#endif  // SBOD_DCN_SPLIT_BF16
 
 constexpr int kDcnThreads = 256;
 constexpr int kMaxN = 49;      // k*k <= 49 (k <= 7)
@@ -152,6 +199,36 @@ __global__ __launch_bounds__(256) void k_weight_layouts(const float *__restrict_
     if (wb) wb[(static_cast<int64_t>(n) * O + o) * C + c0 + cl] = v;
   }
 }
+
+#ifdef SBOD_DCN_SPLIT_BF16
+// The backward-data B operand: Wf [O][N][C] fp32 -> wb3 [3][N][C][Op] bf16 split parts, output
+// channels contiguous (the MFMA's K), zero past O (Op = O rounded up to 64).  64 x 64 tiles of
+// (o, c) per kernel point through LDS.
+__global__ __launch_bounds__(256) void k_wb_split(const float *__restrict__ wf, int O, int C, int N, int Op,
+                                                  __bf16 *__restrict__ wb3) {
+  __shared__ float t[64][65];
+  const int c0 = blockIdx.x * 64, o0 = blockIdx.y * 64, n = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int o = o0 + i, c = c0 + tx;
+    t[i][tx] = (o < O && c < C) ? wf[(static_cast<int64_t>(o) * N + n) * C + c] : 0.f;
+  }
+  __syncthreads();
+  const int64_t part = static_cast<int64_t>(N) * C * Op;
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i;
+    if (c >= C) continue;
+    __bf16 h, m, l;
+    split3(t[tx][i], h, m, l);
+    __bf16 *d = wb3 + (static_cast<int64_t>(n) * C + c) * Op + o0 + tx;
+    d[0] = h;
+    d[part] = m;
+    d[2 * part] = l;
+  }
+}
+inline int dcn_opad(int O) { return (O + 63) / 64 * 64; }
+
+#endif  // SBOD_DCN_SPLIT_BF16
 
 // Bilinear combination in the reference's order: ((lt + rb) + lb) + rt, then * mask.
 __device__ __forceinline__ float combine(const float g[4], float m, float x0, float x1, float x2, float x3) {
@@ -469,6 +546,142 @@ __global__ __launch_bounds__(kDcnThreads, 3) void k_dcn_bwd_data(
       }
     }
 }
+
+#ifdef SBOD_DCN_SPLIT_BF16
+// The same contraction on the split-bf16 matrix cores (mfma6).  Block: 32 R pixels x 256
+// channels of ONE kernel point n; K = output channels in chunks of 32.  A = dout [pixel][o]: each
+// thread loads its pixel's kSt consecutive output channels (coalesced along the pixels), splits
+// them and stores the three parts as one vector per part into LDS [part][pixel][o] (a 40-element
+// row pitch: conflict-free 16-byte reads); B = wb3 [part][n][c][o], 16-byte loads of 8
+// consecutive o straight from L2 into the MFMA registers, the next chunk's in flight through
+// the current chunk's MFMAs.  The epilogue is the fp32 kernel's (dcols rows).
+constexpr int kB3Pitch = 40;
+template <int R>
+__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data3(
+    DcnShape s, const __bf16 *__restrict__ wb3, int Op, const float *__restrict__ gout, float *__restrict__ dcols) {
+  constexpr int kRM = 32 * R;                 // pixels per block
+  constexpr int kSt = kBOC * kRM / kDcnThreads;   // output channels per staging thread (8 or 4)
+  constexpr int kOg = kBOC / kSt;             // staging groups along o
+  __shared__ __attribute__((aligned(16))) __bf16 s_a[2][3][kRM][kB3Pitch];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const Tile3 tl = xcd_tile(gridDim.z, gridDim.x, gridDim.y);
+  const int m0 = tl.y * kRM, cgb = tl.z * 256, n = tl.x;
+  const int HWo = s.Ho * s.Wo;
+  const int OT = (s.O + kBOC - 1) / kBOC;
+  // staging role: pixel mm, output channels og * kSt .. + kSt of each chunk
+  const int mm = tid % kRM, og = tid / kRM;
+  static_assert(kOg * kRM == kDcnThreads, "staging covers the chunk");
+  const int msc = min(m0 + mm, s.M - 1);
+  const bool mok = m0 + mm < s.M;
+  const int sb = msc / HWo, spix = msc - sb * HWo;
+  const float *gp = gout + (static_cast<int64_t>(sb) * s.O) * HWo + spix;   // + o * HWo
+  float dstage[kSt];
+  auto load_dout = [&](int oc) {
+#pragma unroll
+    for (int i = 0; i < kSt; ++i) {
+      const int o = oc * kBOC + og * kSt + i;
+      const float v = gp[static_cast<int64_t>(min(o, s.O - 1)) * HWo];   // unconditional, clamped
+      dstage[i] = (mok && o < s.O) ? v : 0.f;
+    }
+  };
+  auto store_dout = [&](int buf) {
+    if constexpr (kSt == 8) {
+      const Split8 sp = split8(dstage);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8 *>(&s_a[buf][p][mm][og * 8]) = sp.p[p];
+    } else {
+      bf16x4 v[3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __bf16 a, b, c;
+        split3(dstage[i], a, b, c);
+        v[0][i] = a;
+        v[1][i] = b;
+        v[2][i] = c;
+      }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x4 *>(&s_a[buf][p][mm][og * 4]) = v[p];
+    }
+  };
+  // B: this lane's channel rows (clamped: channels past C are never stored)
+  const int64_t part = static_cast<int64_t>(s.N) * s.C * Op;
+  const __bf16 *brow[2];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+    brow[ci] = wb3 + (static_cast<int64_t>(n) * s.C + min(cgb + 64 * wv + 32 * ci + l31, s.C - 1)) * Op + 8 * h;
+  bf16x8 bcur[2][2][3], bnext[2][2][3];   // [ci][j][part]; the next chunk's in flight a whole chunk ahead
+  auto load_b = [&](int oc, bf16x8 (&bb)[2][2][3]) {
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bb[ci][j][p] = *reinterpret_cast<const bf16x8 *>(brow[ci] + p * part + oc * kBOC + 16 * j);
+  };
+  f32x16 acc[R][2];
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  load_dout(0);
+  store_dout(0);
+  load_b(0, bcur);
+  __syncthreads();
+  for (int oc = 0; oc < OT; ++oc) {
+    const int buf = oc & 1;
+    const bool more = oc + 1 < OT;
+    const int ocn = more ? oc + 1 : oc;
+    load_dout(ocn);
+    load_b(ocn, bnext);
+    __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf16x8 a[R][3];
+#pragma unroll
+      for (int ri = 0; ri < R; ++ri)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[ri][p] = *reinterpret_cast<const bf16x8 *>(&s_a[buf][p][32 * ri + l31][16 * j + 8 * h]);
+#pragma unroll
+      for (int ri = 0; ri < R; ++ri)
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci) acc[ri][ci] = mfma6(a[ri], bcur[ci][j], acc[ri][ci]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) store_dout(buf ^ 1);
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bcur[ci][j][p] = bnext[ci][j][p];
+    __syncthreads();
+  }
+  // epilogue: row m = 32 ri + (r&3) + 8 (r>>2) + 4 h, column c = cgb + 64 wv + 32 ci + l31
+#pragma unroll
+  for (int ri = 0; ri < R; ++ri)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + 32 * ri + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m >= s.M) continue;
+      float *row = dcols + (static_cast<int64_t>(m) * s.N + n) * s.C;
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci) {
+        const int c = cgb + 64 * wv + 32 * ci + l31;
+        if (c < s.C) {
+#ifdef SBOD_DCN_DCOLS_PLAIN
+          row[c] = acc[ri][ci][r];
+#else
+          __builtin_nontemporal_store(acc[ri][ci][r], row + c);   // streamed: keeps dout / weights in L2
+#endif
+        }
+      }
+    }
+}
+
+#endif  // SBOD_DCN_SPLIT_BF16
 
 // ----------------------------------------------------------------------------- backward (dx gather)
 // dx[b, y, x, c] = sum over the samples (pixel m, kernel point n, corner q) whose corner q lands
@@ -899,7 +1112,11 @@ struct DcnState {
   Coef *coef;
   float *xt, *wf;
   uint32_t *tcount;   // training: [B*H*W + 1] corner samples per input pixel
-  float *wb;          // training: Wb [N][O][C]
+#ifndef SBOD_DCN_SPLIT_BF16
+  float *wb;          // training: Wb [N][O][C] (A/B build: the fp32-MFMA backward-data kernel)
+#else
+  __bf16 *wb3;        // training: [3][N][C][Op] split parts of the weights, o contiguous
+#endif
 };
 
 // Backward scratch (sbod_dcn_scratch_bytes): dcols rows [M][N][C], the weight-gradient
@@ -934,7 +1151,11 @@ size_t carve_state(const DcnShape &s, void *base, DcnState *w, bool train) {
   t.wf = reinterpret_cast<float *>(take(wbytes));
   if (train) {
     t.tcount = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
+#ifndef SBOD_DCN_SPLIT_BF16
     t.wb = reinterpret_cast<float *>(take(wbytes));
+#else
+    t.wb3 = reinterpret_cast<__bf16 *>(take(static_cast<size_t>(3) * s.N * s.C * dcn_opad(s.O) * 2));
+#endif
   }
   if (w) *w = t;
   return off;
@@ -1004,9 +1225,21 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
   hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, st.coef,
                      train ? st.tcount : nullptr, zero_out, n_zero_out);
   SBOD_LAUNCHED("k_dcn_coef");
+#ifndef SBOD_DCN_SPLIT_BF16
   hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
                      train ? st.wb : nullptr);
   SBOD_LAUNCHED("k_weight_layouts");
+#else
+  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
+                     static_cast<float *>(nullptr));
+  SBOD_LAUNCHED("k_weight_layouts");
+  if (train) {
+    const int op = dcn_opad(s.O);
+    hipLaunchKernelGGL(k_wb_split, dim3((s.C + 63) / 64, op / 64, s.N), dim3(256), 0, hs, st.wf, s.O, s.C, s.N, op,
+                       st.wb3);
+    SBOD_LAUNCHED("k_wb_split");
+  }
+#endif
   return SBOD_OK;
 }
 
@@ -1063,12 +1296,22 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
     KernelTimer kt("k_dcn_bwd_data", hs);
     // 64-pixel blocks, or 32 when that leaves fewer blocks than CUs (C4's 8x8 map: 144 -> 288)
     const int64_t nb64 = static_cast<int64_t>((s.M + kBM - 1) / kBM) * ((s.C + 255) / 256) * s.N;
+#ifndef SBOD_DCN_SPLIT_BF16
     if (nb64 >= kBwdDataMinBlocks)
       hipLaunchKernelGGL(k_dcn_bwd_data<2>, dim3((s.M + 63) / 64, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
                          hs, s, st.wb, grad_out, sc.dcols);
     else
       hipLaunchKernelGGL(k_dcn_bwd_data<1>, dim3((s.M + 31) / 32, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
                          hs, s, st.wb, grad_out, sc.dcols);
+#else
+    const int op = dcn_opad(s.O);
+    if (nb64 >= kBwdDataMinBlocks)
+      hipLaunchKernelGGL(k_dcn_bwd_data3<2>, dim3((s.M + 63) / 64, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
+                         hs, s, static_cast<const __bf16 *>(st.wb3), op, grad_out, sc.dcols);
+    else
+      hipLaunchKernelGGL(k_dcn_bwd_data3<1>, dim3((s.M + 31) / 32, (s.C + 255) / 256, s.N), dim3(kDcnThreads), 0,
+                         hs, s, static_cast<const __bf16 *>(st.wb3), op, grad_out, sc.dcols);
+#endif
   }
   if (need_cols) SBOD_LAUNCHED("k_dcn_bwd_data");
   if (grad_x) {

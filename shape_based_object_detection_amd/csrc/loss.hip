@@ -1390,12 +1390,24 @@ __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ pa
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   Fx128 fc{0ull, 0ull}, fl{0ull, 0ull};
   bool ok = true;
-  for (int i = tid; i < nparts; i += blockDim.x) {
-    const float2 v = reinterpret_cast<const float2 *>(partials)[i];
-    const bool f = fx_foldable(v.x) && fx_foldable(v.y);
-    ok = ok && f;
-    fc = fx128_add(fc, to_fx128(f ? v.x : 0.f));
-    fl = fx128_add(fl, to_fx128(f ? v.y : 0.f));
+  // eight partials per thread in flight per batch (a 1-block launch: its time is load latency)
+  constexpr int kB = 8;
+  const float2 *p2 = reinterpret_cast<const float2 *>(partials);
+  for (int i0 = 0; i0 < nparts; i0 += kB * static_cast<int>(blockDim.x)) {
+    float2 v[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      const int i = i0 + k * static_cast<int>(blockDim.x) + tid;
+      v[k] = p2[min(i, nparts - 1)];   // unconditional (clamped), zeroed below: no wait at a join
+      if (i >= nparts) v[k] = make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      const bool f = fx_foldable(v[k].x) && fx_foldable(v[k].y);
+      ok = ok && f;
+      fc = fx128_add(fc, to_fx128(f ? v[k].x : 0.f));
+      fl = fx128_add(fl, to_fx128(f ? v[k].y : 0.f));
+    }
   }
   for (int i = tid; i < nseg; i += blockDim.x) {
     const float v = hnm[i];
