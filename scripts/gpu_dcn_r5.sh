@@ -39,7 +39,7 @@ if [ $AB = 1 ] && [ -f $LIBV/libsbod_hip_dcnsplit.so ]; then
   python -c "
 import json,sys
 for ln in open(sys.argv[1]):
-    r=json.loads(ln); print("split maps", r['config'][-30:], r['ms'], 'frac', r['mfma_frac'], 'eager', r.get('eager_ms'))
+    r=json.loads(ln); print('split maps', r['config'][-30:], r['ms'], 'frac', r['mfma_frac'], 'eager', r.get('eager_ms'))
 " $O/dcn_maps_split_$TAG.jsonl
 fi
 if [ $PROF = 1 ]; then
