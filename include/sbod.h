@@ -231,10 +231,10 @@ enum { SBOD_LOSS_DEFER_MINING = 64 };
  * publishes its fp32 partials as one tagged 16-byte record and the grid's last workgroup sums
  * all of them exactly, as 128-bit fixed-point integers (2^-64 resolution; a partial that is
  * non-finite or >= 2^40 in magnitude switches the finish to a double sum of the fp32 partials in
- * record order, as the separate finaliser computes it).  The finish's state — an epoch word and
- * the records — is the workspace's first sbod_loss_zero_bytes(B, P) bytes: zero on entry, or as a
- * previous successful call with the same B and P (fused or not) left them.  A caller that knows
- * that passes SBOD_LOSS_WS_ZEROED and the call issues no memset (hipGraph capture); without it the
+ * record order, as the separate finaliser computes it).  The finish's state — a few words and the
+ * records — is the workspace's first sbod_loss_zero_bytes(B, P) bytes: zero on entry, and left
+ * zero by every successful call (so any smaller prefix stays zero too).  A caller that knows that
+ * passes SBOD_LOSS_WS_ZEROED and the call issues no memset (hipGraph capture); without it the
  * call zeroes them first (one hipMemsetAsync).  A finish whose wait for the records timed out
  * (2 s: a hardware fault) makes this and every later loss on the workspace NaN until it is zeroed.
  * SBOD_LOSS_UNFUSED_FINISH finishes a focal criterion with the separate one-block finaliser
@@ -275,9 +275,8 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
  * DESIGN.md round 4); the product library always runs the two launches.  Data parallelism (a
  * normaliser all-reduced between the matcher and the loss) uses the two calls.
  * Workspace: sbod_criterion_workspace_bytes(B, Gmax, P); its first
- * sbod_criterion_zero_bytes(B, Gmax, P) bytes must be zero on entry, or as a previous successful
- * call with the same B, Gmax and P left them (the loss finish's epoch word and records, as for
- * sbod_multibox_loss): pass SBOD_CRIT_WS_ZEROED when they are (else the call zeroes them, one
+ * sbod_criterion_zero_bytes(B, Gmax, P) bytes must be zero on entry and are left zero by every
+ * successful call: pass SBOD_CRIT_WS_ZEROED when they are (else the call zeroes them, one
  * hipMemsetAsync).  flags: SBOD_LOSS_FOCAL_NORM, SBOD_CRIT_WS_ZEROED, SBOD_CRIT_TWO_LAUNCH,
  * SBOD_LOSS_UNFUSED_FINISH.  sbod_criterion_status() (diagnostics, synchronises the stream) reads
  * the sticky word the one-launch form sets if a bounded in-launch wait ever gave up (that call's

@@ -88,7 +88,7 @@ def main():
     torch.cuda.synchronize()
     pr.disable()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats('tottime').print_stats(30)
+    pstats.Stats(pr, stream=s).sort_stats('tottime').print_stats(45)
     res = {'B': B, 'steps': steps, 'api_sync_ms_per_step': round(sync_ms, 4),
            'api_pipelined_ms_per_step': round(pipe_ms, 4), 'pipeline_depth': depth,
            'host_us_per_call_sync': {'criterion': round(parts[0] / steps * 1e6, 1),

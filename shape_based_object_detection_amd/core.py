@@ -565,7 +565,7 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
         gs = torch.empty_like(scores) if want_grad else None
         ws = workspace(nb, dev, 'criterion')
         wp = ws.data_ptr()
-        zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion', (B, gmax, P))
+        zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion')
         _CLEAN.pop(wp, None)
         flags = ((spec.flags & (L.LOSS_FOCAL_NORM | L.LOSS_UNFUSED_FINISH)) | zflag |
                  (L.CRIT_TWO_LAUNCH if two_launch else 0))
@@ -574,7 +574,7 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
                float(threshold), float(neg_threshold), spec.reg, flags, float(spec.reg_weight), float(spec.alpha),
                float(spec.gamma), obj.data_ptr(), ovl.data_ptr(), npos.data_ptr(), L.ptr(gl), L.ptr(gs),
                out.data_ptr(), wp, nb, stream)
-        _CLEAN[wp] = (zb, (B, gmax, P))   # (only the zero-on-entry prefix, for this layout)
+        _CLEAN[wp] = (zb, None)   # (only the zero-on-entry prefix is known clean)
         return out, gl, gs
 
     want = torch.is_grad_enabled() and (locs.requires_grad or scores.requires_grad)
@@ -746,7 +746,7 @@ def _count_slot(dev, B):
 # leaves its candidate counters zero, so after the first call on a workspace no memset is
 # needed — none in a captured graph (SBOD_DETECT_COUNTERS_ZEROED).
 _CLEAN = {}
-_LOSS_ZERO = {}     # (B, P) -> sbod_loss_zero_bytes: the fused finish's epoch word and records
+_LOSS_ZERO = {}     # (B, P) -> sbod_loss_zero_bytes: the fused finish's words and records
 
 
 def _loss_zero_bytes(B, P):

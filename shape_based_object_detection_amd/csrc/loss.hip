@@ -504,29 +504,27 @@ __device__ __forceinline__ void block_sum2(float &x, float &y, float *scratch /*
 // the double sum of all partials in record order (a second, ordered pass) is the result, as
 // k_loss_final computes it — never silently wrong (a NaN row of the focal loss, the reference's
 // 0 * log 0, makes a NaN loss that way).
-// Tags: the call's epoch word E (read by every workgroup at its start; written only by the
-// finisher, after it has seen every record of the call) gives tag E + 1 (never 0); records left
-// by earlier calls carry tags <= E, and a zeroed workspace holds E = 0 and tags 0
-// (sbod_loss_zero_bytes: the epoch word and the records are the zero-on-entry prefix).  The
-// finisher's wait is bounded (kGatherTicks of the 100 MHz clock): a timeout — a hardware fault,
-// never a schedule — makes this and every later call's loss NaN (a sticky word, cleared only by
-// the zeroing memset), since a record landing after it could carry a later call's tag.
+// Tags: a record slot is zero on entry (sbod_loss_zero_bytes: the records are the zero-on-entry
+// prefix) and holds tag 1 once written; the finisher zeroes every slot after folding it, so the
+// workspace is left as it was found (any later call, any shape).  The finisher's wait is bounded
+// (kGatherTicks of the 100 MHz clock): a timeout — a hardware fault, never a schedule — makes
+// this and every later call's loss NaN (a sticky word, cleared only by the zeroing memset), since
+// a record landing after it would look like a later call's.
 // Critical path after the last record is issued: its write landing + one sweep + the fold.
 // (Rounds 4-5a counted arrivals on 32 group counters and a top counter: a drain, two dependent
 // far-memory atomics and the partials read after the last tile, 3.6-4.5 us of an 18 us launch,
 // scripts/mb_imbalance.py.)
-constexpr int kFinEpoch = kFinStride * kFinGroups + 8;    // u64 word index in the fin region
-constexpr int kFinSticky = kFinStride * kFinGroups + 9;
+constexpr int kFinSticky = kFinStride * kFinGroups + 9;   // u64 word index in the fin region
 constexpr unsigned long long kGatherTicks = 200000000ull;   // 2 s
-__device__ __forceinline__ unsigned loss_tag(unsigned epoch) { return epoch + 1u ? epoch + 1u : 1u; }
+constexpr unsigned kRecTag = 1u;
 // One lane: the workgroup's record, written through.
 __device__ __forceinline__ void loss_publish(const LossArgs &a, float conf_l, float loc_l, unsigned tag, unsigned nblk,
                                              unsigned blk) {
   const u32x4_t v = {__float_as_uint(conf_l), tag, __float_as_uint(loc_l), tag};
   st_wt_b128(a.recs, nblk * 16u, blk * 16u, v);
 }
-// The whole workgroup (the finisher): every record of this call, folded exactly; thread 0 writes
-// the loss and the next epoch.
+// The whole workgroup (the finisher): every record of this call, folded exactly, then zeroed;
+// thread 0 writes the loss.
 __device__ void loss_gather(const LossArgs &a, unsigned nblk, unsigned tag, float n, float *out,
                             unsigned long long *s_fx, double *s_red) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -615,12 +613,13 @@ __device__ void loss_gather(const LossArgs &a, unsigned nblk, unsigned tag, floa
     __syncthreads();
     l = block_sum(l, s_red);
   }
+  if (!any_late)   // every slot back to zero (every one was seen: no writer is left)
+    for (unsigned i = tid; i < nblk; i += kLTile) reinterpret_cast<u32x4_t *>(a.recs)[i] = u32x4_t{0u, 0u, 0u, 0u};
   if (tid == 0) {
     unsigned long long *fin = a.fin;
     if (any_late) st_wt_u64(fin + kFinSticky, 1ull);
     if (any_late || ld_wt_u64(fin + kFinSticky) != 0ull) c = l = __builtin_nan("");
     loss_outputs(c, l, n, a.reg, a.cls, a.flags, a.reg_weight, out);
-    st_wt_u64(fin + kFinEpoch, tag);   // the next call's epoch: every record of this one is in
     FIN_MARK(3, __builtin_amdgcn_s_memrealtime());
   }
 }
@@ -1070,7 +1069,6 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   const bool fast = fast_tile<T, NB>(tsrc, np * C);
   int objv, offb;
   float v, n;
-  unsigned epoch = 0;   // the fused finish's epoch (loss_gather)
   int64_t labg;
   RegIn rg;
   typename TileVec<T>::V tr[NB > 0 ? NB : 1];
@@ -1177,7 +1175,6 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     if constexpr (NB > 0 && sizeof(T) != 4)
       if (fast) tile_commit(s_sc, tr, np * C);
     n = static_cast<float>(*a.npos_total);
-    if (a.fin != nullptr) epoch = static_cast<unsigned>(ld_wt_u64(a.fin + kFinEpoch));
     MB_MARK(0, tid == 0);
   }
   SEG_PHASE(1);
@@ -1202,7 +1199,7 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
     // the fused finish (focal): this workgroup's record, its tile, and in the grid's last
     // workgroup the gather of every record
     block_sum2(conf_l, loc_l, s_red);
-    const unsigned tag = loss_tag(epoch);
+    const unsigned tag = kRecTag;
     if (tid == 0) loss_publish(a, conf_l, loc_l, tag, nblk, blk);
     if (grad) tile_store(gsc + rbase * C, s_sc, np * C, 0, kLTile);
     MB_MARK(7, tid == 0);
@@ -1559,7 +1556,7 @@ struct LossWs {
   unsigned long long *fin;
   void *recs;
   size_t pool_off;     // byte offset of `pool` (sbod_loss_pool_offset)
-  size_t zero_bytes;   // the fused finish's state: epoch word (in `fin`) and records
+  size_t zero_bytes;   // the fused finish's state: its words (`fin`) and records, left zero
   size_t bytes;
 };
 LossWs carve(void *w, int B, int P) {
@@ -1879,10 +1876,10 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
     return SBOD_E_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
-  // no mining pass (focal): the fused pass finishes the loss itself (loss_gather), so the step
-  // has no k_loss_final launch; its state (epoch word, records) is zero on entry or as a previous
-  // call of the same shape left it (SBOD_LOSS_WS_ZEROED); every call without the flag zeroes
-  // it, fused or not, and a mining-path call of the same shape never touches it
+  // no mining pass (focal, without SBOD_LOSS_UNFUSED_FINISH): the fused pass finishes the loss
+  // itself (loss_gather), so the step has no k_loss_final launch; its state (sticky word, records)
+  // is zero on entry and left zero (SBOD_LOSS_WS_ZEROED); every call without the flag zeroes it,
+  // fused or not, and no other pass writes it
   const bool fused = cls == SBOD_CLS_FOCAL && !(flags & (SBOD_LOSS_DEFER_MINING | SBOD_LOSS_UNFUSED_FINISH));
   if ((flags & SBOD_LOSS_WS_ZEROED) == 0 &&
       hipMemsetAsync(ws.fin, 0, ws.zero_bytes, s) != hipSuccess)

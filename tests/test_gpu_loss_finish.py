@@ -2,7 +2,7 @@
 range, against the oracle (Loss.py:9-38 focal_loss through models/*.py) and against the
 separate one-block finaliser (``separate_finish``, SBOD_LOSS_UNFUSED_FINISH):
 
-  * RetinaNet-sized grids (B=32, P=32,736: 4,096 workgroups, 128 per accumulator line);
+  * RetinaNet-sized grids (B=32, P=32,736: 4,096 workgroup records);
   * large but finite logits (per-row losses ~100) and huge ones (softmax underflow: the
     reference's 0 * log 0 NaN, which the finish must carry instead of wrapping);
   * a near-zero loss (every row exactly 0 but a dozen at 1e-7): the fixed-point resolution.
@@ -122,14 +122,15 @@ def test_fused_finish_near_zero_loss():
     assert np.array_equal(cf, cu)
 
 
-def test_finish_epochs_repeat_and_interleave():
-    """The fused finish's records carry a per-call tag (the workspace's epoch + 1, loss.hip
-    loss_gather): calls in a row on one workspace give the same loss bits; calls of another
-    shape and CE mining calls (the same workspace: their partials and pools lie past the records)
-    in between change nothing; the separate finaliser gives the same bits."""
+def test_finish_records_repeat_and_interleave():
+    """The fused finish's records (loss.hip loss_gather: tagged on publication, zeroed by the
+    finisher after folding): calls in a row on one workspace give the same loss bits; calls of
+    another shape and CE mining calls on the same workspace in between change nothing; the
+    separate finaliser gives the same bits."""
     Pt = torch.from_numpy(prior_table('SSD512'))
     Pn = Pt.shape[0]
     crit = _crit('ssd512', Pt, 'diou')
+    crit.separate_finish = False   # the in-kernel gather under test
     ce = CR.MultiBoxLoss512(priors_cxcy=Pt.to(DEV), config=Cfg(reg_weights=1.0, device=DEV, n_classes=21,
                                                                reg_loss='diou', cls_loss='ce'))
     spec_f, spec_ce = crit._spec(), ce._spec()
