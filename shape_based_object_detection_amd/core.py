@@ -582,6 +582,50 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
     return loss, holder[0], (obj, ovl, npos)
 
 
+def criterion_focal_fast(locs, scores, boxes, labels, priors_cxcy, priors_xy, spec, threshold, neg_threshold):
+    """The criterion classes' focal call in ONE native call (_sbodhost.criterion_focal_fast): GT
+    list checks + packing into the stream's cached buffers, sbod_criterion_focal (two launches,
+    ``fresh_match=False`` buffers), and the loss tensor's C++ autograd node — the same launches,
+    buffers and gradients as ``pack_gt(reuse=True)`` + ``criterion_focal``.  Returns
+    (loss, components) or None when the call needs that Python path (first call on a stream,
+    growing buffers, conversions, capture, any irregular argument: it re-checks and raises the
+    errors)."""
+    ext = L.host_ext
+    if (ext is None or L._recorder or type(boxes) is not list or type(labels) is not list or not locs.is_cuda
+            or torch.cuda.is_current_stream_capturing()):
+        return None   # (a recording caller needs the sbod_* calls to pass through L.call)
+    dev = locs.device
+    B, P = locs.shape[0], locs.shape[1]
+    stream = L._raw_stream(dev.index)
+    pk = _PACK_CACHE.get((dev.index, stream, B))
+    mo = _MATCH_OUT.get((dev.index, stream, B, P))
+    ws = _WS.get((dev, stream, 'criterion'))
+    if (pk is None or mo is None or ws is None or priors_cxcy.shape[0] != P or not priors_cxcy.is_contiguous()
+            or not priors_xy.is_contiguous()):
+        return None
+    gb, gl, off, cap = pk
+    obj, ovl, npos = mo
+    wp = ws.data_ptr()
+    ent = _CLEAN.pop(wp, None)
+    u = _UNIT.get(dev)
+    flags = (spec.flags & (L.LOSS_FOCAL_NORM | L.LOSS_UNFUSED_FINISH)) | L.CRIT_TWO_LAUNCH
+    r = ext.criterion_focal_fast(locs, scores, boxes, labels, priors_cxcy.data_ptr(), priors_xy.data_ptr(),
+                                 gb.data_ptr(), gl.data_ptr(), off.data_ptr(), cap, spec.reg, flags, float(threshold),
+                                 float(neg_threshold), float(spec.reg_weight), float(spec.alpha), float(spec.gamma),
+                                 obj.data_ptr(), ovl.data_ptr(), npos.data_ptr(), wp, ws.numel(),
+                                 ent[0] if ent is not None else 0, stream, u.data_ptr() if u is not None else None)
+    if r is None:
+        if ent is not None:
+            _CLEAN[wp] = ent   # nothing ran on the workspace
+        return None
+    if type(r) is int:
+        raise L.SbodError('sbod_criterion_focal failed (%d): %s'
+                          % (r, L.lib().sbod_last_error().decode(errors='replace')))
+    loss, comps, zb = r
+    _CLEAN[wp] = (zb, None)
+    return loss, comps
+
+
 def criterion_status(device=None):
     """The one-launch criterion's in-launch wait status on ``device`` (current stream's cached
     workspace): 0 = every wait completed.  Synchronises the stream (diagnostics, tests)."""

@@ -15,8 +15,15 @@
 //       device < 0 = any (one device for the whole batch either way).
 //
 //   stage_and_replay(...): the same packing, then captured graphs and an event (below).
+//
+//   criterion_focal_fast(...): a focal criterion call of the reference-named classes
+//       (MultiBoxLoss512 / 300 / RetinaFocalLoss, models/SSD512.py:525-623) in one call: the GT
+//       list checks + packing, sbod_criterion_focal, and the loss tensor's autograd node — a C++
+//       node (FusedLossFn), so loss.backward() runs no Python on autograd's device thread.
 #include <Python.h>
 
+#include <ATen/ATen.h>
+#include <torch/csrc/autograd/custom_function.h>
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
@@ -344,7 +351,158 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   Py_RETURN_TRUE;
 }
 
+// ---------------------------------------------------------------------------- criterion_focal_fast
+// The criterion launch inside the autograd node's forward, so the node owns the gradients the
+// fused pass writes (core._FusedLoss's contract): backward hands them over as they are when the
+// upstream gradient is core.unit_grad(), else scales them in place on the forward's stream
+// (sbod_scale2_inplace: no host sync), and drops its own references first so AccumulateGrad
+// adopts them as .grad instead of cloning them.
+struct CritCall {
+  int dtype, B, P, C, gmax, reg, flags;
+  const void *pcxcy, *pxy, *gtb, *gtl, *gto;
+  float thr, nthr, reg_weight, alpha, gamma;
+  void *obj, *ovl, *npos, *ws, *stream;
+  size_t ws_bytes;
+  bool want;
+  int64_t unit;      // data pointer of core.unit_grad(device), 0 if none yet
+  at::Tensor out;    // {total, conf, loc, n_pos_total}
+  int status = 0;
+};
+
+struct FusedLossFn : public torch::autograd::Function<FusedLossFn> {
+  static at::Tensor forward(torch::autograd::AutogradContext *ctx, const at::Tensor &locs, const at::Tensor &scores,
+                            CritCall *c) {
+    at::Tensor out = at::empty({4}, locs.options().dtype(at::kFloat));
+    at::Tensor gl, gs;
+    if (c->want) {
+      gl = at::empty_like(locs);
+      gs = at::empty_like(scores);
+    }
+    c->status = sbod_criterion_focal(locs.data_ptr(), scores.data_ptr(), c->dtype, c->B, c->P, c->C,
+                                     static_cast<const float *>(c->pcxcy), static_cast<const float *>(c->pxy),
+                                     static_cast<const float *>(c->gtb), static_cast<const int64_t *>(c->gtl),
+                                     static_cast<const int32_t *>(c->gto), c->gmax, c->thr, c->nthr, c->reg, c->flags,
+                                     c->reg_weight, c->alpha, c->gamma, static_cast<int32_t *>(c->obj),
+                                     static_cast<float *>(c->ovl), static_cast<int32_t *>(c->npos),
+                                     gl.defined() ? gl.data_ptr() : nullptr, gs.defined() ? gs.data_ptr() : nullptr,
+                                     out.data_ptr<float>(), c->ws, c->ws_bytes, c->stream);
+    c->out = out;
+    ctx->saved_data["gl"] = gl;
+    ctx->saved_data["gs"] = gs;
+    ctx->saved_data["stream"] = reinterpret_cast<int64_t>(c->stream);
+    ctx->saved_data["unit"] = c->unit;
+    ctx->saved_data["dt"] = static_cast<int64_t>(c->dtype);
+    ctx->set_materialize_grads(false);
+    return out.select(0, 0);
+  }
+  static torch::autograd::variable_list backward(torch::autograd::AutogradContext *ctx,
+                                                 torch::autograd::variable_list go) {
+    auto &sd = ctx->saved_data;
+    if (sd.find("gl") == sd.end())
+      throw std::runtime_error("sbod fused criterion: backward through the same graph twice is not supported "
+                               "(its gradients are produced in forward)");
+    at::Tensor gl = sd["gl"].toTensor(), gs = sd["gs"].toTensor();
+    void *stream = reinterpret_cast<void *>(sd["stream"].toInt());
+    const int64_t unit = sd["unit"].toInt();
+    const int dt = static_cast<int>(sd["dt"].toInt());
+    sd.erase("gl");
+    sd.erase("gs");
+    if (go.empty() || !go[0].defined() || !gl.defined()) return {at::Tensor(), at::Tensor(), at::Tensor()};
+    at::Tensor g = go[0];
+    if (unit == 0 || reinterpret_cast<int64_t>(g.data_ptr()) != unit) {
+      if (g.scalar_type() != at::kFloat || !g.is_contiguous()) g = g.detach().to(at::kFloat).contiguous();
+      const int st = sbod_scale2_inplace(gl.data_ptr(), gl.numel(), gs.data_ptr(), gs.numel(), dt,
+                                         g.data_ptr<float>(), stream);
+      if (st != SBOD_OK) throw std::runtime_error(std::string("sbod_scale2_inplace: ") + sbod_last_error());
+    }
+    return {std::move(gl), std::move(gs), at::Tensor()};
+  }
+};
+
+// criterion_focal_fast(locs, scores, boxes, labels, priors_cxcy_ptr, priors_xy_ptr, gt_boxes_ptr,
+//                      gt_labels_ptr, gt_offsets_ptr, gt_capacity, reg, flags, threshold,
+//                      neg_threshold, reg_weight, alpha, gamma, obj_ptr, ovl_ptr, npos_ptr, ws_ptr,
+//                      ws_bytes, clean_bytes, stream, unit_ptr)
+//   -> (loss, components, zero_bytes) | None (the batch or the cached buffers need the Python
+//      path: it re-packs) | int (a failing sbod status; the caller raises)
+//   locs / scores: [B,P,4] / [B,P,C] contiguous, both float32 or both bfloat16, on the device of
+//   the GT lists.  flags: SBOD_LOSS_FOCAL_NORM / SBOD_LOSS_UNFUSED_FINISH / SBOD_CRIT_TWO_LAUNCH;
+//   SBOD_CRIT_WS_ZEROED is added here when the workspace's first clean_bytes cover the call's
+//   zero-on-entry prefix (returned, for the caller's bookkeeping).
+PyObject *criterion_focal_fast(PyObject *, PyObject *const *a, Py_ssize_t n) {
+  if (n != 25) {
+    PyErr_SetString(PyExc_TypeError, "criterion_focal_fast: expected 25 arguments");
+    return nullptr;
+  }
+  if (!THPVariable_Check(a[0]) || !THPVariable_Check(a[1])) Py_RETURN_NONE;
+  const at::Tensor &locs = THPVariable_Unpack(a[0]);
+  const at::Tensor &scores = THPVariable_Unpack(a[1]);
+  const auto dt = locs.scalar_type();
+  if (!locs.is_cuda() || !scores.is_cuda() || (dt != at::kFloat && dt != at::kBFloat16) || scores.scalar_type() != dt ||
+      locs.dim() != 3 || scores.dim() != 3 || locs.size(2) != 4 || locs.size(0) != scores.size(0) ||
+      locs.size(1) != scores.size(1) || !locs.is_contiguous() || !scores.is_contiguous() ||
+      locs.get_device() != scores.get_device())
+    Py_RETURN_NONE;
+  CritCall c;
+  c.dtype = dt == at::kFloat ? SBOD_DT_F32 : SBOD_DT_BF16;
+  c.B = static_cast<int>(locs.size(0));
+  c.P = static_cast<int>(locs.size(1));
+  c.C = static_cast<int>(scores.size(2));
+  c.pcxcy = PyLong_AsVoidPtr(a[4]);
+  c.pxy = PyLong_AsVoidPtr(a[5]);
+  void *gb = PyLong_AsVoidPtr(a[6]), *gl = PyLong_AsVoidPtr(a[7]), *go = PyLong_AsVoidPtr(a[8]);
+  const long long cap = PyLong_AsLongLong(a[9]);
+  c.reg = static_cast<int>(PyLong_AsLong(a[10]));
+  c.flags = static_cast<int>(PyLong_AsLong(a[11]));
+  c.thr = static_cast<float>(PyFloat_AsDouble(a[12]));
+  c.nthr = static_cast<float>(PyFloat_AsDouble(a[13]));
+  c.reg_weight = static_cast<float>(PyFloat_AsDouble(a[14]));
+  c.alpha = static_cast<float>(PyFloat_AsDouble(a[15]));
+  c.gamma = static_cast<float>(PyFloat_AsDouble(a[16]));
+  c.obj = PyLong_AsVoidPtr(a[17]);
+  c.ovl = PyLong_AsVoidPtr(a[18]);
+  c.npos = PyLong_AsVoidPtr(a[19]);
+  c.ws = PyLong_AsVoidPtr(a[20]);
+  c.ws_bytes = static_cast<size_t>(PyLong_AsUnsignedLongLong(a[21]));
+  const unsigned long long clean = PyLong_AsUnsignedLongLong(a[22]);
+  c.stream = opt_ptr(a[23]);
+  c.unit = static_cast<int64_t>(reinterpret_cast<intptr_t>(opt_ptr(a[24])));
+  if (PyErr_Occurred()) return nullptr;
+  ListRows rows;
+  const int r = pack_lists(a[2], a[3], cap, -1, locs.get_device(), gb, gl, go, c.stream, 0, rows, c.stream);
+  if (r == 0) Py_RETURN_NONE;
+  if (r < 0) return PyLong_FromLong(r);
+  if (static_cast<int>(rows.cnt.size()) != c.B) Py_RETURN_NONE;   // (the caller's error path names it)
+  int gmax = 1;
+  for (int32_t g : rows.cnt) gmax = g > gmax ? g : gmax;
+  c.gmax = gmax;
+  if (sbod_criterion_workspace_bytes(c.B, gmax, c.P) > c.ws_bytes) Py_RETURN_NONE;   // the Python path grows it
+  const size_t zb = sbod_criterion_zero_bytes(c.B, gmax, c.P);
+  if (zb <= clean) c.flags |= SBOD_CRIT_WS_ZEROED;
+  c.gtb = gb;
+  c.gtl = gl;
+  c.gto = go;
+  c.want = at::GradMode::is_enabled() && (locs.requires_grad() || scores.requires_grad());
+  at::Tensor loss;
+  try {
+    loss = FusedLossFn::apply(locs, scores, &c);
+  } catch (const std::exception &e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+  if (c.status != SBOD_OK) return PyLong_FromLong(c.status);
+  PyObject *res = PyTuple_New(3);
+  if (!res) return nullptr;
+  PyTuple_SET_ITEM(res, 0, THPVariable_Wrap(std::move(loss)));
+  PyTuple_SET_ITEM(res, 1, THPVariable_Wrap(std::move(c.out)));
+  PyTuple_SET_ITEM(res, 2, PyLong_FromSize_t(zb));
+  return res;
+}
+
 PyMethodDef methods[] = {
+    {"criterion_focal_fast",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(criterion_focal_fast)),
+     METH_FASTCALL, "GT packing + sbod_criterion_focal + a C++ autograd node for the loss."},
     {"make_step_program",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(make_step_program)),
      METH_FASTCALL, "Parse a recorded step (GT packing target, criterion and detect calls, event) once."},

@@ -113,8 +113,16 @@ class _AnchorCriterion(nn.Module):
                                              _cfg(self.config, 'reg_loss', 'smoothl1'),
                                              _cfg(self.config, 'cls_loss', 'ce'), self.threshold,
                                              self.neg_pos_ratio, self.alpha)
-        gt = core.pack_gt(boxes, labels, reuse=True)   # consumed by this call's launches only
         spec = self._spec()
+        if spec.cls == L.CLS['focal'] and not self.distributed and not self.one_launch:
+            # the whole call natively (GT packing, the launches, a C++ autograd node), once the
+            # Python path below has set up this stream's buffers
+            r = core.criterion_focal_fast(predicted_locs, predicted_scores, boxes, labels, self.priors_cxcy,
+                                          self.priors_xy, spec, self.threshold, self.threshold - 0.1)
+            if r is not None:
+                self.last_components = r[1]
+                return r[0]
+        gt = core.pack_gt(boxes, labels, reuse=True)   # consumed by this call's launches only
         if spec.cls == L.CLS['focal'] and not self.distributed:
             # one device, no mining: the matcher and the loss pass in one C call (the matcher's
             # launches then the loss launch; ONE launch with ``one_launch``)

@@ -1,0 +1,76 @@
+"""The criterion classes' native call (core.criterion_focal_fast: GT packing + sbod_criterion_focal +
+a C++ autograd node, models/criteria.py) against the Python path of the same launches
+(core.pack_gt + core.criterion_focal): bit-identical loss, components and gradients, for
+consecutive batches of different sizes and object counts, and for the three ways a caller
+back-propagates (``loss.backward()``, ``loss.backward(core.unit_grad(dev))``, a scaled loss).
+Reference: models/SSD512.py:508-626 (MultiBoxLoss512), train_anchor.py:271-284."""
+import pytest
+import torch
+
+from shape_based_object_detection_amd import core, synth
+from shape_based_object_detection_amd.models import criteria as CR
+from shape_based_object_detection_amd.models.priors import prior_table
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+class Cfg(dict):
+    __getattr__ = dict.__getitem__
+
+
+def _inputs(B, seed, P, dtype=torch.float32):
+    boxes, labels = synth.make_gt(B, seed=seed, max_objects=4 + 3 * (seed % 5))
+    locs, scores = synth.make_preds(B, P, 21, seed=seed)
+    return ([b.to(DEV) for b in boxes], [l.to(DEV) for l in labels], locs.to(DEV, dtype), scores.to(DEV, dtype))
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_native_criterion_call_equals_python_path(dtype):
+    Pt = torch.from_numpy(prior_table('SSD512')).to(DEV)
+    cfg = Cfg(reg_weights=1.0, device=DEV, n_classes=21, reg_loss='diou', cls_loss='focal')
+    crit = CR.MultiBoxLoss512(priors_cxcy=Pt, config=cfg)
+    spec = crit._spec()
+    seen_native, expect_native, sizes = 0, 0, set()
+    for i, (B, how) in enumerate([(8, 'plain'), (8, 'plain'), (3, 'unit'), (8, 'scaled'), (8, 'unit'), (5, 'plain')]):
+        boxes, labels, locs, scores = _inputs(B, 80 + i, Pt.shape[0], dtype)
+        lo1, sc1 = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
+        ref, ref_c, _ = core.criterion_focal(lo1, sc1, core.pack_gt(boxes, labels), crit.priors_cxcy, crit.priors_xy,
+                                             spec, crit.threshold, crit.threshold - 0.1, two_launch=True)
+        lo2, sc2 = locs.clone().requires_grad_(True), scores.clone().requires_grad_(True)
+        loss = crit(lo2, sc2, boxes, labels)
+        if loss.grad_fn is not None and 'FusedLossFn' in loss.grad_fn.name():
+            seen_native += 1
+        expect_native += B in sizes   # a batch size this stream has seen: its buffers exist
+        sizes.add(B)
+        comps = crit.last_components
+        if how == 'plain':
+            ref.backward()
+            loss.backward()
+        elif how == 'unit':
+            ref.backward(core.unit_grad(DEV))
+            loss.backward(core.unit_grad(DEV))
+        else:
+            (ref * 3.0).backward()
+            (loss * 3.0).backward()
+        assert torch.equal(loss.detach(), ref.detach()), (i, float(loss), float(ref))
+        assert torch.equal(comps, ref_c), i
+        assert torch.equal(lo2.grad, lo1.grad) and torch.equal(sc2.grad, sc1.grad), i
+    assert seen_native == expect_native == 3, (seen_native, expect_native)
+
+
+def test_native_criterion_call_no_grad_and_errors():
+    Pt = torch.from_numpy(prior_table('SSD512')).to(DEV)
+    crit = CR.MultiBoxLoss512(priors_cxcy=Pt, config=Cfg(reg_weights=1.0, device=DEV, n_classes=21, reg_loss='diou',
+                                                          cls_loss='focal'))
+    boxes, labels, locs, scores = _inputs(4, 91, Pt.shape[0])
+    crit(locs, scores, boxes, labels)   # sets up the stream's buffers
+    with torch.no_grad():
+        loss = crit(locs, scores, boxes, labels)
+    assert loss.grad_fn is None and torch.isfinite(loss)
+    # an image without objects: the reference's error (max of an empty overlap matrix), from the
+    # Python path the native call hands the batch back to
+    boxes[1] = boxes[1][:0]
+    labels[1] = labels[1][:0]
+    with pytest.raises(Exception):
+        crit(locs, scores, boxes, labels)
