@@ -27,6 +27,12 @@ def _inputs(B, seed, P, dtype=torch.float32):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 def test_native_criterion_call_equals_python_path(dtype):
+    with torch.cuda.stream(torch.cuda.Stream()):   # a fresh stream: no per-stream buffers yet
+        _native_vs_python(dtype)
+    torch.cuda.synchronize()
+
+
+def _native_vs_python(dtype):
     Pt = torch.from_numpy(prior_table('SSD512')).to(DEV)
     cfg = Cfg(reg_weights=1.0, device=DEV, n_classes=21, reg_loss='diou', cls_loss='focal')
     crit = CR.MultiBoxLoss512(priors_cxcy=Pt, config=cfg)
