@@ -917,8 +917,8 @@ def main():
     others = {}
     for k in ('k_multibox', 'k_det_prepare'):
         if k != dominant and k in kernel_us:
-            _, nk, sk, _, _ = alone(k)
-            others[k] = (nk, sk)
+            _, nk, sk, w0, w1 = alone(k)
+            others[k] = (nk, sk, w0, w1)
 
     eager_ms = None
     api = None
@@ -1033,8 +1033,8 @@ def main():
     line['roofline_other'] = {
         k: {'avg_us': round(sk * 1e6, 2), 'launches_timed': nk, 'in_step_avg_us': kernel_us.get(k),
             'algorithmic_bytes_per_launch': ALGO_BYTES[k](wl),
-            'frac': round(ALGO_BYTES[k](wl) / sk / 1e9 / HBM_PEAK_GBS, 4)}
-        for k, (nk, sk) in others.items()}
+            'frac': round(ALGO_BYTES[k](wl) / sk / 1e9 / HBM_PEAK_GBS, 4), 'trace_window_ns': [w0, w1]}
+        for k, (nk, sk, w0, w1) in others.items()}
     line['kernel_us_per_step'] = kernel_us
     line['kernel_launches_timed'] = kernel_n
     line['resident_batches'] = len(st.batches)

@@ -44,7 +44,13 @@ def main(bench_json, trace_csv, out=None, prof_log=None):
     if prof_log:
         for ln in open(prof_log):
             if ln.startswith('{') and '"roofline"' in ln:
-                win = json.loads(ln)['roofline'].get('trace_window_ns')
+                pl = json.loads(ln)
+                # the timing pass of the headline kernel in the profiled run: its own roofline when
+                # the profiled run picked the same kernel, else its roofline_other entry
+                if pl['roofline'].get('kernel') == rl['kernel']:
+                    win = pl['roofline'].get('trace_window_ns')
+                else:
+                    win = (pl.get('roofline_other') or {}).get(rl['kernel'], {}).get('trace_window_ns')
     def keys_of(name):
         # k_multibox<..., true> is the one-launch criterion (its KernelTimer name: k_criterion)
         if 'k_multibox<' in name:
