@@ -32,5 +32,12 @@ for ln in sys.stdin:
     r=json.loads(ln); print('$name', r['config'][-22:], 'ms', r['ms'], 'eager', r.get('eager_ms'))"
 }
 run product ''
-for v in "$@"; do run $v $LIBV/libsbod_hip_$v.so; done
+for v in "$@"; do
+  if [ -n "$TESTS" ]; then   # the variant's DCN parity tests first
+    SBOD_LIB=$LIBV/$v/libsbod_hip.so timeout -k 10 400 python -u -m pytest tests/test_gpu_dcn.py -q -x --timeout 120 \
+      --timeout-method thread > $O/kab_${TAG}_${v}_tests.log 2>&1 || { echo "$v tests failed"; tail -30 $O/kab_${TAG}_${v}_tests.log; exit 1; }
+    tail -1 $O/kab_${TAG}_${v}_tests.log
+  fi
+  run $v $LIBV/$v/libsbod_hip.so
+done
 echo EXIT 0

@@ -2,8 +2,10 @@
 // semantics (offset channels [rows | cols], p_0 = 1 + idx * stride, floor of the UNclamped p,
 // corners and p clamped to the zero-padded map, sigmoid modulation, k x k stride-k conv, no bias).
 //
-// The contraction runs on fp32 MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, one rounding
-// per step) so results stay within fp32 tolerance of the reference.  GEMM views, with
+// The contractions keep fp32-level accuracy: the forward's on the bf16 matrix cores with every
+// fp32 operand split into three bf16 parts (six products per pair, split3 / mfma6 below: the
+// dropped terms are below 2^-26 relative), the backward's on fp32 MFMA (v_mfma_f32_32x32x2_f32:
+// exact f32 products, one rounding per step).  GEMM views, with
 // M = B*Ho*Wo output pixels, N = k*k kernel points and the reduction index ordered K' = n*C + c
 // (a permutation of conv.weight's c*N + n, applied to the weight copies below):
 //   forward      out[o, m]   = sum_K' Wf[o, K'] * cols[K', m]
@@ -21,13 +23,20 @@
 
 #include "sbod_common.h"
 
+// The forward's contraction on the split-bf16 matrix cores (k_dcn_fwd3) unless an A/B build asks
+// for the fp32-MFMA kernel (-DSBOD_DCN_FP32_FWD); the backward-data split form is a variant only
+// (-DSBOD_DCN_SPLIT_BF16: measured no faster).
+#ifndef SBOD_DCN_FP32_FWD
+#define SBOD_DCN_SPLIT_FWD 1
+#endif
+
 namespace sbod {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-#ifdef SBOD_DCN_SPLIT_BF16
+#if defined(SBOD_DCN_SPLIT_BF16) || defined(SBOD_DCN_SPLIT_FWD)
 // ---- split-bf16 contraction (the fp32 products on the bf16 matrix cores).  An fp32 value is the
 // exact sum of three bf16 parts, x = h + m + l (h = bf16(x) round-to-nearest-even, m =
 // bf16(x - h), l = x - h - m: 24 significant bits = 3 x 8, every subtraction exact).  A product
@@ -70,7 +79,7 @@ __device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[
   return acc;
 }
 
-#endif  // SBOD_DCN_SPLIT_BF16
+#endif  // split-bf16 helpers
 
 constexpr int kDcnThreads = 256;
 constexpr int kMaxN = 49;      // k*k <= 49 (k <= 7)
@@ -414,6 +423,163 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_FWD_WAVES : 2) voi
       }
   }
 }
+
+#ifdef SBOD_DCN_SPLIT_FWD
+// The forward contraction on the split-bf16 matrix cores (mfma6): k_dcn_fwd's blocking, gathers,
+// coefficient staging and K'-tile order, with (1) the weights' split parts precomputed
+// (wf3 [3][O][N*C] bf16, k_wf_split) and loaded as 16-byte vectors of 8 consecutive channels into
+// the A registers, (2) each combined column value split once by the thread that samples it and
+// stored as three bf16 rows (LDS [buf][part][pixel][channel], a 40-element pitch: conflict-free
+// 16-byte reads) — 48 bf16 MFMAs per K'-tile and wave instead of 64 fp32 ones at twice the cycles.
+// C % 8 == 0 (16-byte weight vectors).
+constexpr int kF3Pitch = 40;
+__global__ __launch_bounds__(256) void k_wf_split(const float *__restrict__ wf, int64_t n, __bf16 *__restrict__ wf3) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  __bf16 h, m, l;
+  split3(wf[i], h, m, l);
+  wf3[i] = h;
+  wf3[n + i] = m;
+  wf3[2 * n + i] = l;
+}
+
+__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd3(DcnShape s, const float *__restrict__ xt,
+                                                                            const Coef *__restrict__ coef,
+                                                                            const __bf16 *__restrict__ wf3,
+                                                                            float *__restrict__ out, int atomic_out) {
+  __shared__ __attribute__((aligned(16))) __bf16 s_cols[2][3][kFM][kF3Pitch];
+  extern __shared__ float s_coefd[];        // dynamic [N][9][kFM]: idx[4] | g[4] | mask of each pixel
+  float (*s_coef)[9][kFM] = reinterpret_cast<float (*)[9][kFM]>(s_coefd);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const Tile3 tl = xcd_tile(gridDim.x, gridDim.y, gridDim.z);
+  const int m0 = tl.x * kFM, o0 = tl.y * 256;
+  const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
+  const int CT = (s.C + kFKC - 1) / kFKC, T = s.N * CT;
+  const int t0 = static_cast<int>(static_cast<int64_t>(tl.z) * T / gridDim.z);
+  const int t1 = static_cast<int>(static_cast<int64_t>(tl.z + 1) * T / gridDim.z);
+  const int mm = tid & 63, cq = tid >> 6;
+  const int ms = min(m0 + mm, s.M - 1);
+  const float *xb = xt + static_cast<int64_t>(ms / HWo) * HW * s.C;
+  struct Cf {
+    int idx[4];
+    float g[4], m;
+  };
+  for (int e = tid; e < s.N * kFM; e += kDcnThreads) {
+    const int n = e / kFM, px = e - n * kFM;
+    const float *c = reinterpret_cast<const float *>(coef + static_cast<int64_t>(min(m0 + px, s.M - 1)) * s.N + n);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) s_coef[n][j][px] = c[j];
+  }
+  __syncthreads();
+  auto load_coef = [&](int t) {
+    const int n = t % s.N;
+    Cf c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      c.idx[q] = __builtin_bit_cast(int, s_coef[n][q][mm]);
+      c.g[q] = s_coef[n][4 + q][mm];
+    }
+    c.m = s_coef[n][8][mm];
+    return c;
+  };
+  float X[4][8];
+  bool xok[4][2];
+  bf16x8 acur[2][2][3];   // [ri][j][part]: the next tile's weights load once the MFMAs have read these
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  auto gather = [&](int t, const Cf &cf, float (&XX)[4][8], bool (&ok)[4][2]) {
+    const int c0 = (t / s.N) * kFKC + 8 * cq;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float *p = xb + static_cast<int64_t>(max(cf.idx[q], 0)) * s.C;
+#pragma unroll
+      for (int v = 0; v < 8; v += 4) {
+        const int c = c0 + v;
+        ok[q][v / 4] = cf.idx[q] >= 0 && c < s.C;
+        load_vec<4>(p + min(c, s.C - 4), true, &XX[q][v]);
+      }
+    }
+  };
+  auto store_cols = [&](int buf, const Cf &cf, float (&XX)[4][8], const bool (&ok)[4][2]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 8; ++v) XX[q][v] = ok[q][v / 4] ? XX[q][v] : 0.f;
+    float col[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) col[v] = combine(cf.g, cf.m, XX[0][v], XX[1][v], XX[2][v], XX[3][v]);
+    const Split8 sp = split8(col);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8 *>(&s_cols[buf][p][mm][8 * cq]) = sp.p[p];
+  };
+  const int64_t part = static_cast<int64_t>(s.O) * s.K;
+  auto load_a = [&](int t) {   // rows past O are never stored; channels past C meet zero columns
+    const int ct = t / s.N, n = t - ct * s.N;
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int o = min(o0 + 64 * wv + 32 * ri + l31, s.O - 1);
+      const __bf16 *pr = wf3 + static_cast<int64_t>(o) * s.K + static_cast<int64_t>(n) * s.C;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = min(ct * kFKC + 16 * j + 8 * h, s.C - 8);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) acur[ri][j][p] = *reinterpret_cast<const bf16x8 *>(pr + p * part + c);
+      }
+    }
+  };
+  if (t0 < t1) {
+    Cf cf = load_coef(t0);
+    gather(t0, cf, X, xok);
+    store_cols(0, cf, X, xok);
+    load_a(t0);
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+      const int buf = (t - t0) & 1;
+      const int tn = min(t + 1, t1 - 1);   // the last pass re-gathers its own tile into the idle buffer
+      cf = load_coef(tn);
+      gather(tn, cf, X, xok);
+      __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bf16x8 b[2][3];
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[bq][p] = *reinterpret_cast<const bf16x8 *>(&s_cols[buf][p][32 * bq + l31][16 * j + 8 * h]);
+#pragma unroll
+        for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+          for (int bq = 0; bq < 2; ++bq) acc[ri][bq] = mfma6(acur[ri][j], b[bq], acc[ri][bq]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      load_a(tn);   // L2-resident weights, in flight through the column store and barrier
+      store_cols(buf ^ 1, cf, X, xok);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int bq = 0; bq < 2; ++bq) {
+    const int m = m0 + 32 * bq + l31;
+    if (m >= s.M) continue;
+    const int b = m / HWo, pix = m - b * HWo;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o >= s.O) continue;
+        float *dst = out + (static_cast<int64_t>(b) * s.O + o) * HWo + pix;
+        if (atomic_out) atomicAdd(dst, acc[a][bq][r]);
+        else *dst = acc[a][bq][r];
+      }
+  }
+}
+#endif  // SBOD_DCN_SPLIT_FWD
 
 // ----------------------------------------------------------------------------- backward (data)
 // Block: 64 pixels x 256 channels for ONE kernel point n (blockIdx.z).  dcols[m, n, c] =
@@ -1111,6 +1277,9 @@ inline bool shape_ok(const DcnShape &s) { return s.B > 0; }
 struct DcnState {
   Coef *coef;
   float *xt, *wf;
+#ifdef SBOD_DCN_SPLIT_FWD
+  __bf16 *wf3;        // [3][O][N*C] split parts of Wf (the split-bf16 forward)
+#endif
   uint32_t *tcount;   // training: [B*H*W + 1] corner samples per input pixel
 #ifndef SBOD_DCN_SPLIT_BF16
   float *wb;          // training: Wb [N][O][C] (A/B build: the fp32-MFMA backward-data kernel)
@@ -1149,6 +1318,9 @@ size_t carve_state(const DcnShape &s, void *base, DcnState *w, bool train) {
   t.coef = reinterpret_cast<Coef *>(take(static_cast<size_t>(s.M) * s.N * sizeof(Coef)));
   t.xt = reinterpret_cast<float *>(take(npix * s.C * 4));
   t.wf = reinterpret_cast<float *>(take(wbytes));
+#ifdef SBOD_DCN_SPLIT_FWD
+  t.wf3 = reinterpret_cast<__bf16 *>(take(static_cast<size_t>(s.O) * s.K * 6));
+#endif
   if (train) {
     t.tcount = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
 #ifndef SBOD_DCN_SPLIT_BF16
@@ -1240,6 +1412,13 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
     SBOD_LAUNCHED("k_wb_split");
   }
 #endif
+#ifdef SBOD_DCN_SPLIT_FWD
+  {
+    const int64_t nw = static_cast<int64_t>(s.O) * s.K;
+    hipLaunchKernelGGL(k_wf_split, dim3((nw + 255) / 256), dim3(256), 0, hs, static_cast<const float *>(st.wf), nw, st.wf3);
+    SBOD_LAUNCHED("k_wf_split");
+  }
+#endif
   return SBOD_OK;
 }
 
@@ -1252,6 +1431,18 @@ static int dcn_forward(const DcnShape &s, const DcnState &st, float *out, int sp
     if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess)
       return launch_status("hipFuncSetAttribute(k_dcn_fwd LDS)");
   }
+#ifdef SBOD_DCN_SPLIT_FWD
+  if (s.C % 8 == 0) {
+    if (lds > 48 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(k_dcn_fwd3), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds)) != hipSuccess)
+      return launch_status("hipFuncSetAttribute(k_dcn_fwd3 LDS)");
+    hipLaunchKernelGGL(k_dcn_fwd3, grid, dim3(kDcnThreads), lds, hs, s, st.xt, st.coef,
+                       static_cast<const __bf16 *>(st.wf3), out, split > 1 ? 1 : 0);
+    SBOD_LAUNCHED("k_dcn_fwd3");
+    return SBOD_OK;
+  }
+#endif
   if (s.C % 4 == 0)
     hipLaunchKernelGGL(k_dcn_fwd<4>, grid, dim3(kDcnThreads), lds, hs, s, st.xt, st.coef, st.wf, out, split > 1 ? 1 : 0);
   else
