@@ -1245,6 +1245,221 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_WGRAD_WAVES : 1) v
     }
 }
 
+#ifdef SBOD_DCN_SPLIT_FWD
+// The weight-gradient contraction on the split-bf16 matrix cores (mfma6), for the common case
+// (C % 4 == 0, 32-pixel chunks inside one image): the sampler splits each column value once into
+// three bf16 rows of LDS [buf][part][channel][pixel] (pixels, the MFMA's K, contiguous; a 40-element
+// pitch), and each wave splits its own dout rows (8 consecutive pixels per 16-byte pair of loads)
+// right before the MFMAs.  The offset / mask gradients are the fp32 kernel's, from the same samples.
+template <bool DOFS>
+__global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight3(
+    DcnShape s, const float *__restrict__ xt, const Coef *__restrict__ coef,
+    const float *__restrict__ gout, float *__restrict__ gwp, int m_slice,
+    const float *__restrict__ dcols, float *__restrict__ goff, float *__restrict__ gmlog) {
+  constexpr int VEC = 4;
+  constexpr bool AVEC = true;
+  __shared__ __attribute__((aligned(16))) __bf16 s_cb[2][3][kWC][kF3Pitch];   // B operand [part][c][m]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const Tile3 tl = xcd_tile(gridDim.x, gridDim.y, gridDim.z);   // one pixel slice's tiles share an L2
+  // kernel point fastest: the N blocks of one channel block and pixel slice (the same corner
+  // lines, dout rows) run side by side on one XCD
+  const int cb = tl.x / s.N, n = tl.x - cb * s.N, c0 = cb * kWC;
+  const int ms0 = tl.y * m_slice, o0 = tl.z * 256;
+  const int mend = min(ms0 + m_slice, s.M);
+  const int HWo = s.Ho * s.Wo, HW = s.H * s.W;
+  const int smm = tid >> 3, scg = (tid & 7) * 8;
+  const bool oblk0 = tl.z == 0;   // offset / mask gradients from output-channel block 0 only
+  const bool dow = gwp != nullptr;
+  // Every operand load is unconditional (pixels past the slice read a clamped pixel and their
+  // columns are stored as zeros; corners outside the map and channels past C are zeroed at the
+  // store), so the loop is straight-line code: the waits before the MFMAs cover the dout rows
+  // they read, not the next chunk's gathers in flight.
+  struct CfW {
+    int idx[4];
+    float g[4], m, tlx, rbx, tly, rby;
+    int inr;
+  };
+  // Address arithmetic.  AVEC (every 32-pixel chunk whole and inside one image): the chunk's
+  // image and first pixel are wave-uniform (scalar unit), the per-lane parts (channel offsets,
+  // this lane's pixel row / output channel rows) are loop-invariant 32-bit offsets, so a chunk
+  // costs one 64-bit add per load instead of divisions and 64-bit multiply-adds per lane.
+  int cofs[8 / VEC];   // this lane's channel offsets, clamped into the row
+#pragma unroll
+  for (int v = 0; v < 8; v += VEC) cofs[v / VEC] = min(c0 + scg + v, s.C - VEC);
+  const int lane_cf = smm * s.N;                       // coef rows of this lane's pixel
+  const int lane_dc = smm * s.N * s.C;                 // dcols rows of this lane's pixel
+  int lane_o[2];                                       // dout rows (o * HWo) of this lane
+#pragma unroll
+  for (int ri = 0; ri < 2; ++ri) lane_o[ri] = min(o0 + 64 * wv + 32 * ri + l31, s.O - 1) * HWo;
+  auto load_cf = [&](int m0) {
+    const Coef *cp = AVEC ? coef + (static_cast<int64_t>(m0) * s.N + n) + lane_cf
+                          : coef + static_cast<int64_t>(min(m0 + smm, mend - 1)) * s.N + n;
+    const float *c = reinterpret_cast<const float *>(cp);
+    float2 w[7];   // a Coef is 8-byte aligned (56 bytes)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) w[j] = reinterpret_cast<const float2 *>(c)[j];
+    return CfW{{__builtin_bit_cast(int, w[0].x), __builtin_bit_cast(int, w[0].y), __builtin_bit_cast(int, w[1].x),
+                __builtin_bit_cast(int, w[1].y)},
+               {w[2].x, w[2].y, w[3].x, w[3].y}, w[4].x, w[4].y, w[5].x, w[5].y, w[6].x, __builtin_bit_cast(int, w[6].y)};
+  };
+  float X[4][8], D[8];
+  bool xok[4][8 / VEC];
+  float acur[2][2][8], anext[2][2][8];
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  auto gather = [&](int m0, const CfW &cf) {
+    const float *xb;
+    if (AVEC) {
+      xb = xt + static_cast<int64_t>(m0 / HWo) * HW * s.C;   // uniform
+    } else {
+      const int m = min(m0 + smm, mend - 1);
+      xb = xt + static_cast<int64_t>(m / HWo) * HW * s.C;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // corner pixel * C: both factors < 2^24 (per-image sizes are validated below 2^31)
+      const float *p = xb + __umul24(static_cast<uint32_t>(max(cf.idx[q], 0)), static_cast<uint32_t>(s.C));
+#pragma unroll
+      for (int v = 0; v < 8; v += VEC) {
+        xok[q][v / VEC] = cf.idx[q] >= 0 && c0 + scg + v < s.C;
+        load_vec<VEC>(p + cofs[v / VEC], true, &X[q][v]);
+      }
+    }
+    if constexpr (DOFS) {
+      const float *dr = AVEC ? dcols + (static_cast<int64_t>(m0) * s.N + n) * s.C + lane_dc
+                             : dcols + (static_cast<int64_t>(min(m0 + smm, mend - 1)) * s.N + n) * s.C;
+#pragma unroll
+      for (int v = 0; v < 8; v += VEC) load_vec<VEC>(dr + cofs[v / VEC], true, &D[v]);
+    }
+  };
+  // live: this chunk's offset / mask partials are added (false for the prefetch past the last).
+  // The column value and the offset / mask partials use fused multiply-adds (the weight and
+  // offset / mask gradients are checked to fp32 tolerance, not bit-exactly):
+  //   raw = g0 X0 + g1 X1 + g2 X2 + g3 X3,
+  //   d/dx = (1 + tly)(X3 - X0) + (1 - rby)(X1 - X2),  d/dy = (1 + tlx)(X2 - X0) + (1 - rbx)(X1 - X3)
+  // (Deformable_convolution.py:59-91 by autograd, corners lt, rb, lb, rt).
+  auto store_cols = [&](int buf, const CfW &cf, int m0, bool live) {
+    const bool ok = AVEC || m0 + smm < mend;
+    const float cm = cf.m;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 8; ++v) X[q][v] = (ok && xok[q][v / VEC]) ? X[q][v] : 0.f;
+    float pm = 0.f, ppx = 0.f, ppy = 0.f;
+    const float ay = 1.f + cf.tly, by = 1.f - cf.rby, ax = 1.f + cf.tlx, bx = 1.f - cf.rbx;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const float raw = __builtin_fmaf(cf.g[3], X[3][v], __builtin_fmaf(cf.g[2], X[2][v],
+                                       __builtin_fmaf(cf.g[1], X[1][v], cf.g[0] * X[0][v])));
+      __bf16 hp, mp, lp;
+      split3(raw * cm, hp, mp, lp);
+      s_cb[buf][0][scg + v][smm] = hp;
+      s_cb[buf][1][scg + v][smm] = mp;
+      s_cb[buf][2][scg + v][smm] = lp;
+      if constexpr (DOFS) {
+        const float d = c0 + scg + v < s.C ? D[v] : 0.f;
+        pm = __builtin_fmaf(d, raw, pm);
+        ppx = __builtin_fmaf(d, __builtin_fmaf(ay, X[3][v] - X[0][v], by * (X[1][v] - X[2][v])), ppx);
+        ppy = __builtin_fmaf(d, __builtin_fmaf(ax, X[2][v] - X[0][v], bx * (X[1][v] - X[3][v])), ppy);
+      }
+    }
+    if constexpr (DOFS) {   // the 8 lanes of this pixel are lanes 8k..8k+7: quad swaps + half-row mirror
+      if (live && oblk0) {
+        pm += dpp_f32_or0<0xB1, 0xf>(pm);
+        ppx += dpp_f32_or0<0xB1, 0xf>(ppx);
+        ppy += dpp_f32_or0<0xB1, 0xf>(ppy);
+        pm += dpp_f32_or0<0x4E, 0xf>(pm);
+        ppx += dpp_f32_or0<0x4E, 0xf>(ppx);
+        ppy += dpp_f32_or0<0x4E, 0xf>(ppy);
+        pm += dpp_f32_or0<0x141, 0xf>(pm);
+        ppx += dpp_f32_or0<0x141, 0xf>(ppx);
+        ppy += dpp_f32_or0<0x141, 0xf>(ppy);
+        if ((tid & 7) == 0 && ok) {
+          const int m = m0 + smm, b = m / HWo, pix = m - b * HWo;
+          if (goff) {
+            atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + n) * HWo + pix, (cf.inr & 1) ? ppx * cm : 0.f);
+            atomicAdd(goff + (static_cast<int64_t>(b) * 2 * s.N + s.N + n) * HWo + pix, (cf.inr & 2) ? ppy * cm : 0.f);
+          }
+          if (gmlog) atomicAdd(gmlog + (static_cast<int64_t>(b) * s.N + n) * HWo + pix, pm * cm * (1.f - cm));
+        }
+      }
+    }
+  };
+  auto load_a = [&](int m0, float (&a)[2][2][8]) {   // dout rows: pixels m0 + 16 j + 8 h + 0..7
+    const int b = m0 / HWo;   // uniform (32-pixel chunks inside one image)
+    const float *pb = gout + static_cast<int64_t>(b) * s.O * HWo + (m0 - b * HWo) + 8 * h;
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 8; v += 4) load_vec<4>(pb + lane_o[ri] + 16 * j + v, true, &a[ri][j][v]);
+  };
+
+  if (ms0 < mend) {
+    const int nch = (mend - ms0 + kWMs - 1) / kWMs;
+    CfW cf = load_cf(ms0);
+    gather(ms0, cf);
+    store_cols(0, cf, ms0, true);
+    load_a(ms0, acur);
+    CfW cn = load_cf(ms0 + min(1, nch - 1) * kWMs);   // coefficients one chunk ahead of the gathers
+    __syncthreads();
+    for (int i = 0; i < nch; ++i) {
+      const int buf = i & 1;
+      const int mn = ms0 + min(i + 1, nch - 1) * kWMs;   // the last pass re-gathers its own chunk
+      cf = cn;
+      gather(mn, cf);
+      load_a(mn, anext);
+      cn = load_cf(ms0 + min(i + 2, nch - 1) * kWMs);
+      __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bf16x8 bb[2][3];
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bb[bq][p] = *reinterpret_cast<const bf16x8 *>(&s_cb[buf][p][32 * bq + l31][16 * j + 8 * h]);
+#pragma unroll
+        for (int ri = 0; ri < 2; ++ri) {
+          const Split8 sa = split8(acur[ri][j]);
+#pragma unroll
+          for (int bq = 0; bq < 2; ++bq) acc[ri][bq] = mfma6(sa.p, bb[bq], acc[ri][bq]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      store_cols(buf ^ 1, cf, mn, i + 1 < nch);
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int v = 0; v < 8; ++v) acur[ri][j][v] = anext[ri][j][v];
+      __syncthreads();
+    }
+  }
+  if (!dow) return;   // (offset / mask gradients only: the MFMA result is not wanted)
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bq = 0; bq < 2; ++bq) {
+      const int c = c0 + 32 * bq + l31;
+      if (c >= s.C) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.N + n) * s.C + c, acc[a][bq][r]);
+      }
+    }
+}
+
+#endif  // SBOD_DCN_SPLIT_FWD (the split weight gradient)
+
 // A shape whose sizes are non-positive, out of range or overflow 32-bit indexing comes back with
 // every field 0 (shape_ok() false): no division by a zero stride, no signed overflow in the
 // products, and the size queries return 0 for it.
@@ -1537,13 +1752,22 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
         hipLaunchKernelGGL(kern, grid, dim3(kDcnThreads), 0, hs, s, st.xt, st.coef, grad_out, grad_weight ? sc.gwp : nullptr, m_slice, dc,
                            grad_offset, grad_mask_logits);
       };
+#if defined(SBOD_DCN_SPLIT_FWD) && !defined(SBOD_DCN_FP32_WGRAD)
+      constexpr bool split = true;   // the split-bf16 weight gradient (A/B build: -DSBOD_DCN_FP32_WGRAD)
+#else
+      constexpr bool split = false;
+#endif
       if (dc) {
-        if (s.C % 4 == 0 && avec) go(k_dcn_bwd_weight<4, true, true>);
-        else if (s.C % 4 == 0) go(k_dcn_bwd_weight<4, false, true>);
+        if (s.C % 4 == 0 && avec) {
+          if constexpr (split) go(k_dcn_bwd_weight3<true>);
+          else go(k_dcn_bwd_weight<4, true, true>);
+        } else if (s.C % 4 == 0) go(k_dcn_bwd_weight<4, false, true>);
         else go(k_dcn_bwd_weight<1, false, true>);
       } else {
-        if (s.C % 4 == 0 && avec) go(k_dcn_bwd_weight<4, true, false>);
-        else if (s.C % 4 == 0) go(k_dcn_bwd_weight<4, false, false>);
+        if (s.C % 4 == 0 && avec) {
+          if constexpr (split) go(k_dcn_bwd_weight3<false>);
+          else go(k_dcn_bwd_weight<4, true, false>);
+        } else if (s.C % 4 == 0) go(k_dcn_bwd_weight<4, false, false>);
         else go(k_dcn_bwd_weight<1, false, false>);
       }
     }
