@@ -741,8 +741,10 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data3(
   const bool mok = m0 + mm < s.M;
   const int sb = msc / HWo, spix = msc - sb * HWo;
   const float *gp = gout + (static_cast<int64_t>(sb) * s.O) * HWo + spix;   // + o * HWo
-  float dstage[kSt];
-  auto load_dout = [&](int oc) {
+  // two dout staging sets: chunk oc+2's loads are in flight while chunk oc+1's are split and stored
+  // and chunk oc's MFMAs run (the split MFMAs leave too little time to cover one chunk of lead)
+  float dA[kSt], dB[kSt];
+  auto load_dout = [&](int oc, float (&dstage)[kSt]) {
 #pragma unroll
     for (int i = 0; i < kSt; ++i) {
       const int o = oc * kBOC + og * kSt + i;
@@ -750,7 +752,7 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data3(
       dstage[i] = (mok && o < s.O) ? v : 0.f;
     }
   };
-  auto store_dout = [&](int buf) {
+  auto store_dout = [&](int buf, float (&dstage)[kSt]) {
     if constexpr (kSt == 8) {
       const Split8 sp = split8(dstage);
 #pragma unroll
@@ -775,7 +777,7 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data3(
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
     brow[ci] = wb3 + (static_cast<int64_t>(n) * s.C + min(cgb + 64 * wv + 32 * ci + l31, s.C - 1)) * Op + 8 * h;
-  bf16x8 bcur[2][2][3], bnext[2][2][3];   // [ci][j][part]; the next chunk's in flight a whole chunk ahead
+  bf16x8 b0[2][2][3], b1[2][2][3];   // [ci][j][part]; the next chunk's in flight a whole chunk ahead
   auto load_b = [&](int oc, bf16x8 (&bb)[2][2][3]) {
 #pragma unroll
     for (int ci = 0; ci < 2; ++ci)
@@ -792,16 +794,15 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data3(
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  load_dout(0);
-  store_dout(0);
-  load_b(0, bcur);
+  load_dout(0, dA);
+  store_dout(0, dA);
+  load_b(0, b0);
+  load_dout(min(1, OT - 1), dA);
   __syncthreads();
-  for (int oc = 0; oc < OT; ++oc) {
+  auto step = [&](int oc, bf16x8 (&bc)[2][2][3], bf16x8 (&bn)[2][2][3], float (&dcur)[kSt], float (&dnext)[kSt]) {
     const int buf = oc & 1;
-    const bool more = oc + 1 < OT;
-    const int ocn = more ? oc + 1 : oc;
-    load_dout(ocn);
-    load_b(ocn, bnext);
+    load_dout(min(oc + 2, OT - 1), dnext);
+    load_b(min(oc + 1, OT - 1), bn);
     __builtin_amdgcn_sched_barrier(0);   // the prefetch stays ahead of the MFMAs
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -813,18 +814,18 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_data3(
 #pragma unroll
       for (int ri = 0; ri < R; ++ri)
 #pragma unroll
-        for (int ci = 0; ci < 2; ++ci) acc[ri][ci] = mfma6(a[ri], bcur[ci][j], acc[ri][ci]);
+        for (int ci = 0; ci < 2; ++ci) acc[ri][ci] = mfma6(a[ri], bc[ci][j], acc[ri][ci]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (more) store_dout(buf ^ 1);
-#pragma unroll
-    for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) bcur[ci][j][p] = bnext[ci][j][p];
+    if (oc + 1 < OT) store_dout(buf ^ 1, dcur);
     __syncthreads();
+  };
+  int oc = 0;
+  for (; oc + 1 < OT; oc += 2) {
+    step(oc, b0, b1, dA, dB);
+    step(oc + 1, b1, b0, dB, dA);
   }
+  if (oc < OT) step(oc, b0, b1, dA, dB);
   // epilogue: row m = 32 ri + (r&3) + 8 (r>>2) + 4 h, column c = cgb + 64 wv + 32 ci + l31
 #pragma unroll
   for (int ri = 0; ri < R; ++ri)
