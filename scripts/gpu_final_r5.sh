@@ -38,4 +38,5 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmcf_$TAG -o run --output-f
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmcw_$TAG -o run --output-format csv -- \
     python bench.py --steps 20 --warmup 5 --no-dcn --no-cpu-baseline --no-c2 > $O/pmcw_$TAG.log 2>&1 || { echo "pmc write failed"; tail -5 $O/pmcw_$TAG.log; exit 1; }
 python scripts/pmc_traffic.py $O/pmcf_$TAG $O/pmcw_$TAG --out $O/pmc_traffic_$TAG.json | tail -12
+bash scripts/gpu_dcn_pmc.sh $TAG > $O/dcn_pmc_$TAG.log 2>&1 || { echo "dcn pmc failed"; tail -5 $O/dcn_pmc_$TAG.log; exit 1; }
 echo EXIT 0
