@@ -1232,6 +1232,9 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_WGRAD_WAVES : 1) v
     }
   }
   if (!dow) return;   // (offset / mask gradients only: the MFMA result is not wanted)
+  // this pixel slice's partial dWp: plain stores into its own [O][N][C] plane (k_wgrad_fold sums
+  // the planes in slice order: deterministic, no far atomics)
+  float *gws = gwp + static_cast<int64_t>(tl.y) * s.O * s.K;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1241,7 +1244,7 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_WGRAD_WAVES : 1) v
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.N + n) * s.C + c, acc[a][bq][r]);
+        if (o < s.O) gws[(static_cast<int64_t>(o) * s.N + n) * s.C + c] = acc[a][bq][r];
       }
     }
 }
@@ -1445,6 +1448,9 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight3(
     }
   }
   if (!dow) return;   // (offset / mask gradients only: the MFMA result is not wanted)
+  // this pixel slice's partial dWp: plain stores into its own [O][N][C] plane (k_wgrad_fold sums
+  // the planes in slice order: deterministic, no far atomics)
+  float *gws = gwp + static_cast<int64_t>(tl.y) * s.O * s.K;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1454,7 +1460,7 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_bwd_weight3(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int o = o0 + 64 * wv + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (o < s.O) atomicAdd(gwp + (static_cast<int64_t>(o) * s.N + n) * s.C + c, acc[a][bq][r]);
+        if (o < s.O) gws[(static_cast<int64_t>(o) * s.N + n) * s.C + c] = acc[a][bq][r];
       }
     }
 }
@@ -1514,6 +1520,25 @@ struct DcnScratch {
   size_t scan_bytes;
 };
 
+// The weight gradient's pixel slices: one round of resident blocks (256 CUs x 2) over the
+// (channel block x kernel point) x output-channel-block tiles (a partial second round would double
+// the time), each slice a whole number of 32-pixel chunks.  The workspace holds one dWp plane per
+// slice (carve_scratch sizes it with the weight gradient wanted, the largest count of tiles).
+struct WgSplit {
+  int gx, gz, slices, m_slice;
+};
+WgSplit wgrad_split(const DcnShape &s, bool grad_weight) {
+  WgSplit w;
+  w.gx = s.N * ((s.C + kWC - 1) / kWC);
+  w.gz = grad_weight ? (s.O + 255) / 256 : 1;
+  int slices = std::max(1, SBOD_WG_TARGET / (w.gx * w.gz));
+  slices = std::max(1, std::min(slices, (s.M + kWMs - 1) / kWMs));
+  int m_slice = (s.M + slices - 1) / slices;
+  w.m_slice = (m_slice + kWMs - 1) / kWMs * kWMs;
+  w.slices = (s.M + w.m_slice - 1) / w.m_slice;
+  return w;
+}
+
 size_t dcn_scan_bytes(int64_t n) {
   if (n <= kScanOneBlock) return 0;
   size_t b = 0;
@@ -1557,7 +1582,7 @@ size_t carve_scratch(const DcnShape &s, void *base, DcnScratch *w) {
   const size_t npix = static_cast<size_t>(s.B) * s.H * s.W;
   DcnScratch t{};
   t.dcols = reinterpret_cast<float *>(take(rows * s.C * 4));
-  t.gwp = reinterpret_cast<float *>(take(static_cast<size_t>(s.O) * s.K * 4));
+  t.gwp = reinterpret_cast<float *>(take(static_cast<size_t>(wgrad_split(s, true).slices) * s.O * s.K * 4));
   t.cur = reinterpret_cast<uint32_t *>(take((npix + 1) * 4));
   t.ent = reinterpret_cast<DxEnt *>(take(rows * 4 * sizeof(DxEnt)));
   t.scan_bytes = dcn_scan_bytes(static_cast<int64_t>(npix) + 1);
@@ -1581,6 +1606,38 @@ int fwd_split(const DcnShape &s) {
   int split = 1;
   while (split * 2 <= T && mt * og * split < 512 && split < 16) split *= 2;
   return split;
+}
+
+// The weight gradient's finish: dw[o][c][n] = sum over pixel slices (in slice order) of
+// gwp[slice][o][n][c].  One block per (64-channel chunk, output channel): the N x 64 sums read
+// along c (16-byte vectors when C % 4 == 0, the slices' loads in flight together), staged in LDS,
+// written along the [c][n] rows.
+template <int VEC>
+__global__ __launch_bounds__(256) void k_wgrad_fold(const float *__restrict__ gwp, int slices, int64_t plane, int N,
+                                                    int C, float *__restrict__ dw) {
+  __shared__ float t[64][kMaxN + 1];
+  const int c0 = blockIdx.x * 64, o = blockIdx.y;
+  const int nc = min(64, C - c0);
+  const float *src = gwp + static_cast<int64_t>(o) * N * C + c0;
+  constexpr int G = 64 / VEC;   // vectors per 64-channel row
+  for (int e = threadIdx.x; e < N * G; e += blockDim.x) {
+    const int n = e / G, cl = (e - n * G) * VEC;
+    if (cl >= nc) continue;
+    float v[VEC] = {};
+    const float *q = src + static_cast<int64_t>(n) * C + cl;
+#pragma unroll 4
+    for (int sl = 0; sl < slices; ++sl) {
+      float x[VEC];
+      load_vec<VEC>(q + sl * plane, true, x);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) v[k] += x[k];
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) t[cl + k][n] = v[k];
+  }
+  __syncthreads();
+  float *dst = dw + (static_cast<int64_t>(o) * C + c0) * N;
+  for (int e = threadIdx.x; e < nc * N; e += blockDim.x) dst[e] = t[e / N][e % N];
 }
 
 }  // namespace sbod
@@ -1680,7 +1737,6 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
                               static_cast<int64_t>(s.N) * s.O * s.C * 4 < (1ll << 31)),
                "sbod_dcn_bwd: grad_out / weight exceed the 2 GiB buffer-descriptor range");
   const int64_t ob = static_cast<int64_t>(s.M) * s.N;
-  const int64_t wn = static_cast<int64_t>(s.O) * s.K;
   if (grad_x) {   // the input pixels' entry ranges (scan of the counts the forward made)
     if (npix + 1 <= kScanOneBlock) {
       hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, hs, st.tcount, sc.cur, npix + 1);
@@ -1692,12 +1748,11 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
     }
     hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hs, s, st.coef, sc.cur, sc.ent,
                        grad_offset, grad_offset ? 2 * ob : 0, grad_mask_logits, grad_mask_logits ? ob : 0,
-                       grad_weight ? sc.gwp : nullptr, grad_weight ? wn : 0);
+                       nullptr, int64_t(0));
     SBOD_LAUNCHED("k_dcn_dx_fill");
   } else {
     if (grad_offset && hipMemsetAsync(grad_offset, 0, 2 * ob * 4, hs) != hipSuccess) return launch_status("memset");
     if (grad_mask_logits && hipMemsetAsync(grad_mask_logits, 0, ob * 4, hs) != hipSuccess) return launch_status("memset");
-    if (grad_weight && hipMemsetAsync(sc.gwp, 0, wn * 4, hs) != hipSuccess) return launch_status("memset");
   }
   if (need_cols) {
     KernelTimer kt("k_dcn_bwd_data", hs);
@@ -1737,14 +1792,9 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
   if (grad_weight || need_om) {
     // weight gradient, and the offset / mask gradients from the same corner samples (C / 64
     // channel-block partials added into the zeroed outputs)
-    const int gx = s.N * ((s.C + kWC - 1) / kWC), gz = grad_weight ? (s.O + 255) / 256 : 1;
-    // one round of resident blocks (256 CUs x 2): a partial second round would double the time
-    int slices = std::max(1, SBOD_WG_TARGET / (gx * gz));
-    slices = std::max(1, std::min(slices, (s.M + kWMs - 1) / kWMs));
-    int m_slice = (s.M + slices - 1) / slices;
-    m_slice = (m_slice + kWMs - 1) / kWMs * kWMs;
-    slices = (s.M + m_slice - 1) / m_slice;
-    const dim3 grid(gx, slices, gz);
+    const WgSplit wg = wgrad_split(s, grad_weight != nullptr);
+    const int m_slice = wg.m_slice;
+    const dim3 grid(wg.gx, wg.slices, wg.gz);
     const bool avec = (s.Ho * s.Wo) % kWMs == 0;   // 32-pixel chunks never straddle images
     const float *dc = need_om ? sc.dcols : nullptr;
     {
@@ -1773,10 +1823,14 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
       }
     }
     SBOD_LAUNCHED("k_dcn_bwd_weight");
-    if (grad_weight) {   // dWp [O][N][C] -> conv.weight's [O][C][N]
-      hipLaunchKernelGGL(k_transpose, dim3((s.C + 63) / 64, (s.N + 63) / 64, s.O), dim3(256), 0, hs, sc.gwp,
-                         grad_weight, s.N, s.C, nullptr, int64_t(0));
-      SBOD_LAUNCHED("k_transpose(dw)");
+    if (grad_weight) {   // the slices' dWp [O][N][C] planes summed -> conv.weight's [O][C][N]
+      const dim3 fg((s.C + 63) / 64, s.O);
+      const int64_t plane = static_cast<int64_t>(s.O) * s.K;
+      if (s.C % 4 == 0)
+        hipLaunchKernelGGL(k_wgrad_fold<4>, fg, dim3(256), 0, hs, sc.gwp, wg.slices, plane, s.N, s.C, grad_weight);
+      else
+        hipLaunchKernelGGL(k_wgrad_fold<1>, fg, dim3(256), 0, hs, sc.gwp, wg.slices, plane, s.N, s.C, grad_weight);
+      SBOD_LAUNCHED("k_wgrad_fold");
     }
   }
   return SBOD_OK;
