@@ -288,8 +288,11 @@ def test_partial_gradients_match_full_backward(which):
     part = [t.clone().requires_grad_(n in want) for n, t in zip(names, (x, off, ml, w))]
     core.deform_conv2d(*part, ks, 1, 1).backward(gout)
     for n, pf, pp in zip(names, full, part):
-        if n in want:
-            # (the weight gradient combines pixel slices with float atomics: not bit-reproducible)
+        if n == 'weight' and n in want:
+            # the weight gradient's pixel slices are summed in slice order (k_wgrad_fold): bitwise
+            assert torch.equal(pp.grad, pf.grad), 'partial weight not bit-identical'
+        elif n in want:
+            # (dx entries and the offset / mask partials are combined by float atomics)
             np.testing.assert_allclose(_np(pp.grad), _np(pf.grad), rtol=1e-5, atol=1e-6 * _amax(pf.grad),
                                        err_msg='partial ' + n)
         else:
@@ -300,8 +303,9 @@ def test_state_backward_stateless_backward_and_retained_graph():
     """The training form (forward state kept by autograd, sbod_dcn_bwd_state_f32) against the
     C-ABI's stateless sbod_dcn_bwd_f32 (state re-derived in its own workspace), a retained graph's
     second backward (the backward only reads the state) against its first, and the inference
-    forward (no state) against the training forward.  The dx entries and the weight / offset
-    partials are combined by atomics in arbitrary order: equal within fp32 rounding, not bitwise."""
+    forward (no state) against the training forward.  The dx entries and the offset / mask
+    partials are combined by atomics in arbitrary order: equal within fp32 rounding, not bitwise;
+    the weight gradient (per-slice planes summed in slice order) is bitwise."""
     from shape_based_object_detection_amd import _lib as L
     g = torch.Generator(device=DEV).manual_seed(21)
     B, C, O, H, ks = 2, 40, 48, 11, 3
@@ -324,6 +328,7 @@ def test_state_backward_stateless_backward_and_retained_graph():
            L.ptr(ws), nb, L.stream_of(gout))
     torch.cuda.synchronize()
     np.testing.assert_allclose(_np(inf), _np(out), rtol=1e-5, atol=1e-6 * _amax(out), err_msg='inference fwd')
+    assert torch.equal(second[3], first[3]) and torch.equal(stateless[3], first[3]), 'weight gradient not bitwise'
     for n, a, b, c in zip(('x', 'offset', 'mask', 'weight'), first, second, stateless):
         np.testing.assert_allclose(_np(b), _np(a), rtol=1e-5, atol=1e-6 * _amax(a), err_msg='retained ' + n)
         np.testing.assert_allclose(_np(c), _np(a), rtol=1e-5, atol=1e-6 * _amax(a), err_msg='stateless ' + n)
