@@ -370,6 +370,7 @@ class Step:
         self.fast = None
         self.k = 0
         self.pending = collections.deque()
+        self.trace = None   # per-step host stamps of the timed run: (submit start, submit end, collect end)
         self.depth = max(2, int(depth))
         # the recorder sees sbod entry points only: with ranks, the normaliser's RCCL all-reduce
         # (torch.distributed) must be in the replayed work, so data-parallel steps replay graphs
@@ -649,12 +650,14 @@ class Step:
         t1 = time.perf_counter()
         self.host_submit += t1 - t0
         self.pending.append(nxt)
+        out = None
         if len(self.pending) >= self.depth:
             prev = self.pending.popleft()
             out = prev[0], prev[1].wait()
             self.host_collect += time.perf_counter() - t1
-            return out
-        return None
+        if self.trace is not None:
+            self.trace.append((t0, t1, time.perf_counter()))
+        return out
 
     def drain(self):
         """Collect every launched step not collected yet (oldest first)."""
@@ -954,9 +957,31 @@ def main():
         st.host_submit = st.host_collect = 0.0
         # the training loop's current stream is the criterion's: the GT lists it hands over
         # are ordered on the stream that packs them (no cross-stream event pair per step)
+        st.trace = []
+        prof = getattr(L.host_ext, 'submit_profile', None) if L.host_ext is not None else None
+        if prof is not None:
+            prof(True)
         with torch.cuda.stream(st.cap_stream):
+            t_before = time.perf_counter()
             elapsed = timed(st.pipelined, a.steps, dist, dev, finish=st.drain)
+            t_after = time.perf_counter()
         host_submit, host_collect = st.host_submit, st.host_collect
+        tr, st.trace = st.trace, None
+        sub_phases = prof(True) if prof is not None else None
+        # where a short run's time goes: until the first submit starts (barrier + synchronize),
+        # the submits and collects of the K steps, and the drain after the last submit
+        if tr:
+            sub = [(b - a_) * 1e6 for a_, b, _ in tr]
+            run_detail = {'before_first_submit_us': round((tr[0][0] - t_before) * 1e6, 1),
+                          'submit_us_first4': [round(x, 1) for x in sub[:4]],
+                          'submit_us_median': round(sorted(sub)[len(sub) // 2], 1),
+                          'last_submit_to_end_us': round((t_after - tr[-1][1]) * 1e6, 1),
+                          'steps_span_us': round((tr[-1][2] - tr[0][0]) * 1e6, 1)}
+            if sub_phases and sub_phases.get('calls'):
+                nc = sub_phases.pop('calls')
+                run_detail['native_submit_us_per_step'] = {k: round(v / nc, 2) for k, v in sub_phases.items()}
+        else:
+            run_detail = None
         # the in-graph span of the dominant kernel (a host-synchronous read, so outside the
         # timed region): each batch's graph keeps the record of its latest replay, so after
         # every full rotation the query returns len(slots) distinct launches
@@ -1039,6 +1064,7 @@ def main():
     line['kernel_launches_timed'] = kernel_n
     line['resident_batches'] = len(st.batches)
     if st.use_graph:   # host time per step: GT packing + replays, and collecting the lists
+        line['timed_run_detail'] = run_detail
         line['host_us_per_step'] = {'submit': round(host_submit / a.steps * 1e6, 1),
                                     'collect_incl_wait': round(host_collect / a.steps * 1e6, 1)}
     if dp is not None:

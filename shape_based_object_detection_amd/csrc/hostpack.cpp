@@ -26,6 +26,7 @@
 #include <torch/csrc/autograd/custom_function.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <chrono>
 #include <cstdint>
 #include <vector>
 
@@ -299,6 +300,30 @@ PyObject *make_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   return cap;
 }
 
+// Host time of submit_step_program by phase (steady clock, summed over calls; read and reset by
+// submit_profile()): list checks + packing launch, criterion launches, detect launches, event.
+double g_sub_ns[5];
+long long g_sub_calls;
+using SteadyClock = std::chrono::steady_clock;
+inline double ns_since(SteadyClock::time_point &t) {
+  const auto n = SteadyClock::now();
+  const double d = std::chrono::duration<double, std::nano>(n - t).count();
+  t = n;
+  return d;
+}
+
+PyObject *submit_profile(PyObject *, PyObject *const *a, Py_ssize_t n) {
+  const bool reset = n > 0 && PyObject_IsTrue(a[0]) == 1;
+  PyObject *r = Py_BuildValue("{s:L,s:d,s:d,s:d,s:d,s:d}", "calls", g_sub_calls, "pack_us", g_sub_ns[0] / 1e3,
+                              "criterion_us", g_sub_ns[1] / 1e3, "detect_us", g_sub_ns[2] / 1e3, "event_us",
+                              g_sub_ns[3] / 1e3, "total_us", g_sub_ns[4] / 1e3);
+  if (reset) {
+    for (double &v : g_sub_ns) v = 0.0;
+    g_sub_calls = 0;
+  }
+  return r;
+}
+
 PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   if (n != 3) {
     PyErr_SetString(PyExc_TypeError, "submit_step_program(program, boxes, labels)");
@@ -306,6 +331,7 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   }
   auto *p = static_cast<StepProgram *>(PyCapsule_GetPointer(a[0], "sbod.StepProgram"));
   if (!p) return nullptr;
+  auto t_start = SteadyClock::now(), t = t_start;
   ListRows rows;
   const int r = pack_lists(a[1], a[2], p->capacity, p->per_image, p->dev, p->ob, p->ol, p->oo, p->pack_stream, 0,
                            rows, p->pack_stream, !p->lists);
@@ -325,6 +351,7 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
       if (sp != SBOD_OK) return PyLong_FromLong(sp);
     }
   }
+  g_sub_ns[0] += ns_since(t);
   int st;
   if (folded)
     st = sbod_criterion_focal_lists(rows.bp.data(), rows.lp.data(), rows.cnt.data(), p->capacity, p->c_locs,
@@ -339,15 +366,20 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
                               p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl, p->c_gs, p->c_out,
                               p->c_ws, p->c_wsb, p->c_stream);
   if (st != SBOD_OK) return PyLong_FromLong(st);
+  g_sub_ns[1] += ns_since(t);
   st = sbod_detect_f32(p->d_locs, p->d_scores, p->d_B, p->d_P, p->d_C, p->d_pri, p->d_pm, p->d_box, p->d_act,
                        p->d_min, p->d_ovl, p->d_topk, p->d_fnms, p->d_window, p->d_flags, p->d_boxes, p->d_labels,
                        p->d_scores_out, p->d_count, p->d_count_host, p->d_dbg_p, p->d_dbg_b, p->d_ws, p->d_wsb,
                        p->d_stream);
   if (st != SBOD_OK) return PyLong_FromLong(st);
+  g_sub_ns[2] += ns_since(t);
   if (p->event) {
     st = sbod_event_record(p->event, p->ev_stream);
     if (st != SBOD_OK) return PyLong_FromLong(st);
   }
+  g_sub_ns[3] += ns_since(t);
+  g_sub_ns[4] += std::chrono::duration<double, std::nano>(t - t_start).count();
+  ++g_sub_calls;
   Py_RETURN_TRUE;
 }
 
@@ -506,6 +538,8 @@ PyMethodDef methods[] = {
     {"make_step_program",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(make_step_program)),
      METH_FASTCALL, "Parse a recorded step (GT packing target, criterion and detect calls, event) once."},
+    {"submit_profile", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(submit_profile)), METH_FASTCALL,
+     "submit_profile([reset]) -> host time of submit_step_program by phase (us, summed over calls)."},
     {"submit_step_program",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(submit_step_program)),
      METH_FASTCALL, "GT packing + the recorded criterion and detect calls + the event, natively."},
