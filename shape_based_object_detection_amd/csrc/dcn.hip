@@ -192,8 +192,11 @@ __global__ __launch_bounds__(256) void k_transpose(const float *__restrict__ in,
 // conv.weight [O][C][N] -> the forward's Wf [O][N][C] and (training) the backward's Wb [N][O][C]
 // in one pass: one block per (64-channel chunk, output channel), the chunk's 64 x N contiguous
 // weights staged in LDS, each layout's rows written along c.
+// With wf3 (the split-bf16 forward), Wf's three bf16 parts [3][O][N][C] are written in the same
+// pass (split3 of each weight).
 __global__ __launch_bounds__(256) void k_weight_layouts(const float *__restrict__ w, int O, int C, int N,
-                                                        float *__restrict__ wf, float *__restrict__ wb) {
+                                                        float *__restrict__ wf, float *__restrict__ wb,
+                                                        __bf16 *__restrict__ wf3) {
   __shared__ float t[64][kMaxN + 1];
   const int c0 = blockIdx.x * 64, o = blockIdx.y;
   const int nc = min(64, C - c0);
@@ -204,8 +207,19 @@ __global__ __launch_bounds__(256) void k_weight_layouts(const float *__restrict_
     const int n = e >> 6, cl = e & 63;
     if (cl >= nc) continue;
     const float v = t[cl][n];
-    wf[(static_cast<int64_t>(o) * N + n) * C + c0 + cl] = v;
+    const int64_t fi = (static_cast<int64_t>(o) * N + n) * C + c0 + cl;
+    wf[fi] = v;
     if (wb) wb[(static_cast<int64_t>(n) * O + o) * C + c0 + cl] = v;
+#if defined(SBOD_DCN_SPLIT_BF16) || defined(SBOD_DCN_SPLIT_FWD)
+    if (wf3) {
+      const int64_t part = static_cast<int64_t>(O) * N * C;
+      __bf16 hp, mp, lp;
+      split3(v, hp, mp, lp);
+      wf3[fi] = hp;
+      wf3[part + fi] = mp;
+      wf3[2 * part + fi] = lp;
+    }
+#endif
   }
 }
 
@@ -427,21 +441,12 @@ __global__ __launch_bounds__(kDcnThreads, VEC == 4 ? SBOD_DCN_FWD_WAVES : 2) voi
 #ifdef SBOD_DCN_SPLIT_FWD
 // The forward contraction on the split-bf16 matrix cores (mfma6): k_dcn_fwd's blocking, gathers,
 // coefficient staging and K'-tile order, with (1) the weights' split parts precomputed
-// (wf3 [3][O][N*C] bf16, k_wf_split) and loaded as 16-byte vectors of 8 consecutive channels into
+// (wf3 [3][O][N*C] bf16, written by k_weight_layouts) and loaded as 16-byte vectors of 8 consecutive channels into
 // the A registers, (2) each combined column value split once by the thread that samples it and
 // stored as three bf16 rows (LDS [buf][part][pixel][channel], a 40-element pitch: conflict-free
 // 16-byte reads) — 48 bf16 MFMAs per K'-tile and wave instead of 64 fp32 ones at twice the cycles.
 // C % 8 == 0 (16-byte weight vectors).
 constexpr int kF3Pitch = 40;
-__global__ __launch_bounds__(256) void k_wf_split(const float *__restrict__ wf, int64_t n, __bf16 *__restrict__ wf3) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  __bf16 h, m, l;
-  split3(wf[i], h, m, l);
-  wf3[i] = h;
-  wf3[n + i] = m;
-  wf3[2 * n + i] = l;
-}
 
 __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd3(DcnShape s, const float *__restrict__ xt,
                                                                             const Coef *__restrict__ coef,
@@ -1670,26 +1675,24 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
   hipLaunchKernelGGL(k_dcn_coef, dim3((nc + 255) / 256), dim3(256), 0, hs, s, offset, mask_logits, st.coef,
                      train ? st.tcount : nullptr, zero_out, n_zero_out);
   SBOD_LAUNCHED("k_dcn_coef");
+#ifdef SBOD_DCN_SPLIT_FWD
+  __bf16 *wf3 = st.wf3;
+#else
+  __bf16 *wf3 = nullptr;
+#endif
 #ifndef SBOD_DCN_SPLIT_BF16
   hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
-                     train ? st.wb : nullptr);
+                     train ? st.wb : nullptr, wf3);
   SBOD_LAUNCHED("k_weight_layouts");
 #else
   hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
-                     static_cast<float *>(nullptr));
+                     static_cast<float *>(nullptr), wf3);
   SBOD_LAUNCHED("k_weight_layouts");
   if (train) {
     const int op = dcn_opad(s.O);
     hipLaunchKernelGGL(k_wb_split, dim3((s.C + 63) / 64, op / 64, s.N), dim3(256), 0, hs, st.wf, s.O, s.C, s.N, op,
                        st.wb3);
     SBOD_LAUNCHED("k_wb_split");
-  }
-#endif
-#ifdef SBOD_DCN_SPLIT_FWD
-  {
-    const int64_t nw = static_cast<int64_t>(s.O) * s.K;
-    hipLaunchKernelGGL(k_wf_split, dim3((nw + 255) / 256), dim3(256), 0, hs, static_cast<const float *>(st.wf), nw, st.wf3);
-    SBOD_LAUNCHED("k_wf_split");
   }
 #endif
   return SBOD_OK;
