@@ -112,6 +112,10 @@ def parse(argv=None):
     ap.add_argument('--timing-steps', type=int, default=12,
                     help='eager steps whose every kernel dispatch carries HIP events')
     ap.add_argument('--no-c2', action='store_true', help='skip the config C2 bf16 B=16 figure')
+    ap.add_argument('--c2-finish', choices=('fused', 'separate'), default='fused',
+                    help='C2 figure\'s loss finish: C2 is host-bound, so the form with one launch fewer per '
+                         'step (fused) wins there: 0.0301-0.0311 vs 0.0351-0.0389 ms, three rounds on one box '
+                         '(profiles/r5_c2_finish_ab_a1.jsonl)')
     ap.add_argument('--c2-det-form', choices=('two', 'one'), default='one',
                     help='C2 figure: detect as two launches (segment, merge) or one (k_det_nms); the C2 step '
                          'is host-bound, so one launch fewer wins there (same-box A/B 0.0327-0.0363 vs '
@@ -710,7 +714,7 @@ def c2_figure(dev, steps, warmup, B=16, n_batches=12, det_form='two', finish='se
     torch.cuda.synchronize()
     return {'config': 'C2 SSD512 batch=%d bf16: MultiBoxLoss512(DIoU+focal) fwd+bwd in bf16 + detect '
                       '(bf16 activations read in place), captured, %d resident batches' % (B, n_batches),
-            'detect_form': det_form,
+            'detect_form': det_form, 'loss_finish': finish,
             'ms_per_step': round(ms, 4), 'images_per_s': round(B / (ms * 1e-3), 1),
             'criterion_algorithmic_bytes': crit_b, 'steps': steps,
             'runs_ms_per_step': [round(r, 4) for r in runs],
@@ -1070,7 +1074,7 @@ def main():
     if dp is not None:
         line['dp_train_step_with_grad_allreduce'] = dp
     if not a.no_c2 and world == 1:
-        line['c2_bf16'] = c2_figure(dev, a.steps, a.warmup, det_form=a.c2_det_form, finish=a.finish)
+        line['c2_bf16'] = c2_figure(dev, a.steps, a.warmup, det_form=a.c2_det_form, finish=a.c2_finish)
     if not a.no_dcn:
         maps = [dcn_figure(dev, H=h, iters=5 if h >= 32 else 20) for h in (64, 32, 16, 8)]
         tot_ms = sum(m['ms'] for m in maps)
