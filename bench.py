@@ -169,6 +169,11 @@ ALGO_BYTES = {
 HBM_KERNELS = tuple(ALGO_BYTES)
 ALL_KERNELS = HBM_KERNELS + ('k_det_nms', 'k_det_segment', 'k_det_merge', 'k_match_final', 'k_hnm', 'k_loss_final')
 PMC_FILE = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
+DIST_BACKEND = os.environ.get('SBOD_BENCH_DIST_BACKEND', 'nccl')   # 'gloo': one-GPU rehearsal only
+# The step's captures restrict unsafe HIP calls in the capturing thread only: with ranks, the
+# process group's watchdog thread queries events while the main thread captures, which a global
+# capture would count against the graph (torch.cuda.graph's capture_error_mode)
+CAPTURE_MODE = 'thread_local'
 
 
 def pmc_traffic(kernel):
@@ -383,6 +388,16 @@ class Step:
         # the read-only unit upstream gradient: no ones-fill and no scale launch in the step
         self.one = core.unit_grad(dev)
 
+    def fresh_streams(self):
+        """New criterion / detect streams (same count and priorities) with their warm-up state
+        reset: the eager fallback after a failed capture, whose streams may stay capturing."""
+        self.cap_streams = [torch.cuda.Stream(self.dev, priority=s.priority) for s in self.cap_streams]
+        self.cap_stream = self.cap_streams[0]
+        self.det_streams = [torch.cuda.Stream(self.dev, priority=s.priority) for s in self.det_streams]
+        self.det_stream = self.det_streams[0]
+        self._cap_warm.clear()
+        self._det_warm.clear()
+
     def _next_batch(self):
         bt = self.batches[self.k % len(self.batches)]
         self.k += 1
@@ -517,7 +532,7 @@ class Step:
                 # joined back, so one hipGraphLaunch submits both chains (which stay concurrent)
                 g = torch.cuda.CUDAGraph()
                 cs, ds = self.cs_of(bi), self.ds_of(bi)
-                with torch.cuda.graph(g, stream=cs):
+                with torch.cuda.graph(g, stream=cs, capture_error_mode=CAPTURE_MODE):
                     ds.wait_stream(cs)
                     with torch.cuda.stream(ds):
                         h = self.detect(bt, True)
@@ -530,15 +545,15 @@ class Step:
                 continue
             if self.two:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga, stream=self.cs_of(bi)):
+                with torch.cuda.graph(ga, stream=self.cs_of(bi), capture_error_mode=CAPTURE_MODE):
                     loss = self.crit(bt.locs, bt.scores, gt, None)
                     loss.backward(self.one)
-                with torch.cuda.graph(gb, stream=self.ds_of(bi)):
+                with torch.cuda.graph(gb, stream=self.ds_of(bi), capture_error_mode=CAPTURE_MODE):
                     h = self.detect(bt, True)
                 self.slots.append((ga, gb, loss, h))
             else:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=self.cs_of(bi)):
+                with torch.cuda.graph(g, stream=self.cs_of(bi), capture_error_mode=CAPTURE_MODE):
                     loss = self.crit(bt.locs, bt.scores, gt, None)
                     h = self.detect(bt, True)
                     loss.backward(self.one)
@@ -812,7 +827,7 @@ def grad_allreduce_figure(step, a, dist, dev, world):
     grad = torch.ones(SSD512_PARAMS, dtype=torch.float32, device=dev)
     per = BUCKET_MB * (1 << 20) // 4
     buckets = list(grad.split(per))
-    group = dist.new_group(backend='nccl')
+    group = dist.new_group(backend=DIST_BACKEND)
     comm = torch.cuda.Stream(dev)
 
     def allreduce():
@@ -858,10 +873,17 @@ def main():
     if world != a.gpus:
         raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' % (a.gpus, world))
     dist = None
+    # rehearsal of the data-parallel path on a one-GPU box (diagnostic only): every rank on cuda:0
+    # and the gloo backend (RCCL refuses two ranks on one device); the driver's runs set neither
+    if os.environ.get('SBOD_BENCH_SAME_DEVICE') == '1':
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if DIST_BACKEND == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(DIST_BACKEND)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     L.lib()
@@ -946,6 +968,16 @@ def main():
             st.graph = None
             st.use_graph = False
             st.capture_error = repr(ex)[:300]
+            # a capture that failed part-way leaves its stream capturing and torch's current stream
+            # set to it; on this runtime an invalidated capture cannot be ended, so the eager
+            # fallback leaves those streams for fresh ones (scripts/probe_capture_abort.py)
+            torch.cuda.set_stream(torch.cuda.default_stream(dev))
+            for s in st.cap_streams + st.det_streams:
+                try:
+                    L.call('sbod_stream_abort_capture', s.cuda_stream)
+                except L.SbodError:
+                    pass
+            st.fresh_streams()
             torch.cuda.synchronize()
         L.timing_enable(None)
     if st.use_graph:

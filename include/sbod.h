@@ -93,6 +93,13 @@ int sbod_event_record(void *event, void *stream);
  * A no-op when both are the same stream. */
 int sbod_stream_wait(void *waiting_stream, void *on_stream);
 
+/* End a stream capture that a failed capture left open (an error inside the captured region can
+ * leave the stream capturing, and then every later call on it fails): ends it if `stream` is
+ * capturing and discards the graph; a no-op otherwise.  Returns SBOD_OK, or SBOD_E_HIP when the
+ * status cannot be read or the stream is still capturing afterwards (ROCm 7.2 keeps an
+ * INVALIDATED capture open: such a stream cannot be reused; the caller moves to a fresh one). */
+int sbod_stream_abort_capture(void *stream);
+
 /* ---------------------------------------------------------------- f1: ground-truth packing
  * Replaces the per-step GT handling of every criterion: the collate_fn list-of-tensors batch
  * (dataset/Datasets.py:58-86), moved to the device image by image (train_anchor.py:266-268) and

@@ -73,6 +73,7 @@ SIGNATURES = {
     'sbod_graph_launch': (I32, [P, P]),
     'sbod_event_record': (I32, [P, P]),
     'sbod_stream_wait': (I32, [P, P]),
+    'sbod_stream_abort_capture': (I32, [P]),
     'sbod_gt_pack': (I32, [P, P, P, I32, I64, P, P, P, P]),
     'sbod_dcn_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),
     'sbod_dcn_fwd_workspace_bytes': (SZ, [I32, I32, I32, I32, I32, I32, I32, I32]),

@@ -297,6 +297,24 @@ int sbod_stream_wait(void *waiting_stream, void *on_stream) {
   return SBOD_OK;
 }
 
+int sbod_stream_abort_capture(void *stream) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(sbod::as_stream(stream), &cs) != hipSuccess)
+    return sbod::launch_status("sbod_stream_abort_capture");
+  if (cs == hipStreamCaptureStatusNone) return SBOD_OK;
+  hipGraph_t g = nullptr;
+  (void)hipStreamEndCapture(sbod::as_stream(stream), &g);   // an invalidated capture ends with an error
+  if (g != nullptr) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(sbod::as_stream(stream), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    sbod::set_error("sbod_stream_abort_capture: the stream is still capturing (status %d): use another stream",
+                    static_cast<int>(cs));
+    return SBOD_E_HIP;
+  }
+  return SBOD_OK;
+}
+
 int sbod_scale_inplace(void *grad, int dtype, int64_t n, const float *scale, void *stream) {
   SBOD_REQUIRE(n >= 0 && scale != nullptr, "sbod_scale_inplace: bad arguments");
   if (n == 0) return SBOD_OK;
