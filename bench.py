@@ -105,6 +105,9 @@ def parse(argv=None):
                     help='graph mode: streams the criterion graphs alternate over (1 = one criterion stream)')
     ap.add_argument('--det-streams', type=int, default=2,
                     help='graph mode: streams the detect graphs alternate over (1 = one detect stream)')
+    ap.add_argument('--sync', choices=('auto', 'spin', 'yield'), default='auto',
+                    help='how the host waits for the GPU (hipSetDeviceFlags schedule, set before the '
+                         'device is initialised): auto = the runtime default (yield with one context)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-dcn', action='store_true')
     ap.add_argument('--batches', type=int, default=6,
@@ -867,6 +870,10 @@ def main():
         # one process per GPU: start the ranks now, before anything touches the GPU
         from shape_based_object_detection_amd.launch import spawn_ranks
         sys.exit(spawn_ranks(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    if a.sync != 'auto':   # before torch creates the device's context
+        import ctypes
+        hip = ctypes.CDLL('libamdhip64.so')
+        hip.hipSetDeviceFlags(ctypes.c_uint(1 if a.sync == 'spin' else 2))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -1064,7 +1071,7 @@ def main():
         'detect_streams': len(st.det_streams), 'criterion_streams': len(st.cap_streams),
         'pipeline_depth': st.depth, 'submit': st.submit,
         'gt_fold': st.gt_fold if st.submit == 'direct' else None,
-        'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'criterion_form': a.crit_form, 'loss_finish': a.finish, 'detect_form': a.det_form,
+        'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'), 'host_sync': a.sync, 'criterion_form': a.crit_form, 'loss_finish': a.finish, 'detect_form': a.det_form,
         'capture_error': st.capture_error,
         'eager_ms_per_step': round(eager_ms, 4) if eager_ms is not None else None,
         'api_ms_per_step': api['ms_per_step'] if api else None,
