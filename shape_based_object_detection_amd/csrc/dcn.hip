@@ -462,7 +462,13 @@ __global__ __launch_bounds__(kDcnThreads, 2) void k_dcn_fwd3(DcnShape s, const f
   const int CT = (s.C + kFKC - 1) / kFKC, T = s.N * CT;
   const int t0 = static_cast<int>(static_cast<int64_t>(tl.z) * T / gridDim.z);
   const int t1 = static_cast<int>(static_cast<int64_t>(tl.z + 1) * T / gridDim.z);
-  const int mm = tid & 63, cq = tid >> 6;
+#ifdef SBOD_DCN_FWD3_WAVE_CHANNELS
+  const int mm = tid & 63, cq = tid >> 6;   // (A/B form) a wave = 64 pixels x one channel group
+#else
+  // a lane quad = one pixel's 32 channels (128 contiguous bytes of xt per corner): a wave's
+  // corner load touches 16 lines instead of 64, the same line no longer fetched by four waves
+  const int mm = tid >> 2, cq = tid & 3;
+#endif
   const int ms = min(m0 + mm, s.M - 1);
   const float *xb = xt + static_cast<int64_t>(ms / HWo) * HW * s.C;
   struct Cf {
