@@ -406,7 +406,9 @@ int sbod_nms_f32(const float *boxes, const float *scores, int64_t n, float overl
  *   output BEFORE sigmoid, or NULL for modulation=False), weight [O,C,k,k] -> out [B,O,Ho,Wo].
  *   Backward: grad_out -> grad_x, grad_offset, grad_mask_logits, grad_weight (any may be NULL).
  *   The backward writes dcols rows [B*Ho*Wo][k²][C] and gathers dx per input pixel (no float
- *   atomics on dx); grad_out and weight must each stay below 2 GiB (buffer-descriptor range).
+ *   atomics on dx); the weight gradient is summed from per-pixel-slice partial planes in a fixed
+ *   order (bit-reproducible run to run); grad_out and weight must each stay below 2 GiB
+ *   (buffer-descriptor range).
  * Workspace: sbod_dcn_workspace_bytes(...) for the backward (it includes the dcols rows,
  * B*Ho*Wo*k²*C*4 bytes); the forward needs only sbod_dcn_fwd_workspace_bytes(...) (coefficients,
  * channels-last x and the transposed weights — a prefix of the backward's layout, so one
