@@ -316,6 +316,57 @@ def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
 
 
 # ----------------------------------------------------------------------------- the step
+class DPGraph:
+    """A data-parallel step's criterion as two captured graphs around an EAGER all-reduce of the
+    positive count: the matcher (and the count's copy into `tot`) | torch.distributed.all_reduce
+    (RCCL enqueues it on the current stream, no host sync) | the loss pass and its backward.  No
+    collective is captured, so the step does not depend on capturing RCCL (or on a capture of it
+    surviving the process group's watchdog thread), and a one-GPU gloo rehearsal replays the same
+    graphs.  replay() runs on the current stream."""
+
+    def __init__(self, ga1, tot, ga2, group=None):
+        self.ga1, self.tot, self.ga2, self.group = ga1, tot, ga2, group
+
+    def replay(self):
+        import torch.distributed as dist
+        self.ga1.replay()
+        dist.all_reduce(self.tot, op=dist.ReduceOp.SUM, group=self.group)
+        self.ga2.replay()
+
+
+def capture_dp_criterion(crit, locs, scores, gt, one, stream):
+    """Capture `crit(locs, scores, gt, None).backward(one)` (a distributed criterion) as a DPGraph:
+    core.allreduce_npos is swapped, for the capture only, for a split point that ends the first
+    graph after the count's copy and begins the second on the same stream and memory pool."""
+    ga1, ga2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    tot = torch.zeros(1, dtype=torch.int32, device=locs.device)
+    orig = core.allreduce_npos
+    split = {'done': False}
+
+    def split_point(n_pos, group=None, force=False):
+        if split['done']:
+            raise RuntimeError('capture_dp_criterion: more than one collective in the criterion')
+        tot.copy_(n_pos[-1:])
+        ga1.capture_end()
+        ga2.capture_begin(pool=ga1.pool(), capture_error_mode=CAPTURE_MODE)
+        split['done'] = True
+        split['group'] = group
+        return tot
+
+    core.allreduce_npos = split_point
+    try:
+        with torch.cuda.stream(stream):
+            ga1.capture_begin(capture_error_mode=CAPTURE_MODE)
+            loss = crit(locs, scores, gt, None)
+            loss.backward(one)
+            if not split['done']:
+                raise RuntimeError('capture_dp_criterion: the criterion issued no all-reduce')
+            ga2.capture_end()
+    finally:
+        core.allreduce_npos = orig
+    return DPGraph(ga1, tot, ga2, split.get('group')), loss
+
+
 class Step:
     """Criterion forward+backward and detect on one batch; eager or captured in hipGraphs.
 
@@ -329,6 +380,7 @@ class Step:
                  dtype=torch.float32, order='criterion_first', det_streams=2, crit_form='two', det_form='two',
                  crit_streams=2, depth=4, submit='direct', gt_fold=True, finish='separate'):
         self.dev, self.B = dev, B
+        self.world = world
         self.gt_fold = bool(gt_fold)
         Pn = prior_table(ARCH)
         self.P = Pn.shape[0]
@@ -547,10 +599,14 @@ class Step:
                     after_first()
                 continue
             if self.two:
-                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga, stream=self.cs_of(bi), capture_error_mode=CAPTURE_MODE):
-                    loss = self.crit(bt.locs, bt.scores, gt, None)
-                    loss.backward(self.one)
+                gb = torch.cuda.CUDAGraph()
+                if self.world > 1:   # two graphs around the eager all-reduce (DPGraph)
+                    ga, loss = capture_dp_criterion(self.crit, bt.locs, bt.scores, gt, self.one, self.cs_of(bi))
+                else:
+                    ga = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(ga, stream=self.cs_of(bi), capture_error_mode=CAPTURE_MODE):
+                        loss = self.crit(bt.locs, bt.scores, gt, None)
+                        loss.backward(self.one)
                 with torch.cuda.graph(gb, stream=self.ds_of(bi), capture_error_mode=CAPTURE_MODE):
                     h = self.detect(bt, True)
                 self.slots.append((ga, gb, loss, h))
@@ -587,7 +643,7 @@ class Step:
                         self.gt_fold)
                 self.programs.append(prog)
             torch.cuda.synchronize()
-        elif L.host_ext is not None:
+        elif L.host_ext is not None and self.world == 1:   # (DP: DPGraph replays from Python)
             self.fast = []
             for bi, (ga, gb, _, h) in enumerate(self.slots):
                 ds, cs = self.ds_of(bi), self.cs_of(bi)
