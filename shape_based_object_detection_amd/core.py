@@ -683,7 +683,8 @@ def allgather_pool(group=None):
 
 def allreduce_npos(n_pos, group=None, force=False):
     """Data parallel: the global positive count (one 4-byte SUM all-reduce over RCCL, enqueued on
-    the current stream — no host sync, so it is captured into a hipGraph with the criterion).
+    the current stream — no host sync; bench.DPGraph issues it eagerly between the criterion's
+    two captured graphs, and tests also capture it whole on one GPU with ``force``).
     Every rank then normalises by the global count, so the per-rank gradients are exactly the
     global-batch gradient's slices.  A one-rank group skips the collective unless
     ``force`` (tests exercise the captured collective on one GPU that way)."""
