@@ -1611,11 +1611,14 @@ size_t carve_all(const DcnShape &s, void *base, DcnState *st, DcnScratch *sc) {
 // split-K of the forward: up to 16 slices of the K' tiles (a sweep of the cap at 32x32 / 16x16 /
 // 8x8, profiles/r3_dcn_split_sweep_s1.jsonl: 16 is at least as fast as 32 or 64 on every map, 7 %
 // faster at 8x8), only while the pixel x output-channel tiles leave the chip under-filled
+#ifndef SBOD_FWD_SPLIT_MAX   // A/B knob: the forward's split-K cap
+#define SBOD_FWD_SPLIT_MAX 16
+#endif
 int fwd_split(const DcnShape &s) {
   const int mt = (s.M + kFM - 1) / kFM, og = (s.O + 255) / 256;
   const int T = s.N * ((s.C + kFKC - 1) / kFKC);
   int split = 1;
-  while (split * 2 <= T && mt * og * split < 512 && split < 16) split *= 2;
+  while (split * 2 <= T && mt * og * split < 512 && split < SBOD_FWD_SPLIT_MAX) split *= 2;
   return split;
 }
 
