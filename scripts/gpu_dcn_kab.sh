@@ -1,6 +1,7 @@
 #!/bin/bash
 # DCN per-kernel A/B: rocprofv3 kernel trace of the 64x64 (and 8x8) maps for the product library
-# and each named variant library; prints the median duration of every DCN kernel per library.
+# and each named variant library, one profiled run per map; prints the median duration of every
+# DCN kernel per library and map.
 #   bash scripts/gpu_dcn_kab.sh TAG variant1 [variant2 ...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -11,15 +12,22 @@ LIBV=$PWD/shape_based_object_detection_amd/lib/variants
 run() {   # name lib
   local name=$1 lib=$2
   if [ -n "$lib" ]; then export SBOD_LIB=$lib; else unset SBOD_LIB; fi
-  timeout -k 10 200 rocprofv3 --kernel-trace -d $O/kab_${TAG}_$name -o run --output-format csv -- \
-      python scripts/dcn_maps.py --maps ${MAPS:-64,8} --iters 5 > $O/kab_${TAG}_$name.log 2>&1 || { echo "$name failed"; tail -20 $O/kab_${TAG}_$name.log; exit 1; }
-  python - $O/kab_${TAG}_$name/run_kernel_trace.csv $name <<'PY'
-import csv, sys, statistics
+  # one profiled run per map: two maps can launch a kernel with the same grid (the weight
+  # gradient's 64x64 and 32x32 grids coincide), and a per-grid median would mix them
+  : > $O/kab_${TAG}_$name.log
+  for H in $(echo ${MAPS:-64,8} | tr ',' ' '); do
+    timeout -k 10 200 rocprofv3 --kernel-trace -d $O/kab_${TAG}_${name}_m$H -o run --output-format csv -- \
+        python scripts/dcn_maps.py --maps $H --iters 5 >> $O/kab_${TAG}_$name.log 2>&1 || { echo "$name failed"; tail -20 $O/kab_${TAG}_$name.log; exit 1; }
+  done
+  python - $O/kab_${TAG}_${name} $name <<'PY'
+import csv, glob, sys, statistics
 d = {}
-for r in csv.DictReader(open(sys.argv[1])):
-    n = r['Kernel_Name'].split('(')[0].replace('void ', '').replace('sbod::', '')[:34]
-    key = '%s %sx%sx%s' % (n, r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'])
-    d.setdefault(key, []).append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
+for f in sorted(glob.glob(sys.argv[1] + '_m*/run_kernel_trace.csv')):
+    m = f.split('_m')[-1].split('/')[0]
+    for r in csv.DictReader(open(f)):
+        n = r['Kernel_Name'].split('(')[0].replace('void ', '').replace('sbod::', '')[:34]
+        key = '%s %sx%sx%s @%s' % (n, r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'], m)
+        d.setdefault(key, []).append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
 tot = {}
 for k, v in d.items():
     if 'rocprim' in k:
