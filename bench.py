@@ -150,10 +150,10 @@ def criterion_bytes(B, P, C):
 
 
 def detect_bytes(w):
-    """scores [B,P,C] + locs [B,P,4] + priors read; decoded boxes [B,P,4], candidate keys (8 B
-    each) and per-(image, class) counts written (k_det_prepare; the NMS kernels after it are
-    latency-bound and read only the candidates)."""
-    return w['B'] * w['P'] * (4 * w['C'] + 16 + 16) + 16 * w['P'] + 8 * w['n_cand'] + 4 * w['B'] * w['C']
+    """scores [B,P,C] read; candidate keys (8 B each) and per-(image, class) counts written
+    (k_det_prepare; since round 6 the boxes are decoded by the NMS kernels after it, for the
+    candidates they read only — those kernels are latency-bound and not counted)."""
+    return w['B'] * w['P'] * 4 * w['C'] + 8 * w['n_cand'] + 4 * w['B'] * w['C']
 
 
 # Algorithmic HBM bytes per launch of the streaming (HBM-bound) kernels of one step (DESIGN.md
@@ -319,19 +319,38 @@ def dcn_figure(dev, H=64, B=16, C=256, O=256, iters=5):
 class DPGraph:
     """A data-parallel step's criterion as two captured graphs around an EAGER all-reduce of the
     positive count: the matcher (and the count's copy into `tot`) | torch.distributed.all_reduce
-    (RCCL enqueues it on the current stream, no host sync) | the loss pass and its backward.  No
-    collective is captured, so the step does not depend on capturing RCCL (or on a capture of it
-    surviving the process group's watchdog thread), and a one-GPU gloo rehearsal replays the same
-    graphs.  replay() runs on the current stream."""
+    (asynchronous: RCCL runs it on its own stream behind the matcher, no host sync) | the loss
+    pass and its backward.  No collective is captured, so the step does not depend on capturing
+    RCCL (or on a capture of it surviving the process group's watchdog thread), and a one-GPU gloo
+    rehearsal replays the same graphs.
+
+    ``front()`` issues the matcher and the all-reduce, ``back()`` makes the current stream wait for
+    the all-reduce and replays the loss pass.  The matcher needs only the ground truth and the
+    priors (models/SSD512.py:535-563), so ``Step`` issues step k+1's front before step k's back:
+    the loss pass of step k then waits on a collective issued one step earlier (long complete),
+    never on one in flight.  Both run on the current stream."""
 
     def __init__(self, ga1, tot, ga2, group=None):
         self.ga1, self.tot, self.ga2, self.group = ga1, tot, ga2, group
+        self.work = None
+
+    def front(self):
+        import torch.distributed as dist
+        if self.work is not None:
+            raise RuntimeError('DPGraph.front: the previous front of this batch was never consumed')
+        self.ga1.replay()
+        self.work = dist.all_reduce(self.tot, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def back(self):
+        if self.work is None:
+            self.front()
+        w, self.work = self.work, None
+        w.wait()          # the current stream waits for the all-reduce (no host sync under RCCL)
+        self.ga2.replay()
 
     def replay(self):
-        import torch.distributed as dist
-        self.ga1.replay()
-        dist.all_reduce(self.tot, op=dist.ReduceOp.SUM, group=self.group)
-        self.ga2.replay()
+        self.front()
+        self.back()
 
 
 def capture_dp_criterion(crit, locs, scores, gt, one, stream):
@@ -702,6 +721,24 @@ class Step:
                                          src_stream=cs) is not None:
                 return loss, h.rearmed()
         cs = self.cs_of(i)
+        if isinstance(ga, DPGraph):
+            with torch.cuda.stream(cs):
+                if ga.work is None:       # not issued by the previous step (the first one)
+                    bt.stage.stage(bt.boxes, bt.labels)
+                    ga.front()
+                if len(self.slots) > 1:
+                    # step k+1's GT packing, matcher and count all-reduce go out BEFORE this step's
+                    # loss pass (its own staging buffers and graphs: nothing of step k is touched)
+                    j = self.k % len(self.slots)
+                    nbt, nga = self.batches[self.k % len(self.batches)], self.slots[j][0]
+                    if nga.work is None:
+                        nbt.stage.stage(nbt.boxes, nbt.labels)
+                        nga.front()
+                ga.back()
+            ds = self.ds_of(i)
+            with torch.cuda.stream(ds):
+                gb.replay()
+                return loss, h.replayed(ds)
         if gb is None:
             with torch.cuda.stream(cs):
                 bt.stage.stage(bt.boxes, bt.labels)
@@ -1061,9 +1098,11 @@ def main():
         if prof is not None:
             prof(True)
         with torch.cuda.stream(st.cap_stream):
-            t_before = time.perf_counter()
+            m_before = time.monotonic_ns()   # host CLOCK_MONOTONIC (rocprofv3's clock): the timed
+            t_before = time.perf_counter()   # region in a kernel trace (scripts/timed_trace.py)
             elapsed = timed(st.pipelined, a.steps, dist, dev, finish=st.drain)
             t_after = time.perf_counter()
+            m_after = time.monotonic_ns()
         host_submit, host_collect = st.host_submit, st.host_collect
         tr, st.trace = st.trace, None
         sub_phases = prof(True) if prof is not None else None
@@ -1075,7 +1114,11 @@ def main():
                           'submit_us_first4': [round(x, 1) for x in sub[:4]],
                           'submit_us_median': round(sorted(sub)[len(sub) // 2], 1),
                           'last_submit_to_end_us': round((t_after - tr[-1][1]) * 1e6, 1),
-                          'steps_span_us': round((tr[-1][2] - tr[0][0]) * 1e6, 1)}
+                          'steps_span_us': round((tr[-1][2] - tr[0][0]) * 1e6, 1),
+                          'timed_window_ns': [m_before, m_after],
+                          # per step (first 40): submit start (us from the first), submit and collect us
+                          'steps_us': [[round((x0 - tr[0][0]) * 1e6, 1), round((x1 - x0) * 1e6, 1),
+                                        round((x2 - x1) * 1e6, 1)] for x0, x1, x2 in tr[:40]]}
             if sub_phases and sub_phases.get('calls'):
                 nc = sub_phases.pop('calls')
                 run_detail['native_submit_us_per_step'] = {k: round(v / nc, 2) for k, v in sub_phases.items()}

@@ -311,6 +311,11 @@ int sbod_criterion_focal_lists(const void *const *box_ptrs, const void *const *l
                                void *grad_scores, float *loss_out, void *workspace, size_t workspace_bytes,
                                void *stream);
 int sbod_criterion_status(const void *workspace, void *stream);
+/* The fused loss finish's sticky word (diagnostics, synchronises the stream): 1 if a bounded gather
+ * wait ever gave up on this workspace (every later loss from it is NaN until its zero-on-entry
+ * prefix is zeroed again: one call without SBOD_LOSS_WS_ZEROED / SBOD_CRIT_WS_ZEROED), else 0.
+ * Gmax == 0: a sbod_multibox_loss workspace; Gmax > 0: a sbod_criterion_focal one of (B, Gmax, P). */
+int sbod_loss_finish_status(const void *workspace, int B, int Gmax, int P, void *stream);
 
 /* grad *= (*scale) in place unless *scale == 1 (decided on the device: no host sync).
  * Used by backward to apply the upstream gradient to gradients produced by the fused

@@ -49,6 +49,7 @@ SIGNATURES = {
     'sbod_criterion_focal_lists': (I32, [P, P, P, I64, P, P, I32, I32, I32, I32, P, P, P, P, P, I32, F32, F32, I32,
                                          I32, F32, F32, F32, P, P, P, P, P, P, P, SZ, P]),
     'sbod_criterion_status': (I32, [P, P]),
+    'sbod_loss_finish_status': (I32, [P, I32, I32, I32, P]),
     'sbod_multibox_mine_global': (I32, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, F32, P, I64, I64, P,
                                         P, P, SZ, P]),
     'sbod_scale_inplace': (I32, [P, I32, I64, P, P]),

@@ -94,6 +94,8 @@ def _pack_fast(boxes, labels, capacity, per_image, dev_index, out_b, out_l, out_
 # it, so the next pack on that stream may overwrite the buffers (as the per-stream workspaces).
 _PACK_CACHE = {}
 _PACK_CAP = {}    # rows to allocate next time for a key whose batch overflowed its buffers
+_PACK_CAPTURED = set()   # data_ptr of cached pack buffers handed out under hipGraph capture
+_PACK_RETIRED = []       # grown-out-of pack buffers a captured graph may still address (kept alive)
 
 
 def _pack_cached(boxes, labels, allow_empty):
@@ -124,6 +126,8 @@ def _pack_cached(boxes, labels, allow_empty):
         return None
     if type(r) is int:
         raise L.SbodError('sbod_gt_pack failed (%d): %s' % (r, L.lib().sbod_last_error().decode(errors='replace')))
+    if torch.cuda.is_current_stream_capturing():
+        _PACK_CAPTURED.add(gb.data_ptr())   # the graph writes these rows on every replay
     n = sum(r)
     return GtPack(gb[:n], gl[:n], off, r)
 
@@ -152,7 +156,12 @@ def pack_gt(boxes, labels, device=None, allow_empty=False, reuse=False):
     key = (dev.index, L._raw_stream(dev.index), len(counts))
     if key in _PACK_CACHE and n > _PACK_CACHE[key][3] and not torch.cuda.is_current_stream_capturing():
         _PACK_CAP[key] = 2 * n    # the stream's buffers grow on its next regular call
-        del _PACK_CACHE[key]
+        old = _PACK_CACHE.pop(key)
+        if old[0].data_ptr() in _PACK_CAPTURED:
+            # a captured graph still packs GT into these buffers on replay: never hand them back
+            # to the allocator (as workspace() retires captured workspaces)
+            _PACK_CAPTURED.discard(old[0].data_ptr())
+            _PACK_RETIRED.append(old)
     gb = torch.empty(max(n, 1), 4, dtype=torch.float32, device=dev)
     gl = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     off = torch.empty(len(counts) + 1, dtype=torch.int32, device=dev)
@@ -502,6 +511,7 @@ def fused_criterion(locs, scores, gt, obj, ovl, n_pos, npos_total, priors_cxcy, 
 _VARIANTS = []        # sbod_build_variants(), queried once
 _CRIT_SIZES = {}      # (B, Gmax, P) -> (workspace bytes, zero-on-entry bytes)
 _MATCH_OUT = {}       # (device, stream, B, P) -> (obj, ovl, npos) reused by criterion classes
+_CRIT_SHAPE = {}      # criterion workspace data_ptr -> (B, Gmax, P) of its last call
 
 
 def _variants():
@@ -511,15 +521,18 @@ def _variants():
 
 
 def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, neg_threshold,
-                    two_launch=False, fresh_match=True):
+                    two_launch=None, fresh_match=True):
     """A focal criterion on one device in ONE launch (sbod_criterion_focal): the matcher and the
     fused loss + gradient pass, the normaliser produced inside the launch.  Returns (scalar loss
     with autograd, device vector {total, conf, loc, n_pos_total}, (obj, ovl, n_pos)).
-    ``two_launch`` runs the same call as the matcher and loss launches — the only form the product
-    library has (the one-launch form is a variant build, sbod_build_variants(); asking for it from
-    the product library raises instead of silently running two launches).
+    ``two_launch`` (default None = True) runs the same call as the matcher and loss launches — the
+    only form the product library has; ``two_launch=False`` asks for the one-launch form, which is
+    a variant build (sbod_build_variants()): asked of the product library it raises instead of
+    silently running two launches.
     ``fresh_match=False`` (the criterion classes, which do not keep the matcher outputs): obj /
     ovl / n_pos live in buffers reused by the next call on the same stream."""
+    if two_launch is None:
+        two_launch = True
     if not two_launch and not (_variants() & L.VARIANT_ONE_LAUNCH_CRITERION):
         raise L.SbodError('the one-launch criterion is built into the variant library only '
                           '(EXTRA=-DSBOD_VARIANT_ONE_LAUNCH scripts/build_lib_variant.sh); this library runs the '
@@ -565,6 +578,7 @@ def criterion_focal(locs, scores, gt, priors_cxcy, priors_xy, spec, threshold, n
         gs = torch.empty_like(scores) if want_grad else None
         ws = workspace(nb, dev, 'criterion')
         wp = ws.data_ptr()
+        _CRIT_SHAPE[wp] = (B, gmax, P)
         zflag = _zeroed_flag(ws, zb, L.CRIT_WS_ZEROED, 'criterion')
         _CLEAN.pop(wp, None)
         flags = ((spec.flags & (L.LOSS_FOCAL_NORM | L.LOSS_UNFUSED_FINISH)) | zflag |
@@ -621,8 +635,9 @@ def criterion_focal_fast(locs, scores, boxes, labels, priors_cxcy, priors_xy, sp
     if type(r) is int:
         raise L.SbodError('sbod_criterion_focal failed (%d): %s'
                           % (r, L.lib().sbod_last_error().decode(errors='replace')))
-    loss, comps, zb = r
+    loss, comps, zb, gmax = r
     _CLEAN[wp] = (zb, None)
+    _CRIT_SHAPE[wp] = (B, gmax, P)
     return loss, comps
 
 
@@ -636,6 +651,39 @@ def criterion_status(device=None):
     if ws is None:
         return 0
     return L.lib().sbod_criterion_status(L.ptr(ws), L._raw_stream(key[0].index))
+
+
+def loss_finish_status(device=None, reset=True):
+    """The fused loss finish's sticky word on the current stream's cached loss and criterion
+    workspaces (sbod_loss_finish_status): 1 if a bounded gather wait ever gave up there — every
+    later loss from that workspace is NaN until its zero-on-entry prefix is zeroed again.  With
+    ``reset`` such a workspace is marked not clean, so the next call zeroes it (one memset, outside
+    any capture) and computes again.  Synchronises the stream (diagnostics: call it when a fused-
+    finish loss reads NaN)."""
+    dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+    if dev.index is None:
+        dev = torch.device('cuda', torch.cuda.current_device())
+    stream = L._raw_stream(dev.index)
+    st = 0
+    for slot in ('loss', 'criterion'):
+        ws = _WS.get((dev, stream, slot))
+        if ws is None:
+            continue
+        if slot == 'loss':
+            B, G, P = 1, 0, 1
+        else:
+            sh = _CRIT_SHAPE.get(ws.data_ptr())
+            if sh is None:
+                continue
+            B, G, P = sh
+        r = L.lib().sbod_loss_finish_status(L.ptr(ws), B, G, P, stream)
+        if r < 0:
+            raise L.SbodError('sbod_loss_finish_status failed (%d): %s'
+                              % (r, L.lib().sbod_last_error().decode(errors='replace')))
+        if r and reset:
+            _CLEAN.pop(ws.data_ptr(), None)
+        st |= r
+    return st
 
 
 _POOL_SIZES_OK = set()   # (group, world, B*P) whose equality over the ranks was verified
@@ -746,7 +794,8 @@ class DetectHandle:
             # THAT stream: a later detect already queued there (pipelined graph replays share
             # the workspace) finishes first and leaves the counters zero, and the retry cannot
             # overlap it.  cnt.cpu() then waits for the retry in that stream's order.
-            with torch.cuda.stream(torch.cuda.ExternalStream(self._stream)):
+            # (ExternalStream on the launch's device, whatever device is current here)
+            with torch.cuda.stream(torch.cuda.ExternalStream(self._stream, device=self._slot_key[0])):
                 _detect_launch(*self._launch_args(4096))
                 counts = cnt.cpu().tolist()
                 if min(counts) < 0:
@@ -801,13 +850,12 @@ def _loss_zero_bytes(B, P):
     return z
 
 
-def _zeroed_flag(ws, need, flag, what, layout=None):
-    """``flag`` when the first ``need`` bytes of ``ws`` are known clean, else 0 (the call zeroes
-    them itself: a memset, which must not be captured).  ``layout``: the clean state is only valid
-    for a call whose workspace layout key matches the last successful call's (the criterion's
-    loss-finish state sits at a shape-dependent offset and is not all-zero between calls)."""
+def _zeroed_flag(ws, need, flag, what):
+    """``flag`` when the first ``need`` bytes of ``ws`` are known clean (every successful call
+    leaves its zero-on-entry prefix zero), else 0 (the call zeroes them itself: a memset, which
+    must not be captured)."""
     ent = _CLEAN.get(ws.data_ptr())
-    if ent is not None and ent[0] >= need and (layout is None or ent[1] == layout):
+    if ent is not None and ent[0] >= need:
         return flag
     if torch.cuda.is_current_stream_capturing():
         raise L.SbodError('%s under hipGraph capture: run it once on the capture stream with this '

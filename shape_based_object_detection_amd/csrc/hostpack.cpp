@@ -523,11 +523,12 @@ PyObject *criterion_focal_fast(PyObject *, PyObject *const *a, Py_ssize_t n) {
     return nullptr;
   }
   if (c.status != SBOD_OK) return PyLong_FromLong(c.status);
-  PyObject *res = PyTuple_New(3);
+  PyObject *res = PyTuple_New(4);
   if (!res) return nullptr;
   PyTuple_SET_ITEM(res, 0, THPVariable_Wrap(std::move(loss)));
   PyTuple_SET_ITEM(res, 1, THPVariable_Wrap(std::move(c.out)));
   PyTuple_SET_ITEM(res, 2, PyLong_FromSize_t(zb));
+  PyTuple_SET_ITEM(res, 3, PyLong_FromLong(gmax));   // the workspace's layout (sbod_loss_finish_status)
   return res;
 }
 

@@ -848,6 +848,11 @@ __device__ __forceinline__ void multibox_rows(const LossArgs &a, T *__restrict__
     }
   }
   MB_MARK(2, tid == 0);
+  // LDS-DMA tile (fp32 fast path): a wave's DMA chunks are read by OTHER waves' rows, and on
+  // gfx950 neither s_barrier nor the workgroup release fence waits for vmcnt — so every wave
+  // waits for its own DMA explicitly before the barrier (a wave whose rows are all
+  // invalid, e.g. SSD300's 28-row last tile, has no later use that would wait for it)
+  drain_vm();
   __syncthreads();   // the score tile is in LDS (every thread committed its part)
   MB_MARK(1, tid == 0);
   before_cls();
@@ -1849,6 +1854,22 @@ int sbod_criterion_status(const void *workspace, void *stream) {
       hipStreamSynchronize(s) != hipSuccess)
     return launch_status("sbod_criterion_status");
   return static_cast<int>(v);
+}
+
+int sbod_loss_finish_status(const void *workspace, int B, int Gmax, int P, void *stream) {
+  // diagnostics: the fused loss finish's sticky word (nonzero: a gather wait gave up in some
+  // call on this workspace, so every later loss from it is NaN until its zero-on-entry prefix is
+  // zeroed again — call without the *_WS_ZEROED flag once).  Gmax == 0: a sbod_multibox_loss
+  // workspace; Gmax > 0: a sbod_criterion_focal workspace of (B, Gmax, P).  Synchronises.
+  SBOD_REQUIRE(workspace != nullptr && B > 0 && P > 0 && Gmax >= 0, "sbod_loss_finish_status: bad arguments");
+  const char *lw = static_cast<const char *>(workspace);
+  if (Gmax > 0) lw = carve_crit(const_cast<void *>(workspace), B, Gmax, P).loss_ws;
+  unsigned long long v = 0;
+  hipStream_t s = as_stream(stream);
+  if (hipMemcpyAsync(&v, lw + kFinSticky * sizeof(unsigned long long), 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return launch_status("sbod_loss_finish_status");
+  return v != 0ull ? 1 : 0;
 }
 
 int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, int P, int C,

@@ -401,13 +401,69 @@ __device__ int block_greedy_matrix(const Box4 *sb, const float *sa, int n, float
 }
 
 
+// ----------------------------------------------------------------------------- boxes
+// The decoded + clamped box of (image b, prior p) (models/utils.py:218-224), recomputed by each
+// consumer from the raw locs (and the prior) instead of k_det_prepare writing all B x P of them:
+// only the candidates a segment's window holds and the merged outputs are ever read (~40K of
+// 328K boxes at SSD512 B=32), so the 5.2 MB box plane and its write are gone, and so is the
+// decode's VALU from the grid-wide pass.  Same inputs, same device functions (-ffp-contract=off):
+// the same bits as the former materialised plane.  CORNER boxes were clamped in place by
+// k_det_prepare (the reference's clamp_), clamping again is the identity.
+struct DetBoxes {
+  const void *locs;      // [B,P,4] f32, or bf16 bit patterns (bf16 != 0)
+  const float *priors;   // [P,4] cxcy (OFFSET); any valid 16-byte buffer otherwise (dummy loads)
+  int P, box_type, bf16;
+};
+// Where a box's latency must run under other work, its loads are issued early (det_box_issue:
+// unconditional, into plain registers) and decoded at the use (det_box_finish).
+struct RawBox {
+  Box4 l, pr;
+};
+
+
+__device__ __forceinline__ RawBox det_box_issue(const DetBoxes &s, int b, uint32_t p) {
+  const int64_t i = static_cast<int64_t>(b) * s.P + p;
+  RawBox r;
+  if (s.bf16) {
+    const uint2 v = *reinterpret_cast<const uint2 *>(static_cast<const uint16_t *>(s.locs) + 4 * i);
+    r.l = Box4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+               __uint_as_float(v.y & 0xffff0000u)};
+  } else {
+    r.l = ld4(static_cast<const float *>(s.locs) + 4 * i);
+  }
+  r.pr = ld4(s.priors + (s.box_type == SBOD_BOX_OFFSET ? 4 * static_cast<int64_t>(p) : 0));
+  return r;
+}
+
+__device__ __forceinline__ Box4 det_box_finish(const DetBoxes &s, const RawBox &r) {
+  Box4 d;
+  if (s.box_type == SBOD_BOX_OFFSET) {
+    d = decode_tenfive_xy(r.l, r.pr);
+  } else if (s.box_type == SBOD_BOX_CENTER) {
+    d = Box4{r.l.a - r.l.c / 2.f, r.l.b - r.l.d / 2.f, r.l.a + r.l.c / 2.f, r.l.b + r.l.d / 2.f};
+  } else {
+    d = r.l;
+  }
+  return Box4{fminf(fmaxf(d.a, 0.f), 1.f), fminf(fmaxf(d.b, 0.f), 1.f), fminf(fmaxf(d.c, 0.f), 1.f),
+              fminf(fmaxf(d.d, 0.f), 1.f)};
+}
+
+// (k_det_prepare's CORNER in-place clamp and debug boxes: the same arithmetic as det_box_finish)
+__device__ __forceinline__ Box4 det_decode(Box4 l, int box_type, const float *priors, uint32_t p) {
+  const RawBox r{l, box_type == SBOD_BOX_OFFSET ? ld4(priors + 4 * static_cast<int64_t>(p)) : l};
+  return det_box_finish(DetBoxes{nullptr, nullptr, 0, box_type, 0}, r);
+}
+
+__device__ __forceinline__ Box4 det_box(const DetBoxes &s, int b, uint32_t p) {
+  return det_box_finish(s, det_box_issue(s, b, p));
+}
+
 // ----------------------------------------------------------------------------- K1
 struct DetArgs {
   int B, P, C, box_type, act;
   const float *priors;
   const uint8_t *pos;
   float min_score;
-  float *boxes_ws;                 // [B,P,4] decoded + clamped
   unsigned long long *cand;        // [B,C,P]
   uint32_t *cand_count;            // [B,C]
   float *dbg_probs, *dbg_boxes;
@@ -489,19 +545,18 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, T *__restrict
   const bool valid = tid < np;
   const int p = p0 + tid;
   const int64_t i = rbase + tid;
-  // this prior's loc / prior / mask loads go out with the score tile's (one memory round trip)
+  // the prior's positive-mask byte goes out with the score tile (one memory round trip)
   const int64_t ic = valid ? i : rbase;
-  // Every prologue load is unconditional and lands in a plain register: a load under a branch
+  // The prologue load is unconditional and lands in a plain register: a load under a branch
   // (or a select of two loaded values) makes the wait-count insertion at the join wait for it
   // BEFORE the score tile below is even issued — one whole memory round trip on every
-  // workgroup's critical path.  Absent priors / positive mask read a valid dummy address (this
-  // row's locs) and are ignored by the uses.
-  const Box4 l = ld_box(locs + 4 * ic);
-  const float *pp = a.box_type == SBOD_BOX_OFFSET ? a.priors + 4 * static_cast<int64_t>(valid ? p : p0)
-                                                  : a.boxes_ws + 4 * ic;
-  const Box4 pr = ld4(pp);
+  // workgroup's critical path.  Without a positive mask it reads a dummy byte of the score tile
+  // this workgroup loads anyway (a dummy read of another plane fetches that plane's lines from
+  // HBM: 5.2 MB per launch at SSD512 B=32 when it was the box plane).
+  // The boxes are decoded by their consumers (det_box): this pass reads no locs and no priors
+  // unless it clamps CORNER boxes in place (models/utils.py:224) or writes the debug boxes.
   const auto *posp = (const __attribute__((address_space(1))) uint8_t *)(
-      a.pos != nullptr ? a.pos + ic : reinterpret_cast<const uint8_t *>(a.boxes_ws + 4 * ic));
+      a.pos != nullptr ? a.pos + ic : reinterpret_cast<const uint8_t *>(scores + rbase * C));
   const uint8_t posraw = *posp;
   constexpr int kPer16 = 16 / static_cast<int>(sizeof(T));   // elements per 16-byte chunk
 #if SBOD_PREP_GLDS
@@ -530,24 +585,18 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, T *__restrict
   else
     for (int e = tid; e < np * C; e += kDTile) s_tile[e] = scores[rbase * C + e];
 #endif
+  drain_vm();   // this wave's LDS-DMA chunks (read by other waves' rows) have landed: s_barrier
+                // does not wait for vmcnt on gfx950
   __syncthreads();
   SEG_PHASE(1);
   float *row = s_sc + tid * C;         // (CM == 0 only: fp32 rows)
   const T *rowt = s_tile + tid * C;
-  if (valid) {
-    Box4 d;
-    if (a.box_type == SBOD_BOX_OFFSET) {
-      d = decode_tenfive_xy(l, pr);
-    } else if (a.box_type == SBOD_BOX_CENTER) {
-      d = Box4{l.a - l.c / 2.f, l.b - l.d / 2.f, l.a + l.c / 2.f, l.b + l.d / 2.f};
-    } else {
-      d = l;
-    }
-    d = Box4{fminf(fmaxf(d.a, 0.f), 1.f), fminf(fmaxf(d.b, 0.f), 1.f), fminf(fmaxf(d.c, 0.f), 1.f),
-             fminf(fmaxf(d.d, 0.f), 1.f)};
+  if (valid && (a.box_type == SBOD_BOX_CORNER || a.dbg_boxes != nullptr)) {   // (wave-uniform test)
+    const Box4 d = det_decode(ld_box(locs + 4 * i), a.box_type, a.priors, static_cast<uint32_t>(p));
     if (a.box_type == SBOD_BOX_CORNER) st_box(locs + 4 * i, d);  // models/utils.py:224 clamp_ in place
-    st4_nt(a.boxes_ws + 4 * i, d);
     if (a.dbg_boxes) st4(a.dbg_boxes + 4 * i, d);
+  }
+  if (valid) {
     if constexpr (CM == 0) {
       if (a.act == SBOD_ACT_SOFTMAX) {
         float m = row[0];
@@ -738,7 +787,7 @@ __device__ __forceinline__ uint32_t key_prior(unsigned long long k, int P, bool 
 // kept keys in rank order.  Called by every thread of the block (it synchronises); used by
 // k_det_segment (one block per segment) and by k_det_merge's inline second pass.
 __device__ void segment_body(const unsigned long long *cand, const uint32_t *cand_count,
-                             const float *__restrict__ boxes_ws, int P, int C, int b, int c, int window,
+                             const DetBoxes boxes_ws, int P, int C, int b, int c, int window,
                              int stride, float thr, SegOut o, unsigned char *s_raw, uint32_t *s_hist,
                              unsigned long long *s_st, unsigned long long *s_flag, unsigned long long *s_m,
                              int *s_nk_p, int *s_cnt_p, int *s_misc) {
@@ -801,7 +850,7 @@ __device__ void segment_body(const unsigned long long *cand, const uint32_t *can
     bool bad;
     const uint32_t p = key_prior(sk[i], P, bad);
     bad_any |= bad;
-    const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
+    const Box4 bx = det_box(boxes_ws, b, p);
     sb[i] = bx;
     sa[i] = (bx.c - bx.a) * (bx.d - bx.b);
   }
@@ -827,7 +876,7 @@ __device__ void segment_body(const unsigned long long *cand, const uint32_t *can
 
 __global__ __launch_bounds__(kSegThreads) void k_det_segment(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
-    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
+    const DetBoxes boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
     const int32_t *__restrict__ need) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   __shared__ uint32_t s_hist[2048];
@@ -890,7 +939,7 @@ __device__ unsigned long long radix_select_below(const unsigned long long *g, in
 
 __global__ __launch_bounds__(kAllThreads) void k_det_segment_all(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
-    const float *__restrict__ boxes_ws, int P, int C, int stride, int top_k, float thr, SegOut o) {
+    const DetBoxes boxes_ws, int P, int C, int stride, int top_k, float thr, SegOut o) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];   // kept so far: keys [stride] | boxes [stride] | areas [stride]
   __shared__ unsigned long long s_key[kAllChunk];
   __shared__ Box4 s_box[kAllChunk];
@@ -931,7 +980,7 @@ __global__ __launch_bounds__(kAllThreads) void k_det_segment_all(
     bool alive = false, bad = false;
     if (tid < q) {
       const uint32_t p = key_prior(s_key[tid], P, bad);
-      const Box4 bx = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
+      const Box4 bx = det_box(boxes_ws, b, p);
       const float ar = (bx.c - bx.a) * (bx.d - bx.b);
       alive = true;
       for (int i = 0; i < kept && alive; ++i)
@@ -1008,7 +1057,7 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 
 __global__ __launch_bounds__(64) void k_det_segment_wave(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
-    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
+    const DetBoxes boxes_ws, int P, int C, int window, int stride, float thr, SegOut o,
     const int32_t *__restrict__ need) {
   __shared__ uint32_t s_hist[256];
   __shared__ unsigned long long s_sel[64];
@@ -1135,7 +1184,7 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
   bool bad = false;
   if (lane < q) {
     const uint32_t p = key_prior(v, P, bad);
-    bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
+    bu = det_box(boxes_ws, b, p);
   }
   const bool corrupt = __ballot(bad) != 0ull;
   int pos = lane;
@@ -1229,7 +1278,7 @@ constexpr int kSegWRegKeys = 2048;             // keys held in registers (2048 /
 template <int W, bool kWT>
 __device__ __forceinline__ void segment_w(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
-    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
+    const DetBoxes boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
   constexpr int kSegW = W;
   constexpr int NT = 64 * kSegW, KR = kSegWRegKeys / NT;
   STAMP_BEGIN();
@@ -1401,12 +1450,12 @@ __device__ __forceinline__ void segment_w(
   bool corrupt = false;
   if (wv == 0) {
     v = lane < q ? s_sel[lane] : 0ull;
-    Box4 bu{0.f, 0.f, 0.f, 0.f};
     bool bad = false;
-    if (lane < q) {
-      const uint32_t p = key_prior(v, P, bad);
-      bu = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p));
-    }
+    uint32_t p = 0;
+    if (lane < q) p = key_prior(v, P, bad);
+    // the box's loads issued now (unconditional: an idle lane reads prior 0), decoded after the
+    // sort, so their latency runs under it
+    const RawBox rb = det_box_issue(boxes_ws, b, p);
     corrupt = __ballot(bad) != 0ull;
     int pos = lane;
 #pragma unroll
@@ -1421,7 +1470,7 @@ __device__ __forceinline__ void segment_w(
         pos = tk ? wp : pos;
       }
     }
-    s_bxu[lane] = bu;
+    s_bxu[lane] = det_box_finish(boxes_ws, rb);
     wave_lds_sync();
     const Box4 bs = s_bxu[pos];
     s_bx[lane] = bs;
@@ -1517,7 +1566,7 @@ __device__ __forceinline__ void segment_w(
 
 __global__ __launch_bounds__(256) void k_det_segment_w4(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
-    const float *__restrict__ boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
+    const DetBoxes boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
   segment_w<4, false>(cand, cand_count, boxes_ws, P, C, window, stride, thr, o);
 }
 
@@ -1558,7 +1607,7 @@ __device__ __forceinline__ int count_before(const float *a, int n, float s, bool
 template <bool kWT = false>   // kWT: kept / kc / lastkey were written in this launch (sc1 loads)
 __device__ __forceinline__ int merge_rank(
     const unsigned long long *kept, const uint32_t *kc, const unsigned long long *lastkey,
-    const float *__restrict__ boxes_ws, int P, int C, int stride, int wmax, int top_k, int pass,
+    const DetBoxes boxes_ws, int P, int C, int stride, int wmax, int top_k, int pass,
     int32_t *__restrict__ need, float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
     float *__restrict__ out_scores, int32_t *__restrict__ out_count, int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
@@ -1645,7 +1694,7 @@ __device__ __forceinline__ int merge_rank(
   int64_t *ol = out_labels + static_cast<int64_t>(b) * top_k;
   float *os = out_scores + static_cast<int64_t>(b) * top_k;
   auto emit = [&](int r, int c, unsigned long long key) {
-    st4(ob + 4 * r, ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(key))));
+    st4(ob + 4 * r, det_box(boxes_ws, b, key_low(key)));
     ol[r] = c;
     os[r] = key_score(key);
   };
@@ -1724,9 +1773,8 @@ __device__ __forceinline__ int merge_rank(
   // so its latency runs under the rank counting; emitted below if the entry's rank < top_k
   const int e0 = min(tid, m - 1);
   const uint32_t low0 = 0xffffffffu - static_cast<uint32_t>(sk[e0]);
-  const Box4 box0 = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P +
-                                        key_low(sl[(static_cast<int>(low0 >> 24) - 1) * wmax +
-                                                   static_cast<int>(low0 & 0xffffffu)])));
+  const RawBox box0 = det_box_issue(
+      boxes_ws, b, key_low(sl[(static_cast<int>(low0 >> 24) - 1) * wmax + static_cast<int>(low0 & 0xffffffu)]));
   const int nsplit = max(1, min(16, NT / m)), per = (m + nsplit - 1) / nsplit;
   for (int t = tid; t < m * nsplit; t += NT) {
     const int e = t % m, part = t / m;
@@ -1758,7 +1806,7 @@ __device__ __forceinline__ int merge_rank(
       const int c = static_cast<int>(low >> 24), pos = static_cast<int>(low & 0xffffffu);
       const unsigned long long key = sl[(c - 1) * wmax + pos];
       if (e == tid) {   // the prefetched box
-        st4(ob + 4 * rank, box0);
+        st4(ob + 4 * rank, det_box_finish(boxes_ws, box0));
         ol[rank] = c;
         os[rank] = key_score(key);
       } else {
@@ -1785,7 +1833,7 @@ __device__ __forceinline__ int merge_rank(
 // 2 = second (only images with need[b]; invalid -> count -1).
 __device__ __forceinline__ int merge_body(
     const unsigned long long *kept, const uint32_t *kc,
-    const unsigned long long *lastkey, const float *__restrict__ boxes_ws, int P,
+    const unsigned long long *lastkey, const DetBoxes boxes_ws, int P,
     int C, int window, int wmax, int top_k, float final_nms, int general, int pass,
     int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
@@ -1864,7 +1912,7 @@ __device__ __forceinline__ int merge_body(
   float *os = out_scores + static_cast<int64_t>(b) * top_k;
   auto emit = [&](int r, int c, unsigned long long key) {
     const uint32_t p = key_low(key);
-    st4(ob + 4 * r, ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + p)));
+    st4(ob + 4 * r, det_box(boxes_ws, b, p));
     ol[r] = c;
     os[r] = key_score(key);
   };
@@ -2020,7 +2068,7 @@ __device__ __forceinline__ int merge_body(
   for (int i = tid; i < R; i += blockDim.x) {
     int c;
     const unsigned long long ck = entry(i, c);
-    const Box4 q = ld4(boxes_ws + 4 * (static_cast<int64_t>(b) * P + key_low(ck)));
+    const Box4 q = det_box(boxes_ws, b, key_low(ck));
     bx[i] = q;
     ar[i] = (q.c - q.a) * (q.d - q.b);
   }
@@ -2065,7 +2113,7 @@ __host__ __device__ inline size_t inline2_lds(int window) {
 // image needs it.
 __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
     const unsigned long long *kept, const uint32_t *kc, const unsigned long long *lastkey,
-    const float *__restrict__ boxes_ws, int P, int C, int window, int wfirst, int top_k, float final_nms,
+    const DetBoxes boxes_ws, int P, int C, int window, int wfirst, int top_k, float final_nms,
     int general, int pass, int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
     float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
     int32_t *__restrict__ out_count, int32_t *out_count_host, const unsigned long long *cand,
@@ -2118,7 +2166,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_det_merge(
 // single-pass merge does (the host re-runs it with a wider window).
 template <int W>
 __global__ __launch_bounds__(64 * W) void k_det_nms(
-    const unsigned long long *__restrict__ cand, uint32_t *cand_count, const float *__restrict__ boxes_ws, int P,
+    const unsigned long long *__restrict__ cand, uint32_t *cand_count, const DetBoxes boxes_ws, int P,
     int C, int window, int stride, float thr, SegOut o, uint32_t *arrive, int top_k, float *__restrict__ out_boxes,
     int64_t *__restrict__ out_labels, float *__restrict__ out_scores, int32_t *__restrict__ out_count,
     int32_t *out_count_host) {
@@ -2202,7 +2250,6 @@ using namespace sbod;
 
 namespace {
 struct DetWs {
-  float *boxes;
   unsigned long long *cand, *kept, *lastkey, *scratch;
   uint32_t *count, *kc, *arrive;
   int32_t *need;
@@ -2216,8 +2263,6 @@ DetWs carve_det(void *w, int B, int P, int C, int window) {
   r.count = ws_at<uint32_t>(w, o);
   r.arrive = ws_at<uint32_t>(w, static_cast<size_t>(B) * C * 4);   // [B] after the counters
   o += align_up(static_cast<size_t>(B) * C * 4 + static_cast<size_t>(B) * 4);
-  r.boxes = ws_at<float>(w, o);
-  o += align_up(static_cast<size_t>(B) * P * 16);
   r.cand = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * C * P * 8);
   r.kept = ws_at<unsigned long long>(w, o);
@@ -2298,12 +2343,15 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
   hipStream_t s = as_stream(stream);
   // the WHOLE aligned prefix (sbod_detect_counter_bytes): a caller that trusts it clean later (a
   // larger B * C whose counters reach into this call's alignment padding) must find zeros there,
-  // not the decoded boxes of an earlier, smaller call whose box region began inside it
+  // not the candidate keys of an earlier, smaller call whose key region began inside it
   if ((flags & SBOD_DETECT_COUNTERS_ZEROED) == 0 &&
       hipMemsetAsync(ws.count, 0, sbod_detect_counter_bytes(B, C), s) != hipSuccess)
     return launch_status("hipMemsetAsync(detect)");
-  DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.boxes, ws.cand, ws.count,
+  DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.cand, ws.count,
             debug_probs, debug_boxes, nullptr};
+  // decoded on demand (det_box); without priors (CENTER / CORNER boxes) the dummy prior loads
+  // read the output buffer's first 16 bytes (values unused)
+  const DetBoxes bxs{locs, priors_cxcy ? priors_cxcy : det_boxes, P, box_type, bf16 ? 1 : 0};
   {
     KernelTimer kt("k_det_prepare", s, true);
     a.span = kt.span();
@@ -2339,28 +2387,28 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
   if (fuse) {
     KernelTimer kt("k_det_nms", s, true);
     tlaunch(kt, k_det_nms<kNmsW>, dim3(C - 1, B), dim3(64 * kNmsW), static_cast<size_t>(rank_slots) * 20, s,
-            ws.cand, ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, ws.arrive, top_k, det_boxes, det_labels,
+            ws.cand, ws.count, bxs, P, C, w1, w2, max_overlap, so, ws.arrive, top_k, det_boxes, det_labels,
             det_scores, det_count, det_count_host);
     SBOD_LAUNCHED("k_det_nms");
     return SBOD_OK;
   }
   if (exhaustive) {
     KernelTimer kt("k_det_segment", s, true);
-    tlaunch(kt, k_det_segment_all, dim3(C - 1, B), dim3(kAllThreads), all_lds, s, ws.cand, ws.count, ws.boxes, P, C,
+    tlaunch(kt, k_det_segment_all, dim3(C - 1, B), dim3(kAllThreads), all_lds, s, ws.cand, ws.count, bxs, P, C,
             w2, top_k, max_overlap, so);
   } else {
     KernelTimer kt("k_det_segment", s, true);
     if (w1 <= 64)
 #ifdef SBOD_SEG_WAVE
-      tlaunch(kt, k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, ws.boxes,
+      tlaunch(kt, k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, bxs,
                          P, C, w1, w2, max_overlap, so, nullptr);
 #else
-      tlaunch(kt, k_det_segment_w4, dim3(C - 1, B), dim3(256), 0, s, ws.cand, ws.count, ws.boxes,
+      tlaunch(kt, k_det_segment_w4, dim3(C - 1, B), dim3(256), 0, s, ws.cand, ws.count, bxs,
                          P, C, w1, w2, max_overlap, so);
 #endif
     else
       tlaunch(kt, k_det_segment, dim3(C - 1, B), dim3(kSegThreads), seg_lds(w1), s, ws.cand,
-                         ws.count, ws.boxes, P, C, w1, w2, max_overlap, so, nullptr);
+                         ws.count, bxs, P, C, w1, w2, max_overlap, so, nullptr);
   }
   SBOD_LAUNCHED("k_det_segment");
   {
@@ -2369,7 +2417,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
     const size_t seg2 = two ? inline2_lds(w2) : 0;
     KernelTimer kt("k_det_merge", s, true);
     tlaunch(kt, k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, ws.kept,
-                       ws.kc, ws.lastkey, ws.boxes, P, C, w2, w1, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
+                       ws.kc, ws.lastkey, bxs, P, C, w2, w1, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
                        ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, det_count_host,
                        ws.cand, ws.count, max_overlap, so);
   }

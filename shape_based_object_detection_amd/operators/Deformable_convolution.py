@@ -5,7 +5,9 @@ modulation=True)`` with children ``zero_padding``, ``conv`` (k×k, stride k), ``
 ``m_conv`` (3×3, pad 1, stride ``stride``, weights zero-initialised) and the no-op ``_set_lr``
 backward hook.  The offset / mask convolutions stay ordinary convolutions (MIOpen); the
 sampling + modulation + k×k contraction, forward and backward, is one C-ABI call each
-(``sbod_dcn_fwd_f32`` / ``sbod_dcn_bwd_f32``, fp32 MFMA) instead of the reference's chain of
+(``sbod_dcn_fwd_f32`` / ``sbod_dcn_bwd_f32``: the forward and the weight gradient as split-bf16
+MFMA contractions — each fp32 operand the exact sum of three bf16 parts, six products kept, fp32
+accumulation, fp32-level error — and the data gradient on fp32 MFMA) instead of the reference's chain of
 gathers, concatenations and an im2col-sized intermediate.  CPU tensors take the host path
 (``hostpath.deform_conv2d``: the reference's sampling arithmetic in torch, autograd backward).
 """

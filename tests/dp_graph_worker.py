@@ -1,7 +1,8 @@
 """Rank worker for tests/test_gpu_dp_graph.py (not a test module): two ranks share cuda:0 over
 gloo; each runs bench.Step's data-parallel criterion eagerly (the positive-count all-reduce
 inside the criterion call) and then as the captured DPGraph (two graphs around an eager
-all-reduce), on the same batches, and writes whether loss and gradients are bit-identical."""
+all-reduce, the next step's matcher and all-reduce issued ahead of the current loss pass), on the
+same batches over two rotations, and writes whether loss and gradients are bit-identical."""
 import json
 import os
 import sys
@@ -18,7 +19,7 @@ def main():
     dist.init_process_group('gloo')
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
-    st = BM.Step(dev, 4, rank, world, graph=True, n_batches=2)
+    st = BM.Step(dev, 4, rank, world, graph=True, n_batches=3)
     eager = []
     for i in range(len(st.batches)):
         loss, _ = st.eager()
@@ -33,7 +34,10 @@ def main():
     st.capture()
     st.k = 0
     res = []
-    for i in range(len(st.batches)):
+    # two rotations: from the second step on, each step's matcher and count all-reduce were
+    # issued by the step before it (DPGraph.front ahead of the previous step's loss pass)
+    for k in range(2 * len(st.batches)):
+        i = k % len(st.batches)
         loss, _ = st.replay()
         torch.cuda.synchronize()
         bt = st.batches[i]

@@ -112,7 +112,7 @@ def test_poisoned_candidate_region_reports_corrupt_not_fault(fused):
     # the contract broken on purpose: image 0, class 1 claims 100 stale candidates whose keys carry
     # the highest score (so they are selected) and a prior index far beyond P
     cnt_off = 0
-    cand_off = -(-(B * C * 4 + B * 4) // 256) * 256 + -(-(B * P * 16) // 256) * 256
+    cand_off = -(-(B * C * 4 + B * 4) // 256) * 256   # the keys follow the counters (no box plane since r6)
     counters = ws[cnt_off:cnt_off + B * C * 4].view(torch.int32)
     counters[1] = 100
     seg = ws[cand_off + (0 * C + 1) * P * 8:cand_off + (0 * C + 1) * P * 8 + 100 * 8].view(torch.int64)

@@ -196,6 +196,59 @@ def test_stage_and_replay_equals_eager():
         locs.grad, scores.grad = g_gl, g_gs
 
 
+def test_captured_pack_cache_survives_growth():
+    """a criterion captured on list GT packs into the stream's cached pack buffers
+    (pack_gt(reuse=True)); a later eager batch that outgrows them must RETIRE those buffers (the
+    graph writes them on every replay), not hand them back to the allocator.  The replay after
+    the growth still gives the capture-time loss and gradients bit for bit."""
+    if L.host_ext is None:
+        pytest.skip('host extension not built (no cached pack path)')
+    B = 2
+    P, crit, locs, scores, det = _setup(B, seed=41)
+    gt1 = _gt(B, 42)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):                               # warm-up: the cached pack buffers exist
+            locs.grad = None
+            scores.grad = None
+            crit(locs, scores, gt1[0], gt1[1]).backward()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        locs.grad = None
+        scores.grad = None
+        l0 = crit(locs, scores, gt1[0], gt1[1])
+        l0.backward()
+    torch.cuda.synchronize()
+    ref_loss, ref_gl, ref_gs = l0.item(), locs.grad.clone(), scores.grad.clone()
+    locs.grad = None
+    scores.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        g_loss = crit(locs, scores, gt1[0], gt1[1])
+        g_loss.backward()
+    g_gl, g_gs = locs.grad, scores.grad
+    key = (DEV.index, side.cuda_stream, B)
+    captured = core._PACK_CACHE[key][0].data_ptr()
+    assert captured in core._PACK_CAPTURED
+    big_b, big_l = synth.make_gt(B, seed=43, max_objects=300)   # tiled to 300 objects per image
+    big_b = [torch.cat([b] * (300 // b.shape[0] + 1))[:300].to(DEV) for b in big_b]
+    big_l = [torch.cat([l] * (300 // l.shape[0] + 1))[:300].to(DEV) for l in big_l]
+    with torch.cuda.stream(side):                        # 600 rows > the cache's 512: it grows
+        locs.grad = None
+        scores.grad = None
+        crit(locs, scores, big_b, big_l).backward()
+    torch.cuda.synchronize()
+    assert any(t[0].data_ptr() == captured for t in core._PACK_RETIRED)
+    junk = [torch.full((1 << 16,), 7.0, device=DEV) for _ in range(8)]   # reuse freed memory
+    locs.grad, scores.grad = g_gl, g_gs
+    g.replay()
+    torch.cuda.synchronize()
+    assert g_loss.item() == ref_loss
+    assert torch.equal(g_gl, ref_gl) and torch.equal(g_gs, ref_gs)
+    del junk
+
+
 def test_workspace_allocation_under_capture_refused():
     """A workspace the captured call would allocate under capture fails loudly instead."""
     B = 2

@@ -157,3 +157,32 @@ def test_finish_records_repeat_and_interleave():
     assert np.array_equal(run(spec_f, 3, 62), b)
     assert np.array_equal(run(spec_u, 8, 61), a)
     assert np.array_equal(run(spec_f, 8, 61), a)
+
+
+def test_loss_finish_status_reset():
+    """the fused finish's sticky word (set when a gather wait gives up) makes every
+    later loss of that workspace NaN; ``core.loss_finish_status`` reports it and marks the
+    workspace not clean, so the next call zeroes it and computes again.  The sticky word is set by
+    hand here (a real timeout needs a hung workgroup)."""
+    P = torch.from_numpy(prior_table('SSD512'))
+    boxes, labels = synth.make_gt(2, seed=71)
+    locs, scores = synth.make_preds(2, P.shape[0], 21, seed=71)
+    crit = _crit('ssd512', P, 'diou')                    # the fused finish (separate_finish False)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        ref, _, _ = _loss(crit, locs, scores, boxes, labels)
+        assert np.isfinite(ref)
+        assert core.loss_finish_status(DEV) == 0
+        key = (torch.device('cuda', torch.cuda.current_device()), side.cuda_stream, 'criterion')
+        ws = core._WS[key]
+        B, G, Pn = core._CRIT_SHAPE[ws.data_ptr()]
+        lib = L.lib()
+        off = 256 + (B * 8 + 255) // 256 * 256 + (lib.sbod_match_workspace_bytes_p(B, G, Pn) + 255) // 256 * 256
+        sticky = off + (16 * 32 + 9) * 8                  # loss.hip kFinSticky (u64 words into the loss region)
+        ws[sticky:sticky + 8].view(torch.int64).fill_(1)
+        bad, _, _ = _loss(crit, locs, scores, boxes, labels)
+        assert np.isnan(bad)                              # the sticky state: NaN, never a wrong number
+        assert core.loss_finish_status(DEV) == 1          # reported, and the workspace marked not clean
+        again, _, _ = _loss(crit, locs, scores, boxes, labels)
+        assert again == ref                               # zeroed by the next call: clean again
+        assert core.loss_finish_status(DEV) == 0
