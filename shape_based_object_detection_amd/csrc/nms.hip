@@ -1180,12 +1180,10 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
   // ---- sort descending over lanes; the selected boxes are fetched BEFORE the sort (their
   // latency overlaps it) and each key carries its original lane to find its box afterwards
   unsigned long long v = lane < q ? s_sel[lane] : 0ull;
-  Box4 bu{0.f, 0.f, 0.f, 0.f};
   bool bad = false;
-  if (lane < q) {
-    const uint32_t p = key_prior(v, P, bad);
-    bu = det_box(boxes_ws, b, p);
-  }
+  uint32_t pr0 = 0;
+  if (lane < q) pr0 = key_prior(v, P, bad);
+  const RawBox rb = det_box_issue(boxes_ws, b, pr0);   // unconditional (idle lanes: prior 0)
   const bool corrupt = __ballot(bad) != 0ull;
   int pos = lane;
 #pragma unroll
@@ -1200,7 +1198,7 @@ __global__ __launch_bounds__(64) void k_det_segment_wave(
       pos = take ? wp : pos;
     }
   }
-  s_box[lane] = bu;
+  s_box[lane] = det_box_finish(boxes_ws, rb);
   wave_lds_sync();
   SEG_PHASE(3);
   // ---- greedy NMS over the q ranked boxes (torchvision suppression rule)
