@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=$1; R=${2:-2}
 O=$PWD/gpurun_out; mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests/test_gpu_criteria.py tests/test_gpu_match.py tests/test_gpu_bf16.py tests/test_gpu_operators.py \
-   tests/test_gpu_loss_finish.py tests/test_gpu_c1.py tests/test_gpu_c5.py tests/test_gpu_api_fast.py tests/test_gpu_gt_fold.py -q -x \
+   tests/test_gpu_loss_finish.py tests/test_gpu_c1.py tests/test_gpu_c5.py tests/test_gpu_api_fast.py tests/test_gpu_gt_fold.py tests/test_gpu_stress.py tests/test_gpu_graph.py -q -x \
    --timeout 200 --timeout-method thread > $O/ctests_$TAG.log 2>&1 || { echo "tests failed"; tail -40 $O/ctests_$TAG.log; exit 1; }
 tail -1 $O/ctests_$TAG.log
 for t in ab_base .; do

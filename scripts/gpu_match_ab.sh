@@ -1,20 +1,22 @@
 #!/bin/bash
-# GPU box: matcher-related -m gpu tests, per-kernel A/B of variant libraries (kernel_ab.py:
-# default, each variant, default again), then a bench line.
-#   bash scripts/gpu_match_ab.sh TAG "TEST FILES" VAR1 [VAR2 ...]
+# GPU box: matcher / criterion parity tests, per-kernel times of ab_base and this tree
+# (kernel_ab.py), k_match_tile stamps (stamps build), then the whole-tree A/B (gpu_tree_ab.sh).
+#   bash scripts/gpu_match_ab.sh TAG [rounds]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=$1; shift
-SEL=$1; shift
-LIBD=$PWD/shape_based_object_detection_amd/lib
-VARD=$PWD/variants
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest $SEL -m gpu -x -v --timeout 120 --timeout-method thread \
-    > gpurun_out/tests_$TAG.log 2>&1 || { echo "TESTS FAILED"; exit 1; }
-ab() { SBOD_LIB=$1 timeout -k 10 120 python scripts/kernel_ab.py >> gpurun_out/kab_$TAG.json 2>> gpurun_out/kab_$TAG.err; }
-ab $LIBD/libsbod_hip.so || exit 1
-for v in "$@"; do ab $VARD/libsbod_hip_$v.so || exit 1; done
-ab $LIBD/libsbod_hip.so || exit 1
-timeout -k 10 300 python bench.py --no-cpu-baseline --no-dcn > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
-rc=$?; echo "EXIT $rc"; exit $rc
+TAG=$1; R=${2:-1}
+O=$PWD/gpurun_out; mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_stress.py tests/test_gpu_criteria.py \
+   tests/test_gpu_gt_fold.py tests/test_gpu_graph.py tests/test_gpu_bf16.py tests/test_gpu_c1.py tests/test_gpu_operators.py \
+   tests/test_gpu_loss_finish.py tests/test_gpu_api_fast.py -q -x --timeout 200 --timeout-method thread \
+   > $O/mtests_$TAG.log 2>&1 || { echo "tests failed"; tail -40 $O/mtests_$TAG.log; exit 1; }
+tail -1 $O/mtests_$TAG.log
+for t in ab_base . ab_base .; do
+  ( cd $t && timeout -k 10 150 python scripts/kernel_ab.py ) >> $O/mkab_$TAG.json 2>> $O/mkab_$TAG.err || { echo "kab failed"; tail -5 $O/mkab_$TAG.err; exit 1; }
+done
+cat $O/mkab_$TAG.json
+SBOD_LIB=$PWD/shape_based_object_detection_amd/lib/variants/libsbod_hip_stamps.so timeout -k 10 120 python scripts/match_stamps.py --reps 3 \
+   > $O/mstamps_$TAG.json 2> $O/mstamps_$TAG.err || { echo "stamps failed"; tail -5 $O/mstamps_$TAG.err; exit 1; }
+tail -2 $O/mstamps_$TAG.json
+bash scripts/gpu_tree_ab.sh $TAG $R

@@ -8,11 +8,34 @@
 //
 // Roofline: HBM-bound.  Algorithmic bytes per launch (matcher alone) = 16*P (priors once) +
 // B*P*8 (obj + ovl written); ~17*G flops per prior-image.
-#include "match_dev.h"
+#include "sbod_common.h"
 
 namespace sbod {
 
 SBOD_STAMP_DECL
+
+// Diagnostic build only (-DSBOD_BLOCK_STAMPS, scripts/build_stamps_lib.sh): wave 0 of each
+// k_match_tile workgroup records four wall-clock marks while its stamps are armed — 0 the anchors
+// reduced to the wave's bounding box, 1 the first object chunk's hit ballot taken (its loads
+// landed), 2 the object loop done, 3 the keys flushed — read by sbod_debug_match_marks
+// (scripts/match_stamps.py).  Compiles to nothing otherwise.
+#ifdef SBOD_BLOCK_STAMPS
+static __device__ unsigned long long g_match_marks[SBOD_STAMP_REGION * 4];
+#define MATCH_WAVE_MARK(slot, dep)                                                                  \
+  do {                                                                                              \
+    asm volatile("" ::"v"(dep)); /* the mark follows the value it times */                          \
+    if ((g_stamp_armed & (1 << 5)) && threadIdx.x == 0) {                                           \
+      const unsigned _b = blockIdx.x + gridDim.x * blockIdx.y;                                      \
+      if (_b < SBOD_STAMP_REGION) g_match_marks[_b * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                               \
+  } while (0)
+#endif
+
+}  // namespace sbod
+
+#include "match_dev.h"
+
+namespace sbod {
 
 constexpr int kTile = 256;
 
@@ -532,3 +555,17 @@ int sbod_match_ssd_f32(const float *truths, const int64_t *labels, int G,
 }  // extern "C"
 
 SBOD_STAMP_EXPORT(match)
+
+#ifdef SBOD_BLOCK_STAMPS
+// k_match_tile's per-workgroup marks (diagnostic build): copies the first n workgroups' 4 marks out,
+// then clears them.
+extern "C" int sbod_debug_match_marks(unsigned long long *host, int n) {
+  const int cap = static_cast<int>(SBOD_STAMP_REGION);
+  if (host && n > 0)
+    hipMemcpyFromSymbol(host, HIP_SYMBOL(sbod::g_match_marks), sizeof(unsigned long long) * 4 * (n < cap ? n : cap));
+  void *sym = nullptr;
+  if (hipGetSymbolAddress(&sym, HIP_SYMBOL(sbod::g_match_marks)) == hipSuccess)
+    hipMemset(sym, 0, sizeof(unsigned long long) * 4 * cap);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+#endif

@@ -10,6 +10,13 @@
 
 #include "sbod_common.h"
 
+// per-wave phase marks of the diagnostic stamps build (match.hip defines them there)
+#ifndef MATCH_WAVE_MARK
+#define MATCH_WAVE_MARK(slot, dep) \
+  do {                             \
+  } while (0)
+#endif
+
 namespace sbod {
 
 constexpr int kMThreads = 256;  // matcher tile: one prior per thread
@@ -121,6 +128,7 @@ __device__ __forceinline__ MatchLane match_wave(const float *__restrict__ gt, co
   const uint32_t wx1 = ~wave_max_u32(live ? ~f2ord(a.x1) : 0u), wy1 = ~wave_max_u32(live ? ~f2ord(a.y1) : 0u);
   const uint32_t wx2 = wave_max_u32(live ? f2ord(a.x2) : 0u), wy2 = wave_max_u32(live ? f2ord(a.y2) : 0u);
   const bool wlive = __ballot(live) != 0ull;
+  MATCH_WAVE_MARK(0, wx1 ^ wy2);
   float best = 0.f;
   int bi = 0, blab = 0;
   // metrics.py:224-250, in the reference's order: this lane's overlap with chunk object j
@@ -187,6 +195,7 @@ __device__ __forceinline__ MatchLane match_wave(const float *__restrict__ gt, co
     const bool hit = wlive && lane < gn && f2ord(o.x2) > wx1 && f2ord(o.x1) < wx2 && f2ord(o.y2) > wy1 &&
                      f2ord(o.y1) < wy2;
     unsigned long long todo = __ballot(hit) | (gc == 0 ? 1ull : 0ull);
+    if (gc == 0) MATCH_WAVE_MARK(1, static_cast<uint32_t>(todo));
     // two objects per step (independent IoU chains), applied in object order
     while (todo) {
       const int j1 = __builtin_ctzll(todo);
@@ -210,7 +219,9 @@ __device__ __forceinline__ MatchLane match_wave(const float *__restrict__ gt, co
       if (two) note_key(gc + j2, ov2);
     }
   }
+  MATCH_WAVE_MARK(2, __float_as_uint(best) ^ static_cast<uint32_t>(nslot));
   flush_keys();
+  MATCH_WAVE_MARK(3, static_cast<uint32_t>(nslot));
   return MatchLane{p, bi, blab, best, valid, eas0, eas1};
 }
 
