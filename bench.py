@@ -1121,7 +1121,10 @@ def main():
                                         round((x2 - x1) * 1e6, 1)] for x0, x1, x2 in tr[:40]]}
             if sub_phases and sub_phases.get('calls'):
                 nc = sub_phases.pop('calls')
+                first = sub_phases.pop('first_calls_us', None)
                 run_detail['native_submit_us_per_step'] = {k: round(v / nc, 2) for k, v in sub_phases.items()}
+                if first:   # the fill: [pack, criterion, detect, event] us of the first submits
+                    run_detail['native_submit_first_us'] = [[round(x, 1) for x in c] for c in first]
         else:
             run_detail = None
         # the in-graph span of the dominant kernel (a host-synchronous read, so outside the

@@ -304,6 +304,8 @@ PyObject *make_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
 // submit_profile()): list checks + packing launch, criterion launches, detect launches, event.
 double g_sub_ns[5];
 long long g_sub_calls;
+constexpr int kSubFirst = 8;   // the first calls after a reset, phase by phase (the pipeline's fill)
+double g_sub_first[kSubFirst][4];
 using SteadyClock = std::chrono::steady_clock;
 inline double ns_since(SteadyClock::time_point &t) {
   const auto n = SteadyClock::now();
@@ -314,9 +316,17 @@ inline double ns_since(SteadyClock::time_point &t) {
 
 PyObject *submit_profile(PyObject *, PyObject *const *a, Py_ssize_t n) {
   const bool reset = n > 0 && PyObject_IsTrue(a[0]) == 1;
-  PyObject *r = Py_BuildValue("{s:L,s:d,s:d,s:d,s:d,s:d}", "calls", g_sub_calls, "pack_us", g_sub_ns[0] / 1e3,
+  PyObject *first = PyList_New(0);
+  for (long long i = 0; first && i < g_sub_calls && i < kSubFirst; ++i) {
+    PyObject *e = Py_BuildValue("[d,d,d,d]", g_sub_first[i][0] / 1e3, g_sub_first[i][1] / 1e3,
+                                g_sub_first[i][2] / 1e3, g_sub_first[i][3] / 1e3);
+    if (!e || PyList_Append(first, e) != 0) Py_CLEAR(first);
+    Py_XDECREF(e);
+  }
+  if (!first) return nullptr;
+  PyObject *r = Py_BuildValue("{s:L,s:d,s:d,s:d,s:d,s:d,s:N}", "calls", g_sub_calls, "pack_us", g_sub_ns[0] / 1e3,
                               "criterion_us", g_sub_ns[1] / 1e3, "detect_us", g_sub_ns[2] / 1e3, "event_us",
-                              g_sub_ns[3] / 1e3, "total_us", g_sub_ns[4] / 1e3);
+                              g_sub_ns[3] / 1e3, "total_us", g_sub_ns[4] / 1e3, "first_calls_us", first);
   if (reset) {
     for (double &v : g_sub_ns) v = 0.0;
     g_sub_calls = 0;
@@ -332,6 +342,7 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
   auto *p = static_cast<StepProgram *>(PyCapsule_GetPointer(a[0], "sbod.StepProgram"));
   if (!p) return nullptr;
   auto t_start = SteadyClock::now(), t = t_start;
+  double ph[4] = {0.0, 0.0, 0.0, 0.0};
   ListRows rows;
   const int r = pack_lists(a[1], a[2], p->capacity, p->per_image, p->dev, p->ob, p->ol, p->oo, p->pack_stream, 0,
                            rows, p->pack_stream, !p->lists);
@@ -351,7 +362,7 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
       if (sp != SBOD_OK) return PyLong_FromLong(sp);
     }
   }
-  g_sub_ns[0] += ns_since(t);
+  g_sub_ns[0] += ph[0] = ns_since(t);
   int st;
   if (folded)
     st = sbod_criterion_focal_lists(rows.bp.data(), rows.lp.data(), rows.cnt.data(), p->capacity, p->c_locs,
@@ -366,19 +377,21 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
                               p->c_rw, p->c_fa, p->c_fg, p->c_obj, p->c_ovl, p->c_npos, p->c_gl, p->c_gs, p->c_out,
                               p->c_ws, p->c_wsb, p->c_stream);
   if (st != SBOD_OK) return PyLong_FromLong(st);
-  g_sub_ns[1] += ns_since(t);
+  g_sub_ns[1] += ph[1] = ns_since(t);
   st = sbod_detect_f32(p->d_locs, p->d_scores, p->d_B, p->d_P, p->d_C, p->d_pri, p->d_pm, p->d_box, p->d_act,
                        p->d_min, p->d_ovl, p->d_topk, p->d_fnms, p->d_window, p->d_flags, p->d_boxes, p->d_labels,
                        p->d_scores_out, p->d_count, p->d_count_host, p->d_dbg_p, p->d_dbg_b, p->d_ws, p->d_wsb,
                        p->d_stream);
   if (st != SBOD_OK) return PyLong_FromLong(st);
-  g_sub_ns[2] += ns_since(t);
+  g_sub_ns[2] += ph[2] = ns_since(t);
   if (p->event) {
     st = sbod_event_record(p->event, p->ev_stream);
     if (st != SBOD_OK) return PyLong_FromLong(st);
   }
-  g_sub_ns[3] += ns_since(t);
+  g_sub_ns[3] += ph[3] = ns_since(t);
   g_sub_ns[4] += std::chrono::duration<double, std::nano>(t - t_start).count();
+  if (g_sub_calls < kSubFirst)
+    for (int k = 0; k < 4; ++k) g_sub_first[g_sub_calls][k] = ph[k];
   ++g_sub_calls;
   Py_RETURN_TRUE;
 }
