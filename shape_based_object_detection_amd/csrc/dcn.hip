@@ -1658,6 +1658,49 @@ __global__ __launch_bounds__(256) void k_wgrad_fold(const float *__restrict__ gw
 
 using namespace sbod;
 
+// The independent branches of an eager call at a large map (the weight layouts beside the x
+// transpose + coefficients; the dx scan + entry fill beside the backward-data contraction; the dx
+// gather beside the weight gradient) go to a side stream, forked from and joined back into the
+// caller's stream with events: C4 64x64 eager fwd+bwd 2.259-2.262 vs 2.294-2.304 ms.  Smaller maps
+// do not pay for the event calls (round 4), and a captured graph keeps one stream: as parallel
+// graph branches the same forks made the replay SLOWER (8x8 0.144-0.146 vs 0.124-0.125 ms, 16x16
+// 0.259-0.265 vs 0.244-0.249; 64x64 equal), the branches' cross-queue edges costing more than the
+// overlap.  One side stream and four events per host thread and device.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ok = false;
+};
+constexpr int64_t kEagerForkWork = int64_t(1) << 24;   // M x O: C4's 64x64 map (B=16, O=256)
+static SideStream *dcn_side(const DcnShape &s, hipStream_t hs) {
+  static thread_local SideStream side[16];
+  hipDevice_t dev = 0;
+  if (hipStreamGetDevice(hs, &dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(hs, &cs) != hipSuccess) return nullptr;
+  const bool capturing = cs == hipStreamCaptureStatusActive;
+  SideStream &x = side[dev];
+  if (!x.ok && !capturing) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    bool ok = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) == hipSuccess;
+    for (auto &e : x.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    x.ok = ok;
+    if (cur != dev) (void)hipSetDevice(cur);
+  }
+  if (!x.ok || capturing || static_cast<int64_t>(s.M) * s.O < kEagerForkWork) return nullptr;
+  return &x;
+}
+// side stream waits for everything issued on hs so far
+static bool dcn_fork(SideStream *x, int e, hipStream_t hs) {
+  return hipEventRecord(x->ev[e], hs) == hipSuccess && hipStreamWaitEvent(x->s, x->ev[e], 0) == hipSuccess;
+}
+// hs waits for everything issued on the side stream so far
+static bool dcn_join(SideStream *x, int e, hipStream_t hs) {
+  return hipEventRecord(x->ev[e], x->s) == hipSuccess && hipStreamWaitEvent(hs, x->ev[e], 0) == hipSuccess;
+}
+
 static int dcn_check(const DcnShape &s, const float *x, const float *offset, const float *weight) {
   SBOD_REQUIRE(x && offset && weight && shape_ok(s),
                "sbod_dcn: bad arguments (NULL tensor, or sizes non-positive, kernel_size > 7 or "
@@ -1677,6 +1720,9 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
                       hipStream_t hs) {
   const int64_t npix = static_cast<int64_t>(s.B) * s.H * s.W;
   const int HW = s.H * s.W;
+  SideStream *side = dcn_side(s, hs);
+  if (side && !dcn_fork(side, 0, hs)) return launch_status("dcn fork (derive)");
+  const hipStream_t ls = side ? side->s : hs;   // the weight layouts' stream
   hipLaunchKernelGGL(k_transpose, dim3((HW + 63) / 64, (s.C + 63) / 64, s.B), dim3(256), 0, hs, x, st.xt, s.C, HW,
                      train ? reinterpret_cast<float *>(st.tcount) : nullptr, train ? npix + 1 : 0);
   SBOD_LAUNCHED("k_transpose(x)");   // x [B][C][HW] -> xt [B][HW][C]
@@ -1690,20 +1736,21 @@ static int dcn_derive(const DcnShape &s, const float *x, const float *offset, co
   __bf16 *wf3 = nullptr;
 #endif
 #ifndef SBOD_DCN_SPLIT_BF16
-  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
+  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, ls, weight, s.O, s.C, s.N, st.wf,
                      train ? st.wb : nullptr, wf3);
   SBOD_LAUNCHED("k_weight_layouts");
 #else
-  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, hs, weight, s.O, s.C, s.N, st.wf,
+  hipLaunchKernelGGL(k_weight_layouts, dim3((s.C + 63) / 64, s.O), dim3(256), 0, ls, weight, s.O, s.C, s.N, st.wf,
                      static_cast<float *>(nullptr), wf3);
   SBOD_LAUNCHED("k_weight_layouts");
   if (train) {
     const int op = dcn_opad(s.O);
-    hipLaunchKernelGGL(k_wb_split, dim3((s.C + 63) / 64, op / 64, s.N), dim3(256), 0, hs, st.wf, s.O, s.C, s.N, op,
+    hipLaunchKernelGGL(k_wb_split, dim3((s.C + 63) / 64, op / 64, s.N), dim3(256), 0, ls, st.wf, s.O, s.C, s.N, op,
                        st.wb3);
     SBOD_LAUNCHED("k_wb_split");
   }
 #endif
+  if (side && !dcn_join(side, 1, hs)) return launch_status("dcn join (derive)");
   return SBOD_OK;
 }
 
@@ -1749,16 +1796,22 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
                               static_cast<int64_t>(s.N) * s.O * s.C * 4 < (1ll << 31)),
                "sbod_dcn_bwd: grad_out / weight exceed the 2 GiB buffer-descriptor range");
   const int64_t ob = static_cast<int64_t>(s.M) * s.N;
+  // with dx: the scan + entry fill (side stream) beside the backward-data contraction, joined
+  // before the weight gradient (which adds into the offset / mask gradients the fill zeroes);
+  // then the dx gather (side stream) beside the weight gradient, joined at the end
+  SideStream *side = grad_x && need_cols ? dcn_side(s, hs) : nullptr;
+  if (side && !dcn_fork(side, 0, hs)) return launch_status("dcn fork (backward)");
+  const hipStream_t xs = side ? side->s : hs;   // the dx branch's stream
   if (grad_x) {   // the input pixels' entry ranges (scan of the counts the forward made)
     if (npix + 1 <= kScanOneBlock) {
-      hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, hs, st.tcount, sc.cur, npix + 1);
+      hipLaunchKernelGGL(k_dcn_scan, dim3(1), dim3(1024), 0, xs, st.tcount, sc.cur, npix + 1);
       SBOD_LAUNCHED("k_dcn_scan");
     } else {
       size_t tb = sc.scan_bytes;
-      if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, tb, st.tcount, sc.cur, npix + 1, hs) != hipSuccess)
+      if (hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp, tb, st.tcount, sc.cur, npix + 1, xs) != hipSuccess)
         return launch_status("DeviceScan(dcn dx offsets)");
     }
-    hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, hs, s, st.coef, sc.cur, sc.ent,
+    hipLaunchKernelGGL(k_dcn_dx_fill, dim3((ob + 255) / 256), dim3(256), 0, xs, s, st.coef, sc.cur, sc.ent,
                        grad_offset, grad_offset ? 2 * ob : 0, grad_mask_logits, grad_mask_logits ? ob : 0,
                        nullptr, int64_t(0));
     SBOD_LAUNCHED("k_dcn_dx_fill");
@@ -1788,15 +1841,16 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
 #endif
   }
   if (need_cols) SBOD_LAUNCHED("k_dcn_bwd_data");
+  if (side && !(dcn_join(side, 1, hs) && dcn_fork(side, 2, hs))) return launch_status("dcn join / fork (backward)");
   if (grad_x) {
     {
-      KernelTimer kt("k_dcn_dx_gather", hs);
+      KernelTimer kt("k_dcn_dx_gather", xs);
       const dim3 grid((npix + kGxPix - 1) / kGxPix);
       if (s.C % 4 == 0)
-        hipLaunchKernelGGL(k_dcn_dx_gather<4>, grid, dim3(64 * kGxPix), 0, hs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
+        hipLaunchKernelGGL(k_dcn_dx_gather<4>, grid, dim3(64 * kGxPix), 0, xs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
                            sc.dcols, grad_x);
       else
-        hipLaunchKernelGGL(k_dcn_dx_gather<1>, grid, dim3(64 * kGxPix), 0, hs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
+        hipLaunchKernelGGL(k_dcn_dx_gather<1>, grid, dim3(64 * kGxPix), 0, xs, s.C, s.H * s.W, npix, sc.cur, sc.ent,
                            sc.dcols, grad_x);
     }
     SBOD_LAUNCHED("k_dcn_dx_gather");
@@ -1845,6 +1899,7 @@ static int dcn_backward(const DcnShape &s, const DcnState &st, const DcnScratch 
       SBOD_LAUNCHED("k_wgrad_fold");
     }
   }
+  if (side && !dcn_join(side, 3, hs)) return launch_status("dcn join (backward)");
   return SBOD_OK;
 }
 
