@@ -417,7 +417,11 @@ int sbod_nms_f32(const float *boxes, const float *scores, int64_t n, float overl
  * Workspace: sbod_dcn_workspace_bytes(...) for the backward (it includes the dcols rows,
  * B*Ho*Wo*k²*C*4 bytes); the forward needs only sbod_dcn_fwd_workspace_bytes(...) (coefficients,
  * channels-last x and the transposed weights — a prefix of the backward's layout, so one
- * workspace sized for the backward serves both). */
+ * workspace sized for the backward serves both).
+ * Streams: all work is ordered on `stream` as for any entry point.  An eager (not capturing)
+ * call with B*Ho*Wo*O >= 2^24 runs its independent branches on an internal side stream of the
+ * calling host thread, forked from and joined back into `stream` with events before it returns;
+ * a call under hipGraph capture stays on `stream`. */
 size_t sbod_dcn_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
 size_t sbod_dcn_fwd_workspace_bytes(int B, int C, int H, int W, int O, int k, int stride, int pad);
 int sbod_dcn_fwd_f32(const float *x, const float *offset, const float *mask_logits,
