@@ -95,10 +95,12 @@ def parse(argv=None):
                     help='graph: replay captured hipGraphs (criterion and detect, two launches); fork: one '
                          'graph per step with detect forked onto its stream inside it; direct: issue the '
                          'recorded entry-point calls')
-    ap.add_argument('--gt-fold', type=int, choices=(0, 1), default=0,
+    ap.add_argument('--gt-fold', type=int, choices=(0, 1), default=1,
                     help='direct submit: 1 = the GT packing folded into the matcher\'s first launch '
-                         '(sbod_criterion_focal_lists), 0 = a separate sbod_gt_pack launch (the headline default: '
-                         'same-box A/B 0.0345 vs 0.0353 ms at B=32; C2 at B=16 takes the fold)')
+                         '(sbod_criterion_focal_lists: one launch fewer per step), 0 = a separate sbod_gt_pack '
+                         'launch.  Same-box A/B at the driver\'s 20 steps, six rounds: 0.0367-0.0401 vs '
+                         '0.0379-0.0426 ms (fold faster in 5 of 6; host submit 25-27 vs 28-31 us); at 300 '
+                         'GPU-bound steps 0.0331 vs 0.0325 (profiles/r6_fold20_ab_a.jsonl)')
     ap.add_argument('--depth', type=int, default=4,
                     help='graph mode: steps in flight (submit step k, then collect step k - depth + 1)')
     ap.add_argument('--crit-streams', type=int, default=2,
