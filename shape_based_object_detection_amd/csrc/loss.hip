@@ -1381,11 +1381,10 @@ __global__ __launch_bounds__(kHBlock) void k_hnm(const float *__restrict__ pool,
 // SBOD_LOSS_UNFUSED_FINISH): one block sums every workgroup's fp32 partials and the mining
 // segments' sums EXACTLY (128-bit fixed point, as the fused finish: the same loss bit for bit
 // whichever finish ran), falling back to a double sum when a value cannot be folded.
-__global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ partials, int nparts,
-                                                    const float *__restrict__ hnm, int nseg,
-                                                    const int32_t *__restrict__ npos_total, int reg,
-                                                    int cls, int flags, float reg_weight,
-                                                    float *__restrict__ out) {
+__device__ __forceinline__ void loss_final_body(const float *__restrict__ partials, int nparts,
+                                                const float *__restrict__ hnm, int nseg,
+                                                const int32_t *__restrict__ npos_total, int reg, int cls,
+                                                int flags, float reg_weight, float *__restrict__ out) {
   STAMP_BEGIN();
   __shared__ double s_red[16];
   __shared__ unsigned long long s_fx[5 * 4];
@@ -1454,6 +1453,23 @@ __global__ __launch_bounds__(256) void k_loss_final(const float *__restrict__ pa
   }
   if (tid == 0) loss_outputs(c, l, static_cast<float>(*npos_total), reg, cls, flags, reg_weight, out);
   STAMP_END(6, 1);
+}
+
+// The launch takes ONE by-value argument: this runtime's host cost of a launch grows with the
+// argument count (≈ 0.5 µs more for sixteen arguments than for one struct of the same bytes,
+// scripts/micro/launch_cost.hip), and this kernel is on every step's criterion submit.
+struct LossFinalArgs {
+  const float *partials;
+  int nparts;
+  const float *hnm;
+  int nseg;
+  const int32_t *npos_total;
+  int reg, cls, flags;
+  float reg_weight;
+  float *out;
+};
+__global__ __launch_bounds__(256) void k_loss_final(const LossFinalArgs a) {
+  loss_final_body(a.partials, a.nparts, a.hnm, a.nseg, a.npos_total, a.reg, a.cls, a.flags, a.reg_weight, a.out);
 }
 
 // ----------------------------------------------------------------------------- standalone
@@ -1615,8 +1631,10 @@ int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const in
   }
   {
     KernelTimer kt("k_loss_final", s, true);
-    tlaunch(kt, k_loss_final, dim3(1), dim3(256), 0, s, static_cast<const float *>(ws.partials), nblk,
-            static_cast<const float *>(ws.hnm), nseg, npos_total, reg, cls, flags, reg_weight, loss_out);
+    tlaunch(kt, k_loss_final, dim3(1), dim3(256), 0, s,
+            LossFinalArgs{static_cast<const float *>(ws.partials), static_cast<int>(nblk),
+                          static_cast<const float *>(ws.hnm), nseg, npos_total, reg, cls, flags, reg_weight,
+                          loss_out});
   }
   SBOD_LAUNCHED("k_loss_final");
   return SBOD_OK;

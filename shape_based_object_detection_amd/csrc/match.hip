@@ -137,29 +137,44 @@ __device__ __forceinline__ void match_tile_body(
   STAMP_END(5, 1);
 }
 
+// The matcher's launches take one by-value argument struct (the host cost of a launch grows with
+// the argument count on this runtime: scripts/micro/launch_cost.hip).
+struct MatchArgs {
+  const float *anchors, *priors, *arm_scores;
+  int P, Gmax;
+  float thr, theta;
+  int32_t *obj;
+  float *ovl;
+  unsigned long long *best_key;
+  int32_t *wcnt, *npos;
+  int B;
+};
+
 template <bool kOdm, int kFlags>
-__global__ __launch_bounds__(kMThreads) void k_match_tile(
-    const float *__restrict__ gt, const int64_t *__restrict__ labels,
-    const int32_t *__restrict__ off, const float *__restrict__ anchors,
-    const float *__restrict__ priors, const float *__restrict__ arm_scores, int P, int Gmax,
-    float thr, float theta, int32_t *__restrict__ obj, float *__restrict__ ovl,
-    unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt, int32_t *__restrict__ npos,
-    int B, SpanRing *span) {
-  match_tile_body<kOdm, kFlags>(gt, labels, off, -1, 0, anchors, priors, arm_scores, P, Gmax, thr, theta, obj, ovl,
-                                best_key, wcnt, npos, B, span);
+__global__ __launch_bounds__(kMThreads) void k_match_tile(const float *__restrict__ gt, const int64_t *__restrict__ labels,
+                                                          const int32_t *__restrict__ off, const MatchArgs m,
+                                                          SpanRing *span) {
+  match_tile_body<kOdm, kFlags>(gt, labels, off, -1, 0, m.anchors, m.priors, m.arm_scores, m.P, m.Gmax, m.thr, m.theta,
+                                m.obj, m.ovl, m.best_key, m.wcnt, m.npos, m.B, span);
 }
 
 // The list form (B <= kPackImgs): each image's rows are read in place from the collate_fn lists
 // (pointers and row offsets in the kernel arguments), and the image's first workgroup also writes
 // them packed (gt_boxes / gt_labels / gt_offsets) for k_match_final and the loss pass after this
 // launch — the separate sbod_gt_pack launch folded in.  Every image has >= 1 row, 16-B aligned.
+struct MatchListsArgs {
+  float *out_boxes;
+  int64_t *out_labels;
+  int32_t *out_off;
+  MatchArgs m;
+};
 template <bool kOdm, int kFlags>
-__global__ __launch_bounds__(kMThreads) void k_match_tile_lists(
-    GtPackArgs lists, float *__restrict__ out_boxes, int64_t *__restrict__ out_labels,
-    int32_t *__restrict__ out_off, const float *__restrict__ anchors, const float *__restrict__ priors,
-    const float *__restrict__ arm_scores, int P, int Gmax, float thr, float theta, int32_t *__restrict__ obj,
-    float *__restrict__ ovl, unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt,
-    int32_t *__restrict__ npos, int B) {
+__global__ __launch_bounds__(kMThreads) void k_match_tile_lists(const GtPackArgs lists, const MatchListsArgs la) {
+  float *__restrict__ out_boxes = la.out_boxes;
+  int64_t *__restrict__ out_labels = la.out_labels;
+  int32_t *__restrict__ out_off = la.out_off;
+  const MatchArgs &m = la.m;
+  const int B = m.B;
   const int b = blockIdx.y;
   const int r0 = lists.off[b], G = lists.off[b + 1] - r0;
   const float *gtb = lists.boxes[b];
@@ -176,8 +191,8 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile_lists(
       if (b == B - 1) out_off[B] = r0 + G;
     }
   }
-  match_tile_body<kOdm, kFlags>(gtb, lab, nullptr, 0, G, anchors, priors, arm_scores, P, Gmax, thr, theta, obj, ovl,
-                                best_key, wcnt, npos, B, nullptr);
+  match_tile_body<kOdm, kFlags>(gtb, lab, nullptr, 0, G, m.anchors, m.priors, m.arm_scores, m.P, m.Gmax, m.thr, m.theta,
+                                m.obj, m.ovl, m.best_key, m.wcnt, m.npos, B, nullptr);
 }
 
 // k_match_final: one workgroup per image; 64 threads when Gmax <= 64 (the register form),
@@ -185,16 +200,15 @@ __global__ __launch_bounds__(kMThreads) void k_match_tile_lists(
 constexpr int kFThreads = 256;
 
 template <int kFlags>
-__global__ __launch_bounds__(kFThreads) void k_match_final(
-    const int64_t *__restrict__ labels, const int32_t *__restrict__ off,
-    unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt, int nw, int Gmax,
-    int P, float thr, const float *__restrict__ arm_scores, float theta, int32_t *__restrict__ obj,
-    float *__restrict__ ovl, int32_t *__restrict__ npos, int B) {
+__global__ __launch_bounds__(kFThreads) void k_match_final(const int64_t *__restrict__ labels,
+                                                           const int32_t *__restrict__ off, const MatchArgs m,
+                                                           int nw) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   __shared__ int s_red[16];
   STAMP_BEGIN();
-  match_final_image<kFlags, false>(blockIdx.x, labels, off, best_key, wcnt, nw, Gmax, P, thr, arm_scores, theta,
-                                   obj, ovl, npos, B, 0, ForcedOut{nullptr, nullptr, nullptr}, s_dyn, s_red);
+  match_final_image<kFlags, false>(blockIdx.x, labels, off, m.best_key, m.wcnt, nw, m.Gmax, m.P, m.thr, m.arm_scores,
+                                   m.theta, m.obj, m.ovl, m.npos, m.B, 0, ForcedOut{nullptr, nullptr, nullptr}, s_dyn,
+                                   s_red);
   STAMP_END(7, 0);
 }
 
@@ -422,25 +436,24 @@ int match_run(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt
     return launch_status("hipMemsetAsync");
   dim3 grid(ntile, B);
   const int fthreads = Gmax <= 64 ? 64 : kFThreads;
+  const MatchArgs ma{anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, ovl, w.best, w.wcnt, n_pos, B};
 #define SBOD_MATCH(ODM, FL)                                                                          \
   do {                                                                                               \
     if (lists) {                                                                                     \
-      hipLaunchKernelGGL((k_match_tile_lists<ODM, FL>), grid, dim3(kMThreads), 0, s, *lists,         \
-                         const_cast<float *>(gt_boxes), const_cast<int64_t *>(gt_labels),            \
-                         const_cast<int32_t *>(gt_offsets), anchors, priors_cxcy, arm_scores, P, Gmax, \
-                         threshold, theta, obj, ovl, w.best, w.wcnt, n_pos, B);                     \
+      KernelTimer kt("k_match_tile_lists", s, true);                                                 \
+      tlaunch(kt, (k_match_tile_lists<ODM, FL>), grid, dim3(kMThreads), 0, s, *lists,                \
+              MatchListsArgs{const_cast<float *>(gt_boxes), const_cast<int64_t *>(gt_labels),        \
+                             const_cast<int32_t *>(gt_offsets), ma});                                \
       SBOD_LAUNCHED("k_match_tile_lists");                                                           \
     } else {                                                                                         \
       KernelTimer kt("k_match_tile", s, true);                                                       \
       tlaunch(kt, (k_match_tile<ODM, FL>), grid, dim3(kMThreads), 0, s, gt_boxes, gt_labels,          \
-              gt_offsets, anchors, priors_cxcy, arm_scores, P, Gmax, threshold, theta, obj, ovl,      \
-              w.best, w.wcnt, n_pos, B, kt.span());                                                   \
+              gt_offsets, ma, kt.span());                                                             \
       SBOD_LAUNCHED("k_match_tile");                                                                 \
     }                                                                                                \
     KernelTimer kt("k_match_final", s, true);                                                        \
     tlaunch(kt, (k_match_final<FL>), dim3(B), dim3(fthreads),                                        \
-            Gmax <= 64 ? 0 : static_cast<size_t>(Gmax) * 24, s, gt_labels, gt_offsets, w.best,       \
-            w.wcnt, w.nw, Gmax, P, threshold, arm_scores, theta, obj, ovl, n_pos, B);                \
+            Gmax <= 64 ? 0 : static_cast<size_t>(Gmax) * 24, s, gt_labels, gt_offsets, ma, w.nw);   \
   } while (0)
   if (odm)
     SBOD_MATCH(true, SBOD_MATCH_ODM);

@@ -2109,13 +2109,46 @@ __host__ __device__ inline size_t inline2_lds(int window) {
 // second pass inline — its truncated classes are re-selected with window w2 by segment_body in
 // this block, then the merge is repeated (pass 2) — so no extra launches when (as usual) no
 // image needs it.
-__global__ __launch_bounds__(kMergeThreads) void k_det_merge(
-    const unsigned long long *kept, const uint32_t *kc, const unsigned long long *lastkey,
-    const DetBoxes boxes_ws, int P, int C, int window, int wfirst, int top_k, float final_nms,
-    int general, int pass, int32_t *__restrict__ need, unsigned long long *__restrict__ scratch,
-    float *__restrict__ out_boxes, int64_t *__restrict__ out_labels, float *__restrict__ out_scores,
-    int32_t *__restrict__ out_count, int32_t *out_count_host, const unsigned long long *cand,
-    uint32_t *cand_count, float thr, SegOut so) {
+// One by-value argument (the host cost of a launch grows with the argument count on this runtime:
+// scripts/micro/launch_cost.hip).
+struct MergeArgs {
+  const unsigned long long *kept;
+  const uint32_t *kc;
+  const unsigned long long *lastkey;
+  DetBoxes boxes_ws;
+  int P, C, window, wfirst, top_k;
+  float final_nms;
+  int general, pass;
+  int32_t *need;
+  unsigned long long *scratch;
+  float *out_boxes;
+  int64_t *out_labels;
+  float *out_scores;
+  int32_t *out_count, *out_count_host;
+  const unsigned long long *cand;
+  uint32_t *cand_count;
+  float thr;
+  SegOut so;
+};
+__global__ __launch_bounds__(kMergeThreads) void k_det_merge(const MergeArgs ma) {
+  const unsigned long long *kept = ma.kept;
+  const uint32_t *kc = ma.kc;
+  const unsigned long long *lastkey = ma.lastkey;
+  const DetBoxes boxes_ws = ma.boxes_ws;
+  const int P = ma.P, C = ma.C, window = ma.window, wfirst = ma.wfirst, top_k = ma.top_k;
+  const float final_nms = ma.final_nms;
+  const int general = ma.general, pass = ma.pass;
+  int32_t *__restrict__ need = ma.need;
+  unsigned long long *__restrict__ scratch = ma.scratch;
+  float *__restrict__ out_boxes = ma.out_boxes;
+  int64_t *__restrict__ out_labels = ma.out_labels;
+  float *__restrict__ out_scores = ma.out_scores;
+  int32_t *__restrict__ out_count = ma.out_count;
+  int32_t *out_count_host = ma.out_count_host;
+  const unsigned long long *cand = ma.cand;
+  uint32_t *cand_count = ma.cand_count;
+  const float thr = ma.thr;
+  const SegOut so = ma.so;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   STAMP_BEGIN();
   const int b = blockIdx.x;
@@ -2414,10 +2447,10 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
     // so the merge's dynamic LDS also covers one segment with window w2
     const size_t seg2 = two ? inline2_lds(w2) : 0;
     KernelTimer kt("k_det_merge", s, true);
-    tlaunch(kt, k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s, ws.kept,
-                       ws.kc, ws.lastkey, bxs, P, C, w2, w1, top_k, final_nms, two ? 0 : general, two ? 1 : 0,
-                       ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count, det_count_host,
-                       ws.cand, ws.count, max_overlap, so);
+    tlaunch(kt, k_det_merge, dim3(B), dim3(kMergeThreads), merge_lds > seg2 ? merge_lds : seg2, s,
+            MergeArgs{ws.kept, ws.kc, ws.lastkey, bxs, P, C, w2, w1, top_k, final_nms, two ? 0 : general,
+                      two ? 1 : 0, ws.need, ws.scratch, det_boxes, det_labels, det_scores, det_count,
+                      det_count_host, ws.cand, ws.count, max_overlap, so});
   }
   SBOD_LAUNCHED("k_det_merge");
   return SBOD_OK;
