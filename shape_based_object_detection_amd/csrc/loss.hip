@@ -1381,6 +1381,7 @@ __global__ __launch_bounds__(kHBlock) void k_hnm(const float *__restrict__ pool,
 // SBOD_LOSS_UNFUSED_FINISH): one block sums every workgroup's fp32 partials and the mining
 // segments' sums EXACTLY (128-bit fixed point, as the fused finish: the same loss bit for bit
 // whichever finish ran), falling back to a double sum when a value cannot be folded.
+constexpr int kFinThreads = 256;   // k_loss_final's block (a constant: no hidden-argument load for blockDim)
 __device__ __forceinline__ void loss_final_body(const float *__restrict__ partials, int nparts,
                                                 const float *__restrict__ hnm, int nseg,
                                                 const int32_t *__restrict__ npos_total, int reg, int cls,
@@ -1394,11 +1395,11 @@ __device__ __forceinline__ void loss_final_body(const float *__restrict__ partia
   // eight partials per thread in flight per batch (a 1-block launch: its time is load latency)
   constexpr int kB = 8;
   const float2 *p2 = reinterpret_cast<const float2 *>(partials);
-  for (int i0 = 0; i0 < nparts; i0 += kB * static_cast<int>(blockDim.x)) {
+  for (int i0 = 0; i0 < nparts; i0 += kB * kFinThreads) {
     float2 v[kB];
 #pragma unroll
     for (int k = 0; k < kB; ++k) {
-      const int i = i0 + k * static_cast<int>(blockDim.x) + tid;
+      const int i = i0 + k * kFinThreads + tid;
       v[k] = p2[min(i, nparts - 1)];   // unconditional (clamped), zeroed below: no wait at a join
       if (i >= nparts) v[k] = make_float2(0.f, 0.f);
     }
@@ -1410,7 +1411,7 @@ __device__ __forceinline__ void loss_final_body(const float *__restrict__ partia
       fl = fx128_add(fl, to_fx128(f ? v[k].y : 0.f));
     }
   }
-  for (int i = tid; i < nseg; i += blockDim.x) {
+  for (int i = tid; i < nseg; i += kFinThreads) {
     const float v = hnm[i];
     const bool f = fx_foldable(v);
     ok = ok && f;
@@ -1433,7 +1434,7 @@ __device__ __forceinline__ void loss_final_body(const float *__restrict__ partia
   bool all_ok = true;
   fc = Fx128{0ull, 0ull};
   fl = Fx128{0ull, 0ull};
-  for (int w2 = 0; w2 < static_cast<int>(blockDim.x >> 6); ++w2) {
+  for (int w2 = 0; w2 < kFinThreads / 64; ++w2) {
     fc = fx128_add(fc, Fx128{s_fx[5 * w2 + 0], s_fx[5 * w2 + 1]});
     fl = fx128_add(fl, Fx128{s_fx[5 * w2 + 2], s_fx[5 * w2 + 3]});
     all_ok = all_ok && s_fx[5 * w2 + 4] != 0ull;
@@ -1442,11 +1443,11 @@ __device__ __forceinline__ void loss_final_body(const float *__restrict__ partia
   if (!all_ok) {   // a non-finite or huge value: the double sum
     c = 0.0;
     l = 0.0;
-    for (int i = tid; i < nparts; i += blockDim.x) {
+    for (int i = tid; i < nparts; i += kFinThreads) {
       c += partials[2 * i];
       l += partials[2 * i + 1];
     }
-    for (int i = tid; i < nseg; i += blockDim.x) c += hnm[i];
+    for (int i = tid; i < nseg; i += kFinThreads) c += hnm[i];
     c = block_sum(c, s_red);
     __syncthreads();
     l = block_sum(l, s_red);
@@ -1468,7 +1469,7 @@ struct LossFinalArgs {
   float reg_weight;
   float *out;
 };
-__global__ __launch_bounds__(256) void k_loss_final(const LossFinalArgs a) {
+__global__ __launch_bounds__(kFinThreads) void k_loss_final(const LossFinalArgs a) {
   loss_final_body(a.partials, a.nparts, a.hnm, a.nseg, a.npos_total, a.reg, a.cls, a.flags, a.reg_weight, a.out);
 }
 
@@ -1631,7 +1632,7 @@ int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const in
   }
   {
     KernelTimer kt("k_loss_final", s, true);
-    tlaunch(kt, k_loss_final, dim3(1), dim3(256), 0, s,
+    tlaunch(kt, k_loss_final, dim3(1), dim3(kFinThreads), 0, s,
             LossFinalArgs{static_cast<const float *>(ws.partials), static_cast<int>(nblk),
                           static_cast<const float *>(ws.hnm), nseg, npos_total, reg, cls, flags, reg_weight,
                           loss_out});
