@@ -23,7 +23,10 @@ namespace sbod {
 
 SBOD_STAMP_DECL
 
-constexpr int kDTile = 256;
+#ifndef SBOD_DTILE
+#define SBOD_DTILE 256
+#endif
+constexpr int kDTile = SBOD_DTILE;   // k_det_prepare's rows per workgroup (A/B builds: -DSBOD_DTILE=128)
 #ifndef SBOD_PREP_GLDS
 #define SBOD_PREP_GLDS 1
 #endif
