@@ -19,6 +19,23 @@ void set_error(const char *fmt, ...) {
   va_end(ap);
 }
 
+int balanced_rows(int B, int P, int max_rows, int min_rows) {
+  static int ncu = 0;   // CUs of the device (one model per process)
+  if (ncu <= 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return max_rows;
+    ncu = n;
+  }
+  for (int k = 1; k <= 6; ++k) {
+    const int tpi = (k * ncu + B - 1) / B;   // tiles per image
+    const int rows = (((P + tpi - 1) / tpi) + 7) & ~7;
+    if (rows <= max_rows) return rows < min_rows ? min_rows : rows;
+  }
+  return max_rows;
+}
+
 int launch_status(const char *what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

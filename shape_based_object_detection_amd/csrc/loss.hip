@@ -386,6 +386,7 @@ struct LossArgs {
   unsigned long long *forced; // [B][Gmax] (prior << 32 | object) rewritten by the forced match
   int32_t *nforced;           // [B]
   void *recs;                 // fused finish: [nblk] 16-byte records {conf, tag, loc, tag}
+  int rows = kLTile;          // rows (priors) per k_multibox tile (mb_rows; the one-launch form: kLTile)
 };
 
 // The fused finish of k_multibox (focal / no mining).  Each workgroup folds its partial sums
@@ -1063,9 +1064,9 @@ __global__ __launch_bounds__(kLTile, (CM > 24 ? 5 : 6)) void k_multibox(LossArgs
   span_begin(a.span);
   PHASE_DECL;
   SEG_PHASE(0);
-  const int b = blockIdx.y, p0 = blockIdx.x * kLTile, tid = threadIdx.x;
+  const int b = blockIdx.y, p0 = blockIdx.x * a.rows, tid = threadIdx.x;
   const int P = a.P, C = a.C;
-  const int np = min(kLTile, P - p0);
+  const int np = min(a.rows, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
   const bool valid = tid < np;
   const int64_t ic = rbase + (valid ? tid : 0);
@@ -1581,8 +1582,12 @@ struct LossWs {
   size_t zero_bytes;   // the fused finish's state: its words (`fin`) and records, left zero
   size_t bytes;
 };
+// Rows per k_multibox tile (balanced_rows, sbod_common.h); the workspaces are sized for
+// kLMinRows-row tiles.
+constexpr int kLMinRows = 64;
+inline int mb_rows(int B, int P) { return balanced_rows(B, P, kLTile, kLMinRows); }
 LossWs carve(void *w, int B, int P) {
-  const size_t nblk = static_cast<size_t>(B) * ((P + kLTile - 1) / kLTile);
+  const size_t nblk = static_cast<size_t>(B) * ((P + kLMinRows - 1) / kLMinRows);   // the most tiles mb_rows makes
   LossWs r;
   // the fused finish's state first (zero on entry, SBOD_LOSS_WS_ZEROED): its words, then one
   // record per workgroup; no other pass writes them
@@ -1607,7 +1612,8 @@ int mine_and_finish(const void *scores, int dtype, int B, int P, int C, const in
                     const int32_t *npos_total, int reg, int cls, int flags, int neg_pos_ratio,
                     float reg_weight, const float *pool, int64_t n_all, int64_t local_off,
                     void *grad_scores, float *loss_out, const LossWs &ws, hipStream_t s) {
-  const int nblk = B * ((P + kLTile - 1) / kLTile);
+  const int rows = mb_rows(B, P);
+  const int nblk = B * ((P + rows - 1) / rows);
   int nseg = 0;
   if (cls == SBOD_CLS_CE) {
     const int global = (flags & SBOD_POOL_GLOBAL_NEG) ? 1 : 0;
@@ -1929,9 +1935,10 @@ int sbod_multibox_loss(const void *locs, const void *scores, int dtype, int B, i
              focal_alpha, 1.f - focal_alpha, focal_gamma, ws.partials, ws.pool, nullptr,
              fused ? ws.fin : nullptr, loss_out};
   a.recs = ws.recs;
-  dim3 grid((P + kLTile - 1) / kLTile, B);
+  a.rows = mb_rows(B, P);
+  dim3 grid((P + a.rows - 1) / a.rows, B);
   // + 8 floats: the register path's constant-offset row reads may run up to 7 past the last row
-  const size_t lds = (static_cast<size_t>(kLTile) * C + 8) * sizeof(float);
+  const size_t lds = (static_cast<size_t>(a.rows) * C + 8) * sizeof(float);
   {
     KernelTimer kt("k_multibox", s, true);
     a.span = kt.span();

@@ -471,6 +471,7 @@ struct DetArgs {
   uint32_t *cand_count;            // [B,C]
   float *dbg_probs, *dbg_boxes;
   SpanRing *span;                  // KernelTimer span ring under graph capture, else null
+  int rows = kDTile;               // rows (priors) per k_det_prepare tile
 };
 
 // exp(x) and the logistic function on the hardware exp2 / rcp units (~1-2 ulp; the detect path's
@@ -532,14 +533,14 @@ __global__ __launch_bounds__(kDTile) void k_det_prepare(DetArgs a, T *__restrict
   extern __shared__ float s_sc[];
   STAMP_BEGIN();
   span_begin(a.span);
-  const int b = blockIdx.y, p0 = blockIdx.x * kDTile, tid = threadIdx.x, lane = tid & 63;
+  const int b = blockIdx.y, p0 = blockIdx.x * a.rows, tid = threadIdx.x, lane = tid & 63;
   const int P = a.P, C = CE > 0 ? CE : a.C;
   T *const s_tile = reinterpret_cast<T *>(s_sc);
   unsigned long long *s_balf = reinterpret_cast<unsigned long long *>(s_tile + kDTile * C);
   uint32_t *s_wbf = reinterpret_cast<uint32_t *>(s_balf + (kDTile / 64) * C);   // per-wave slot bases
 #define s_bal(w, c) s_balf[(w) * C + (c)]
 #define s_wb(w, c) s_wbf[(w) * C + (c)]
-  const int np = min(kDTile, P - p0);
+  const int np = min(a.rows, P - p0);
   const int64_t rbase = static_cast<int64_t>(b) * P + p0;
 #ifdef SBOD_PHASE_CLOCKS
   long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -2383,13 +2384,15 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
     return launch_status("hipMemsetAsync(detect)");
   DetArgs a{B, P, C, box_type, act, priors_cxcy, pos_mask, min_score, ws.cand, ws.count,
             debug_probs, debug_boxes, nullptr};
+  // a.rows stays kDTile: balanced tiles (216 rows, six workgroups per CU at SSD512 B = 32) made
+  // this kernel slower, 12.92 / 12.96 vs 12.58 / 12.54 us (the loss pass gains from them)
   // decoded on demand (det_box); without priors (CENTER / CORNER boxes) the dummy prior loads
   // read the output buffer's first 16 bytes (values unused)
   const DetBoxes bxs{locs, priors_cxcy ? priors_cxcy : det_boxes, P, box_type, bf16 ? 1 : 0};
   {
     KernelTimer kt("k_det_prepare", s, true);
     a.span = kt.span();
-    const dim3 pg((P + kDTile - 1) / kDTile, B);
+    const dim3 pg((P + a.rows - 1) / a.rows, B);
     const size_t pl = static_cast<size_t>(kDTile) * C * (bf16 ? 2 : 4) + (kDTile / 64) * C * 12;
     uint16_t *lh = reinterpret_cast<uint16_t *>(locs);
     const uint16_t *sh = reinterpret_cast<const uint16_t *>(scores);
@@ -2406,7 +2409,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
     else if (C == 21) tlaunch(kt, k_det_prepare<24, 21>, pg, dim3(kDTile), pl, s, a, lf, sf);
     else if (C <= 24) tlaunch(kt, k_det_prepare<24, 0>, pg, dim3(kDTile), pl, s, a, lf, sf);
     else if (C <= 32) tlaunch(kt, k_det_prepare<32, 0>, pg, dim3(kDTile), pl, s, a, lf, sf);
-    else tlaunch(kt, k_det_prepare<0, 0>, dim3((P + kDTile - 1) / kDTile, B), dim3(kDTile),
+    else tlaunch(kt, k_det_prepare<0, 0>, pg, dim3(kDTile),
                  static_cast<size_t>(kDTile) * C * 4 + (kDTile / 64) * C * 12, s, a, lf, sf);
   }
   SBOD_LAUNCHED("k_det_prepare");

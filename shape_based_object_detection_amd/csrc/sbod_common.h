@@ -19,6 +19,14 @@ namespace sbod {
 
 void set_error(const char *fmt, ...);
 int launch_status(const char *what);  // hipGetLastError -> SBOD_OK / SBOD_E_HIP
+// Rows per tile of a one-round kernel over B images x P rows (k_multibox, k_det_prepare): every
+// workgroup of such a launch loads, computes and stores in lockstep, so it lasts as long as its
+// busiest CU.  The tile is sized for the fewest workgroups that give every CU the same count (k
+// per CU, k <= 6) as long as a tile stays within max_rows — SSD512 (P = 10,248) at B = 32: 1,536
+// tiles of 216 rows, six per CU, instead of 1,312 of 256 (five or six per CU); at B = 16: 768
+// (three per CU) instead of 656 (two or three) — else max_rows.  A multiple of 8 rows (whole
+// 16-byte chunks of fp32 and bf16 rows when P % 8 == 0), at least min_rows.
+int balanced_rows(int B, int P, int max_rows, int min_rows);
 
 constexpr int kWave = 64;
 constexpr float kIouEps = 1e-5f;  // metrics.py:233 EPS (compared as float32, like torch)
