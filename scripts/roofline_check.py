@@ -38,8 +38,10 @@ def main(bench_json, trace_csv, out=None, prof_log=None):
         algo['k_det_prepare'] = rl['algorithmic_bytes_per_launch']
     else:
         algo['k_det_prepare'] = line['step_algorithmic_bytes'] - BM.criterion_bytes(B, P, C)
-    grid_x = 256 * ((P + 255) // 256)
-    durs = {k: [] for k in algo}
+    # the bench workload's dispatches are the ones with Grid_Size_Y == B; tile heights differ per
+    # kernel (k_multibox's are sized per CU count, balanced_rows), so each kernel keeps its most
+    # frequent grid rather than an assumed 256-row one
+    durs = {k: {} for k in algo}
     win, wdurs = None, []
     if prof_log:
         for ln in open(prof_log):
@@ -63,11 +65,14 @@ def main(bench_json, trace_csv, out=None, prof_log=None):
                 if k in algo:
                     if 'unsigned short' in name:      # the bf16 (C2) instantiation
                         continue
-                    if int(r['Grid_Size_X']) == grid_x and int(r['Grid_Size_Y']) == B:
+                    if int(r['Grid_Size_Y']) == B:
                         t0, t1 = int(r['Start_Timestamp']), int(r['End_Timestamp'])
-                        durs[k].append(t1 - t0)
-                        if k == rl['kernel'] and win and win[0] <= t0 and t1 <= win[1]:
-                            wdurs.append(t1 - t0)
+                        durs[k].setdefault(int(r['Grid_Size_X']), []).append((t0, t1))
+    for k, byg in list(durs.items()):
+        d = max(byg.values(), key=len) if byg else []
+        durs[k] = [t1 - t0 for t0, t1 in d]
+        if k == rl['kernel'] and win:
+            wdurs = [t1 - t0 for t0, t1 in d if win[0] <= t0 and t1 <= win[1]]
     res = {'bench': os.path.basename(bench_json), 'trace': os.path.basename(trace_csv),
            'workload': {'B': B, 'P': P, 'C': C}, 'peak_GBps': BM.HBM_PEAK_GBS, 'kernels': {}}
     for k, d in durs.items():
