@@ -191,8 +191,10 @@ PyObject *stage_and_replay(PyObject *, PyObject *const *a, Py_ssize_t n) {
 //     pack = (capacity, per_image_cap, device, out_boxes, out_labels, out_offsets, stream);
 //     crit_args / det_args = the recorded argument tuples of sbod_criterion_focal /
 //     sbod_detect_f32 (include/sbod.h order; pointers as int or None).
-//   submit_step_program(capsule, boxes, labels) -> True | None | int
+//   submit_step_program(capsule, boxes, labels[, parts]) -> True | None | int
 //     None: the lists need the Python path (nothing launched); int: a failing sbod status.
+//     parts (default 3): bit 0 the GT packing + criterion, bit 1 the detect + event — one chain
+//     alone is a diagnostic (scripts/gpu_interval.py), the step submits both.
 //   The lists are taken as ready on the packing stream (resident device tensors), which is the
 //   criterion's stream.  With `lists` true the packing is folded into the matcher's first launch
 //   (sbod_criterion_focal_lists) whenever the batch allows it (<= 64 images, each 1..Gmax
@@ -335,12 +337,31 @@ PyObject *submit_profile(PyObject *, PyObject *const *a, Py_ssize_t n) {
 }
 
 PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
-  if (n != 3) {
-    PyErr_SetString(PyExc_TypeError, "submit_step_program(program, boxes, labels)");
+  if (n != 3 && n != 4) {
+    PyErr_SetString(PyExc_TypeError, "submit_step_program(program, boxes, labels[, parts])");
     return nullptr;
   }
   auto *p = static_cast<StepProgram *>(PyCapsule_GetPointer(a[0], "sbod.StepProgram"));
   if (!p) return nullptr;
+  const long parts = n == 4 ? PyLong_AsLong(a[3]) : 3;
+  if (parts < 1 || parts > 3) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "submit_step_program: parts must be 1, 2 or 3");
+    return nullptr;
+  }
+  if (!(parts & 1)) {   // detect (+ event) alone: no lists, no packing
+    auto t = SteadyClock::now();
+    const int sd = sbod_detect_f32(p->d_locs, p->d_scores, p->d_B, p->d_P, p->d_C, p->d_pri, p->d_pm, p->d_box,
+                                   p->d_act, p->d_min, p->d_ovl, p->d_topk, p->d_fnms, p->d_window, p->d_flags,
+                                   p->d_boxes, p->d_labels, p->d_scores_out, p->d_count, p->d_count_host,
+                                   p->d_dbg_p, p->d_dbg_b, p->d_ws, p->d_wsb, p->d_stream);
+    if (sd != SBOD_OK) return PyLong_FromLong(sd);
+    if (p->event) {
+      const int se = sbod_event_record(p->event, p->ev_stream);
+      if (se != SBOD_OK) return PyLong_FromLong(se);
+    }
+    g_sub_ns[2] += ns_since(t);
+    Py_RETURN_TRUE;
+  }
   auto t_start = SteadyClock::now(), t = t_start;
   double ph[4] = {0.0, 0.0, 0.0, 0.0};
   ListRows rows;
@@ -378,6 +399,7 @@ PyObject *submit_step_program(PyObject *, PyObject *const *a, Py_ssize_t n) {
                               p->c_ws, p->c_wsb, p->c_stream);
   if (st != SBOD_OK) return PyLong_FromLong(st);
   g_sub_ns[1] += ph[1] = ns_since(t);
+  if (!(parts & 2)) Py_RETURN_TRUE;   // the criterion alone
   st = sbod_detect_f32(p->d_locs, p->d_scores, p->d_B, p->d_P, p->d_C, p->d_pri, p->d_pm, p->d_box, p->d_act,
                        p->d_min, p->d_ovl, p->d_topk, p->d_fnms, p->d_window, p->d_flags, p->d_boxes, p->d_labels,
                        p->d_scores_out, p->d_count, p->d_count_host, p->d_dbg_p, p->d_dbg_b, p->d_ws, p->d_wsb,
@@ -556,7 +578,7 @@ PyMethodDef methods[] = {
      "submit_profile([reset]) -> host time of submit_step_program by phase (us, summed over calls)."},
     {"submit_step_program",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(submit_step_program)),
-     METH_FASTCALL, "GT packing + the recorded criterion and detect calls + the event, natively."},
+     METH_FASTCALL, "GT packing + the recorded criterion and detect calls + the event, natively (parts: 1 criterion, 2 detect, 3 both)."},
     {"pack_device_lists",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(pack_device_lists)),
      METH_FASTCALL, "Check and pack per-image device GT lists with one sbod_gt_pack launch."},

@@ -120,3 +120,7 @@ def test_step_program_rejects_malformed_recordings(ext):
     b = [torch.zeros(3, 4)]
     l = [torch.zeros(3, dtype=torch.long)]
     assert ext.submit_step_program(prog, b, l) is None                       # CPU lists: Python path
+    assert ext.submit_step_program(prog, b, l, 1) is None                    # the criterion alone too
+    for bad in (0, 4, -1):                                                   # parts: 1, 2 or 3
+        with pytest.raises(ValueError):
+            ext.submit_step_program(prog, b, l, bad)
