@@ -11,6 +11,8 @@ segment, merge).  If both ~ criterion + detect, the two chains contend for the s
 both ~ max of the two, one chain sets the step.
 
     python scripts/gpu_interval.py [--n1 10] [--n2 40] [--reps 3] [--crit-streams 2] [--det-streams 2]
+                                   [--batches 6] [--det-form two|one] [--finish separate|fused]
+                                   (GPU_MAX_HW_QUEUES from the environment)
 """
 import json
 import os
@@ -33,8 +35,9 @@ def main():
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     L.lib()
-    st = bench.Step(dev, 32, 0, 1, graph=True, priority='detect', n_batches=6,
-                    crit_streams=arg('--crit-streams', 2), det_streams=arg('--det-streams', 2))
+    st = bench.Step(dev, 32, 0, 1, graph=True, priority='detect', n_batches=arg('--batches', 6),
+                    crit_streams=arg('--crit-streams', 2), det_streams=arg('--det-streams', 2),
+                    det_form=arg('--det-form', 'two'), finish=arg('--finish', 'separate'))
     for _ in range(4):
         st.eager_split()
     torch.cuda.synchronize()
@@ -81,7 +84,9 @@ def main():
         return gpu_ms, host_ms
 
     out = {'n1': n1, 'n2': n2, 'spin_cycles_per_ms': round(per_ms), 'crit_streams': len(st.cap_streams),
-           'det_streams': len(st.det_streams), 'modes': {}}
+           'batches': len(st.batches), 'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'),
+           'det_streams': len(st.det_streams), 'det_form': arg('--det-form', 'two'),
+           'finish': arg('--finish', 'separate'), 'modes': {}}
     names = {3: 'both', 1: 'criterion', 2: 'detect'}
     for rep in range(reps):
         for parts in (3, 1, 2):
@@ -96,7 +101,9 @@ def main():
             print(json.dumps(dict(mode=names[parts], **rec)), flush=True)
     summ = {m: sorted(r['interval_us'] for r in v) for m, v in out['modes'].items()}
     print(json.dumps({'summary_interval_us': summ, 'crit_streams': out['crit_streams'],
-                      'det_streams': out['det_streams']}), flush=True)
+                      'det_streams': out['det_streams'], 'batches': out['batches'],
+                      'hw_queues': out['hw_queues'], 'det_form': out['det_form'],
+                      'finish': out['finish']}), flush=True)
 
 
 if __name__ == '__main__':
