@@ -1566,10 +1566,16 @@ __device__ __forceinline__ void segment_w(
 #endif
 }
 
-__global__ __launch_bounds__(256) void k_det_segment_w4(
+#ifndef SBOD_SEG_W
+#define SBOD_SEG_W 4
+#endif
+// waves per pass-1 segment workgroup.  A/B builds: -DSBOD_SEG_W=8 made the kernel 0.6 us faster
+// alone but the pipelined step's GPU interval 34.0-34.9 vs 30.5-31.7 us (r6_det_ab_a.jsonl)
+constexpr int kSegPassW = SBOD_SEG_W;
+__global__ __launch_bounds__(64 * kSegPassW) void k_det_segment_w4(
     const unsigned long long *__restrict__ cand, const uint32_t *__restrict__ cand_count,
     const DetBoxes boxes_ws, int P, int C, int window, int stride, float thr, SegOut o) {
-  segment_w<4, false>(cand, cand_count, boxes_ws, P, C, window, stride, thr, o);
+  segment_w<kSegPassW, false>(cand, cand_count, boxes_ws, P, C, window, stride, thr, o);
 }
 
 // ----------------------------------------------------------------------------- K3
@@ -2440,7 +2446,7 @@ int sbod_detect_f32(void *locs, const void *scores, int B, int P, int C,
       tlaunch(kt, k_det_segment_wave, dim3(C - 1, B), dim3(64), 0, s, ws.cand, ws.count, bxs,
                          P, C, w1, w2, max_overlap, so, nullptr);
 #else
-      tlaunch(kt, k_det_segment_w4, dim3(C - 1, B), dim3(256), 0, s, ws.cand, ws.count, bxs,
+      tlaunch(kt, k_det_segment_w4, dim3(C - 1, B), dim3(64 * kSegPassW), 0, s, ws.cand, ws.count, bxs,
                          P, C, w1, w2, max_overlap, so);
 #endif
     else
