@@ -12,6 +12,7 @@ both ~ max of the two, one chain sets the step.
 
     python scripts/gpu_interval.py [--n1 10] [--n2 40] [--reps 3] [--crit-streams 2] [--det-streams 2]
                                    [--batches 6] [--det-form two|one] [--finish separate|fused]
+                                   [--crit-cu-reserve K [--mask spread|block]]
                                    (GPU_MAX_HW_QUEUES from the environment)
 """
 import json
@@ -38,6 +39,30 @@ def main():
     st = bench.Step(dev, 32, 0, 1, graph=True, priority='detect', n_batches=arg('--batches', 6),
                     crit_streams=arg('--crit-streams', 2), det_streams=arg('--det-streams', 2),
                     det_form=arg('--det-form', 'two'), finish=arg('--finish', 'separate'))
+    reserve = arg('--crit-cu-reserve', 0)
+    if reserve > 0:
+        # criterion streams on a CU-masked queue that leaves `reserve` CUs to the detect chain
+        # (hipExtStreamCreateWithCUMask; the detect streams keep every CU and their priority)
+        import ctypes
+        hip = ctypes.CDLL('libamdhip64.so')
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        pattern = arg('--mask', 'spread')
+        off = set(range(ncu - reserve, ncu)) if pattern == 'block' else \
+            {i for i in range(ncu) if i % (ncu // reserve) == ncu // reserve - 1}
+        words = (ncu + 31) // 32
+        mask = (ctypes.c_uint32 * words)()
+        for i in range(ncu):
+            if i not in off:
+                mask[i // 32] |= 1 << (i % 32)
+        streams_new = []
+        for _ in st.cap_streams:
+            h = ctypes.c_void_p()
+            rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask)
+            if rc != 0:
+                raise RuntimeError('hipExtStreamCreateWithCUMask: %d' % rc)
+            streams_new.append(torch.cuda.ExternalStream(h.value, device=dev))
+        st.cap_streams = streams_new
+        st.cap_stream = streams_new[0]
     for _ in range(4):
         st.eager_split()
     torch.cuda.synchronize()
@@ -86,7 +111,8 @@ def main():
     out = {'n1': n1, 'n2': n2, 'spin_cycles_per_ms': round(per_ms), 'crit_streams': len(st.cap_streams),
            'batches': len(st.batches), 'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'),
            'det_streams': len(st.det_streams), 'det_form': arg('--det-form', 'two'),
-           'finish': arg('--finish', 'separate'), 'modes': {}}
+           'finish': arg('--finish', 'separate'), 'crit_cu_reserve': arg('--crit-cu-reserve', 0),
+           'mask': arg('--mask', 'spread'), 'modes': {}}
     names = {3: 'both', 1: 'criterion', 2: 'detect'}
     for rep in range(reps):
         for parts in (3, 1, 2):
@@ -103,7 +129,8 @@ def main():
     print(json.dumps({'summary_interval_us': summ, 'crit_streams': out['crit_streams'],
                       'det_streams': out['det_streams'], 'batches': out['batches'],
                       'hw_queues': out['hw_queues'], 'det_form': out['det_form'],
-                      'finish': out['finish']}), flush=True)
+                      'finish': out['finish'], 'crit_cu_reserve': out['crit_cu_reserve'],
+                      'mask': out['mask']}), flush=True)
 
 
 if __name__ == '__main__':
