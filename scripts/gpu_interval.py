@@ -12,7 +12,7 @@ both ~ max of the two, one chain sets the step.
 
     python scripts/gpu_interval.py [--n1 10] [--n2 40] [--reps 3] [--crit-streams 2] [--det-streams 2]
                                    [--batches 6] [--det-form two|one] [--finish separate|fused]
-                                   [--crit-cu-reserve K [--mask spread|block]]
+                                   [--crit-cu-reserve K [--mask spread|block]] [--shared-streams]
                                    (GPU_MAX_HW_QUEUES from the environment)
 """
 import json
@@ -63,6 +63,10 @@ def main():
             streams_new.append(torch.cuda.ExternalStream(h.value, device=dev))
         st.cap_streams = streams_new
         st.cap_stream = streams_new[0]
+    if '--shared-streams' in sys.argv:
+        # each step's criterion and detect on ONE stream (the criterion's), steps over the streams
+        st.det_streams = st.cap_streams
+        st.det_stream = st.cap_stream
     for _ in range(4):
         st.eager_split()
     torch.cuda.synchronize()
@@ -112,7 +116,7 @@ def main():
            'batches': len(st.batches), 'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'),
            'det_streams': len(st.det_streams), 'det_form': arg('--det-form', 'two'),
            'finish': arg('--finish', 'separate'), 'crit_cu_reserve': arg('--crit-cu-reserve', 0),
-           'mask': arg('--mask', 'spread'), 'modes': {}}
+           'mask': arg('--mask', 'spread'), 'shared_streams': '--shared-streams' in sys.argv, 'modes': {}}
     names = {3: 'both', 1: 'criterion', 2: 'detect'}
     for rep in range(reps):
         for parts in (3, 1, 2):
@@ -130,7 +134,7 @@ def main():
                       'det_streams': out['det_streams'], 'batches': out['batches'],
                       'hw_queues': out['hw_queues'], 'det_form': out['det_form'],
                       'finish': out['finish'], 'crit_cu_reserve': out['crit_cu_reserve'],
-                      'mask': out['mask']}), flush=True)
+                      'mask': out['mask'], 'shared_streams': out['shared_streams']}), flush=True)
 
 
 if __name__ == '__main__':
