@@ -345,3 +345,44 @@ def test_bench_pipelined_step_equals_eager(depth, two, submit, fold):
                 assert torch.equal(a, b)
     for i, bt in enumerate(st.batches):   # the captured backward left the same gradients
         assert torch.equal(bt.locs.grad, ref[i][1]) and torch.equal(bt.scores.grad, ref[i][2])
+
+
+def test_step_program_parts_equal_whole():
+    """The native step submit's ``parts`` mask (scripts/gpu_interval.py submits one chain alone):
+    the GT packing + criterion (parts=1) and the detect + event (parts=2) issued as two calls leave
+    the same loss, gradients and per-image detections as the eager step on the same batch — the
+    same launches as the whole submit (parts=3) that test_bench_pipelined_step_equals_eager checks."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    if L.host_ext is None:
+        pytest.skip('the _sbodhost extension is not built')
+    st = bench.Step(DEV, 4, 0, 1, graph=True, priority='detect', n_batches=4, det_streams=2, crit_streams=2,
+                    depth=4, submit='direct', gt_fold=True)
+    ref = []
+    for bt in st.batches:
+        loss, dets = st.eager_split()
+        ref.append((loss.item(), bt.locs.grad.clone(), bt.scores.grad.clone(),
+                    [[t.clone() for t in part] for part in dets]))
+    for _ in range(2):
+        st.eager_split()
+    torch.cuda.synchronize()
+    st.capture()
+    assert all(p is not None for p in st.programs)
+    for k in range(len(st.batches)):
+        i = st.k % len(st.slots)
+        bt = st._next_batch()
+        _, _, loss, h = st.slots[i]
+        order = (2, 1) if k % 2 else (1, 2)   # either chain first
+        for parts in order:
+            assert L.host_ext.submit_step_program(st.programs[i], bt.boxes, bt.labels, parts) is True
+        dets = h.rearmed().wait()
+        torch.cuda.synchronize()
+        rl, rgl, rgs, rd = ref[i]
+        assert loss.item() == rl
+        assert torch.equal(bt.locs.grad, rgl) and torch.equal(bt.scores.grad, rgs)
+        for part, rpart in zip(dets, rd):
+            assert len(part) == len(rpart) == 4
+            for a, b in zip(part, rpart):
+                assert torch.equal(a, b)
