@@ -112,16 +112,39 @@ __device__ __forceinline__ void match_tile_body(
     const float *__restrict__ arm_scores, int P, int Gmax, float thr, float theta, int32_t *__restrict__ obj,
     float *__restrict__ ovl, unsigned long long *__restrict__ best_key, int32_t *__restrict__ wcnt,
     int32_t *__restrict__ npos, int B, SpanRing *span) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_od[kMThreads / 64][kSlots][64];   // per wave
+  __shared__ __attribute__((aligned(16))) uint32_t s_od[kMThreads / 64][kSlots][64 * SBOD_MATCH_PPL];   // per wave
   __shared__ int s_slot[kMThreads / 64][kSlots];
   STAMP_BEGIN();
   span_begin(span);
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   if (blockIdx.x == 0 && b == 0 && tid == 0) npos[B] = 0;   // k_match_final accumulates
-  const int wbase = blockIdx.x * kMThreads + (tid & ~63), wv = tid >> 6;
+  const int wbase = blockIdx.x * kMPriors + SBOD_MATCH_PPL * (tid & ~63), wv = tid >> 6;
   // this workgroup's shard of the image's keys (kKeyShards copies: the waves of one image spread
   // their atomics over kKeyShards words per object instead of queueing on one)
   unsigned long long *brow = best_key + (static_cast<int64_t>(b) * kKeyShards + (blockIdx.x & (kKeyShards - 1))) * Gmax;
+  // the wave's positive count per 64 priors, one plain store each (summed by k_match_final)
+  int32_t *wc = wcnt + static_cast<int64_t>(b) * (gridDim.x * (kMPriors / 64)) + (wbase >> 6);
+#if SBOD_MATCH_PPL == 2
+  MatchLane ma, mb;
+  match_wave2<kOdm, kFlags>(gt, labels, off, anchors, priors, arm_scores, P, b, wbase, brow, s_od[wv], s_slot[wv],
+                            g0_in, G_in, ma, mb);
+  if (ma.valid) {
+    const int64_t i = static_cast<int64_t>(b) * P + ma.p;
+    obj[i] = ma.bi;
+    ovl[i] = ma.best;
+  }
+  if (mb.valid) {
+    const int64_t i = static_cast<int64_t>(b) * P + mb.p;
+    obj[i] = mb.bi;
+    ovl[i] = mb.best;
+  }
+  const int na = __popcll(__ballot(phase1_positive<kOdm>(ma, thr, theta)));
+  const int nb = __popcll(__ballot(phase1_positive<kOdm>(mb, thr, theta)));
+  if (lane == 0) {
+    wc[0] = na;
+    wc[1] = nb;
+  }
+#else
   const MatchLane m = match_wave<kOdm, kFlags>(gt, labels, off, anchors, priors, arm_scores, P, b, wbase, brow,
                                                s_od[wv], s_slot[wv], g0_in, G_in);
   if (m.valid) {
@@ -130,9 +153,9 @@ __device__ __forceinline__ void match_tile_body(
     ovl[i] = m.best;
   }
   const bool pos = phase1_positive<kOdm>(m, thr, theta);
-  // the wave's positive count, one plain store per wave (summed by k_match_final)
   const int n = __popcll(__ballot(pos));
-  if (lane == 0) wcnt[static_cast<int64_t>(b) * (gridDim.x * (kMThreads / 64)) + (wbase >> 6)] = n;
+  if (lane == 0) wc[0] = n;
+#endif
   span_end(span);
   STAMP_END(5, 1);
 }
@@ -371,7 +394,7 @@ struct MatchWs {
 };
 MatchWs carve_match(void *w, int B, int Gmax, int P) {
   MatchWs r;
-  r.nw = ((P + kMThreads - 1) / kMThreads) * (kMThreads / 64);
+  r.nw = ((P + kMPriors - 1) / kMPriors) * (kMPriors / 64);
   size_t o = 0;
   r.best = ws_at<unsigned long long>(w, o);
   o += align_up(static_cast<size_t>(B) * kKeyShards * Gmax * 8);
@@ -428,7 +451,7 @@ int match_run(const float *gt_boxes, const int64_t *gt_labels, const int32_t *gt
     set_error("%s: workspace %zu < %zu", who, workspace_bytes, need);
     return SBOD_E_WORKSPACE;
   }
-  const int ntile = (P + kMThreads - 1) / kMThreads;
+  const int ntile = (P + kMPriors - 1) / kMPriors;
   MatchWs w = carve_match(workspace, B, Gmax, P);
   // the keys and counts must be zero on entry: every call leaves them so (k_match_final), so
   // only a workspace the caller does not know to be clean is zeroed here (not capturable)

@@ -20,6 +20,10 @@
 namespace sbod {
 
 constexpr int kMThreads = 256;  // matcher tile: one prior per thread
+#ifndef SBOD_MATCH_PPL
+#define SBOD_MATCH_PPL 1           // priors per lane in k_match_tile (A/B builds: 2, match_wave2)
+#endif
+constexpr int kMPriors = kMThreads * SBOD_MATCH_PPL;   // priors per k_match_tile workgroup
 constexpr int kKeyShards = 8;   // copies of the per-object key words (one per XCD-sized group of tiles)
 constexpr int kSlots = 16;      // per-wave LDS rows of pending per-object ords
 
@@ -224,6 +228,140 @@ __device__ __forceinline__ MatchLane match_wave(const float *__restrict__ gt, co
   MATCH_WAVE_MARK(3, static_cast<uint32_t>(nslot));
   return MatchLane{p, bi, blab, best, valid, eas0, eas1};
 }
+
+#if SBOD_MATCH_PPL == 2
+// match_wave2 (A/B build -DSBOD_MATCH_PPL=2): match_wave with TWO priors per lane — the wave's
+// 128 priors [wbase, wbase + 128), lane l holding wbase + l and wbase + 64 + l — so the tile
+// covers 512 priors and the grid is half as large; the object's readlanes are shared by the two
+// IoUs and the two chains are independent.  Per prior the same arithmetic in the same object
+// order (first index on ties); the per-object key row holds the wave's 128 ords (s_od[slot][128]).
+template <bool kOdm, int kFlags>
+__device__ __forceinline__ void match_wave2(const float *__restrict__ gt, const int64_t *__restrict__ labels,
+                                            const int32_t *__restrict__ off, const float *__restrict__ anchors,
+                                            const float *__restrict__ priors, const float *__restrict__ arm_scores,
+                                            int P, int b, int wbase, unsigned long long *brow, uint32_t (*s_od)[128],
+                                            int *s_slot, int g0_in, int G_in, MatchLane &ra, MatchLane &rb) {
+  const int lane = threadIdx.x & 63;
+  const int pA = wbase + lane, pB = wbase + 64 + lane;
+  const bool validA = pA < P, validB = pB < P;
+  const int pcA = min(pA, P - 1), pcB = min(pB, P - 1);
+  const Box4 arA = ld4(kOdm ? anchors + 4 * (static_cast<int64_t>(b) * P + pcA) : anchors + 4 * static_cast<int64_t>(pcA));
+  const Box4 arB = ld4(kOdm ? anchors + 4 * (static_cast<int64_t>(b) * P + pcB) : anchors + 4 * static_cast<int64_t>(pcB));
+  const Box4 apA = kOdm ? ld4(priors + 4 * pcA) : Box4{0.f, 0.f, 0.f, 0.f};
+  const Box4 apB = kOdm ? ld4(priors + 4 * pcB) : Box4{0.f, 0.f, 0.f, 0.f};
+  const int g0 = g0_in >= 0 ? g0_in : ld_i32_uniform(off + b);
+  const int G = g0_in >= 0 ? G_in : ld_i32_uniform(off + b + 1) - g0;
+  const bool has = G > 0;
+  GtLane o = load_gt_lane<kFlags>(gt, labels, has ? g0 : 0, 0, has ? min(G, 64) : 1, lane);
+  float eA0 = 0.f, eA1 = 0.f, eB0 = 0.f, eB1 = 0.f;
+  if constexpr (kOdm) {
+    const int64_t icA = static_cast<int64_t>(b) * P + pcA, icB = static_cast<int64_t>(b) * P + pcB;
+    eA0 = arm_scores[2 * icA];
+    eA1 = arm_scores[2 * icA + 1];
+    eB0 = arm_scores[2 * icB];
+    eB1 = arm_scores[2 * icB + 1];
+  }
+  const Anchor aA = make_anchor<kOdm>(arA, apA), aB = make_anchor<kOdm>(arB, apB);
+  const bool liveA = validA && !aA.zero, liveB = validB && !aB.zero;
+  const uint32_t wx1 = ~wave_max_u32(max(liveA ? ~f2ord(aA.x1) : 0u, liveB ? ~f2ord(aB.x1) : 0u));
+  const uint32_t wy1 = ~wave_max_u32(max(liveA ? ~f2ord(aA.y1) : 0u, liveB ? ~f2ord(aB.y1) : 0u));
+  const uint32_t wx2 = wave_max_u32(max(liveA ? f2ord(aA.x2) : 0u, liveB ? f2ord(aB.x2) : 0u));
+  const uint32_t wy2 = wave_max_u32(max(liveA ? f2ord(aA.y2) : 0u, liveB ? f2ord(aB.y2) : 0u));
+  const bool wlive = __ballot(liveA || liveB) != 0ull;
+  float bestA = 0.f, bestB = 0.f;
+  int biA = 0, blabA = 0, biB = 0, blabB = 0;
+  // metrics.py:224-250, in the reference's order (as match_wave's iou_of), for both priors
+  auto iou2 = [&](int j, int &glab, float &ovA, float &ovB) {
+    const float tx1 = rl_f(o.x1, j), ty1 = rl_f(o.y1, j), tx2 = rl_f(o.x2, j), ty2 = rl_f(o.y2, j);
+    const float garea = rl_f(o.area, j);
+    const int gzero = __builtin_amdgcn_readlane(o.zero, j);
+    glab = __builtin_amdgcn_readlane(o.lab, j);
+    auto one = [&](const Anchor &a) {
+      float iw = fminf(tx2, a.x2) - fmaxf(tx1, a.x1);
+      if (iw < 0.f) iw = 0.f;
+      float ih = fminf(ty2, a.y2) - fmaxf(ty1, a.y1);
+      if (ih < 0.f) ih = 0.f;
+      const float inner = iw * ih;
+      float ov = inner / (((garea + a.area) - inner) + kIouEps);
+      if (gzero) ov = 0.f;
+      if (a.zero) ov = -1.f;
+      return ov;
+    };
+    ovA = one(aA);
+    ovB = one(aB);
+  };
+  int nslot = 0;
+  auto flush_keys = [&]() {
+    if (nslot == 0) return;
+    __builtin_amdgcn_wave_barrier();
+    const int j = lane >> 2, q = lane & 3;   // row j, 32-prior segment q
+    unsigned long long key = 0ull;
+    if (j < nslot) {
+      const uint4 *row = reinterpret_cast<const uint4 *>(&s_od[j][32 * q]);
+      uint32_t v[32];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint4 x = row[r];
+        v[4 * r] = x.x;
+        v[4 * r + 1] = x.y;
+        v[4 * r + 2] = x.z;
+        v[4 * r + 3] = x.w;
+      }
+      uint32_t mx = v[0];
+#pragma unroll
+      for (int c = 1; c < 32; ++c) mx = max(mx, v[c]);
+      int c0 = 31;
+#pragma unroll
+      for (int c = 30; c >= 0; --c) c0 = v[c] == mx ? c : c0;
+      key = mx ? ((static_cast<unsigned long long>(mx) << 32) |
+                  (0xffffffffull - static_cast<uint32_t>(wbase + 32 * q + c0)))
+               : 0ull;
+    }
+    key = quad_max_u64(key);
+    if (q == 0 && j < nslot && key)
+      __hip_atomic_fetch_max(brow + s_slot[j], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_wave_barrier();
+    nslot = 0;
+  };
+  auto note_key = [&](int g, float ovA, float ovB) {
+    const uint32_t odA = (validA && ovA > 0.f) ? f2ord(ovA) : 0u;
+    const uint32_t odB = (validB && ovB > 0.f) ? f2ord(ovB) : 0u;
+    if (__ballot((odA | odB) != 0u) == 0ull) return;
+    s_od[nslot][lane] = odA;
+    s_od[nslot][64 + lane] = odB;
+    if (lane == 0) s_slot[nslot] = g;
+    if (++nslot == kSlots) flush_keys();
+  };
+  for (int gc = 0; gc < G; gc += 64) {
+    const int gn = min(G - gc, 64);
+    if (gc > 0) o = load_gt_lane<kFlags>(gt, labels, g0, gc, gn, lane);
+    const bool hit = wlive && lane < gn && f2ord(o.x2) > wx1 && f2ord(o.x1) < wx2 && f2ord(o.y2) > wy1 &&
+                     f2ord(o.y1) < wy2;
+    unsigned long long todo = __ballot(hit) | (gc == 0 ? 1ull : 0ull);
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1ull;
+      int lab;
+      float ovA, ovB;
+      iou2(j, lab, ovA, ovB);
+      if (gc + j == 0 || ovA > bestA) {
+        bestA = ovA;
+        biA = gc + j;
+        blabA = lab;
+      }
+      if (gc + j == 0 || ovB > bestB) {
+        bestB = ovB;
+        biB = gc + j;
+        blabB = lab;
+      }
+      note_key(gc + j, ovA, ovB);
+    }
+  }
+  flush_keys();
+  ra = MatchLane{pA, biA, blabA, bestA, validA, eA0, eA1};
+  rb = MatchLane{pB, biB, blabB, bestB, validB, eB0, eB1};
+}
+#endif
 
 // The positive rule of the criteria before the forced match (label of the best object, overlap
 // threshold; ODM: easy negatives excluded, RefineDet512.py:894-899).
