@@ -13,6 +13,7 @@ both ~ max of the two, one chain sets the step.
     python scripts/gpu_interval.py [--n1 10] [--n2 40] [--reps 3] [--crit-streams 2] [--det-streams 2]
                                    [--batches 6] [--det-form two|one] [--finish separate|fused]
                                    [--crit-cu-reserve K [--mask spread|block]] [--shared-streams]
+                                   [--detect-offset K]   (step k's detect on batch k + K)
                                    (GPU_MAX_HW_QUEUES from the environment)
 """
 import json
@@ -88,6 +89,8 @@ def main():
     torch.cuda.synchronize()
     per_ms = 1_000_000 / max(e0.elapsed_time(e1), 1e-3)
 
+    doff = arg('--detect-offset', 0)   # > 0: each step's detect reads another resident batch
+
     def timed(n, parts, gate_ms):
         ev = torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(gate):
@@ -99,7 +102,13 @@ def main():
         for _ in range(n):
             i = st.k % len(st.slots)
             bt = st._next_batch()
-            r = L.host_ext.submit_step_program(st.programs[i], bt.boxes, bt.labels, parts)
+            if doff and parts == 3:   # the criterion on batch i, the detect on batch i + doff
+                r = L.host_ext.submit_step_program(st.programs[i], bt.boxes, bt.labels, 1)
+                if r is True:
+                    j = (i + doff) % len(st.slots)
+                    r = L.host_ext.submit_step_program(st.programs[j], st.batches[j].boxes, st.batches[j].labels, 2)
+            else:
+                r = L.host_ext.submit_step_program(st.programs[i], bt.boxes, bt.labels, parts)
             if r is not True:
                 raise RuntimeError('submit failed: %r' % (r,))
         host_ms = (time.perf_counter() - t0) * 1e3
@@ -116,7 +125,8 @@ def main():
            'batches': len(st.batches), 'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'),
            'det_streams': len(st.det_streams), 'det_form': arg('--det-form', 'two'),
            'finish': arg('--finish', 'separate'), 'crit_cu_reserve': arg('--crit-cu-reserve', 0),
-           'mask': arg('--mask', 'spread'), 'shared_streams': '--shared-streams' in sys.argv, 'modes': {}}
+           'mask': arg('--mask', 'spread'), 'shared_streams': '--shared-streams' in sys.argv,
+           'detect_offset': arg('--detect-offset', 0), 'modes': {}}
     names = {3: 'both', 1: 'criterion', 2: 'detect'}
     for rep in range(reps):
         for parts in (3, 1, 2):
@@ -134,7 +144,8 @@ def main():
                       'det_streams': out['det_streams'], 'batches': out['batches'],
                       'hw_queues': out['hw_queues'], 'det_form': out['det_form'],
                       'finish': out['finish'], 'crit_cu_reserve': out['crit_cu_reserve'],
-                      'mask': out['mask'], 'shared_streams': out['shared_streams']}), flush=True)
+                      'mask': out['mask'], 'shared_streams': out['shared_streams'],
+                      'detect_offset': out['detect_offset']}), flush=True)
 
 
 if __name__ == '__main__':
