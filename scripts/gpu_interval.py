@@ -14,6 +14,7 @@ both ~ max of the two, one chain sets the step.
                                    [--batches 6] [--det-form two|one] [--finish separate|fused]
                                    [--crit-cu-reserve K [--mask spread|block]] [--shared-streams]
                                    [--detect-offset K]   (step k's detect on batch k + K)
+                                   [--null-kernels N [--null-blocks M]]   (N empty kernels per step stream)
                                    (GPU_MAX_HW_QUEUES from the environment)
 """
 import json
@@ -90,6 +91,7 @@ def main():
     per_ms = 1_000_000 / max(e0.elapsed_time(e1), 1e-3)
 
     doff = arg('--detect-offset', 0)   # > 0: each step's detect reads another resident batch
+    nnull, nblocks = arg('--null-kernels', 0), arg('--null-blocks', 1)
 
     def timed(n, parts, gate_ms):
         ev = torch.cuda.Event(enable_timing=True)
@@ -111,6 +113,10 @@ def main():
                 r = L.host_ext.submit_step_program(st.programs[i], bt.boxes, bt.labels, parts)
             if r is not True:
                 raise RuntimeError('submit failed: %r' % (r,))
+            for _ in range(nnull):   # empty kernels on the step's two streams (dispatch-floor probe)
+                for sx in (st.cs_of(i), st.ds_of(i)):
+                    if L.call('sbod_null_kernel', nblocks, sx.cuda_stream) != 0:
+                        raise RuntimeError('sbod_null_kernel failed')
         host_ms = (time.perf_counter() - t0) * 1e3
         ends = []
         for s in streams:
@@ -126,7 +132,8 @@ def main():
            'det_streams': len(st.det_streams), 'det_form': arg('--det-form', 'two'),
            'finish': arg('--finish', 'separate'), 'crit_cu_reserve': arg('--crit-cu-reserve', 0),
            'mask': arg('--mask', 'spread'), 'shared_streams': '--shared-streams' in sys.argv,
-           'detect_offset': arg('--detect-offset', 0), 'modes': {}}
+           'detect_offset': arg('--detect-offset', 0), 'null_kernels': arg('--null-kernels', 0),
+           'null_blocks': arg('--null-blocks', 1), 'modes': {}}
     names = {3: 'both', 1: 'criterion', 2: 'detect'}
     for rep in range(reps):
         for parts in (3, 1, 2):
@@ -145,7 +152,8 @@ def main():
                       'hw_queues': out['hw_queues'], 'det_form': out['det_form'],
                       'finish': out['finish'], 'crit_cu_reserve': out['crit_cu_reserve'],
                       'mask': out['mask'], 'shared_streams': out['shared_streams'],
-                      'detect_offset': out['detect_offset']}), flush=True)
+                      'detect_offset': out['detect_offset'], 'null_kernels': out['null_kernels'],
+                      'null_blocks': out['null_blocks']}), flush=True)
 
 
 if __name__ == '__main__':
